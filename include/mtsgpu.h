@@ -1,0 +1,198 @@
+/*
+ * mtsgpu.h -- C-ABI of the MI355X-native `path` integrator (libmtsgpu.so).
+ *
+ * This is the drop-in boundary for Mitsuba 0.6's unidirectional path tracer.
+ * The reference renders through the Integrator plugin API:
+ *
+ *   SamplingIntegrator::render      src/librender/integrator.cpp:95-129
+ *   SamplingIntegrator::renderBlock src/librender/integrator.cpp:140-188
+ *   MIPathTracer::Li                src/integrators/path/path.cpp:119-294
+ *
+ * and a plugin is loaded through `extern "C" CreateInstance/GetDescription`
+ * (include/mitsuba/core/cobject.h:99-107, src/libcore/plugin.cpp:62-123).
+ * A `gpupath` plugin shim overrides render() and calls
+ * the entry points below with plain pointers and sizes: no C++ or torch types
+ * cross this boundary, every call returns an int status, nothing throws.
+ *
+ * Ownership: the caller owns every host buffer; the library copies what it
+ * needs during mtsgpu_upload_scene.  One context per host thread.
+ *
+ * The scene description is the reference's scene *after plugin construction
+ * and before configure()*: world-space triangle meshes (the TriMesh the
+ * shape plugins produce), BSDF/emitter parameters, sensor, film and sampler
+ * properties.  Everything the reference derives in configure() (vertex
+ * normals, UV tangents, TriAccel, emitter CDFs, camera matrices, filter LUT)
+ * is derived by the library itself, following the cited reference code.
+ */
+#ifndef MTSGPU_H
+#define MTSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTSGPU_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+enum {
+    MTSGPU_OK = 0,
+    MTSGPU_EINVAL = -1,   /* bad argument / inconsistent scene (reference: Log(EError)) */
+    MTSGPU_EHIP = -2,     /* HIP runtime error                                      */
+    MTSGPU_ENOMEM = -3,   /* device or host allocation failed                        */
+    MTSGPU_ESTATE = -4,   /* call out of order (e.g. render before upload)           */
+    MTSGPU_EDIM = -5,     /* Sobol dimension table exhausted (sobol.cpp:224,238)     */
+    MTSGPU_ECANCEL = -6,  /* *cancel flag was set (Integrator::cancel)               */
+    MTSGPU_ENODEV = -7    /* no usable gfx950 device                                 */
+};
+
+/* ---- scene description (POD) ------------------------------------------- */
+enum { /* BSDF plugins on the path (src/bsdfs) */
+    MTSGPU_BSDF_DIFFUSE = 0,         /* diffuse.cpp         */
+    MTSGPU_BSDF_ROUGHCONDUCTOR = 1,  /* roughconductor.cpp  */
+    MTSGPU_BSDF_ROUGHDIELECTRIC = 2  /* roughdielectric.cpp */
+};
+
+enum { /* MicrofacetDistribution::EType (src/bsdfs/microfacet.h:48-57) */
+    MTSGPU_DISTR_BECKMANN = 0,
+    MTSGPU_DISTR_GGX = 1,
+    MTSGPU_DISTR_PHONG = 2
+};
+
+typedef struct {
+    int32_t type;                   /* MTSGPU_BSDF_*                               */
+    int32_t distribution;           /* MTSGPU_DISTR_* (rough BSDFs)                */
+    int32_t sample_visible;         /* 'sampleVisible' (default 1)                 */
+    int32_t ensure_energy_conservation; /* 'ensureEnergyConservation' (default 1)   */
+    float alpha_u, alpha_v;         /* 'alpha' / 'alphaU','alphaV' as given        */
+    float reflectance[3];           /* diffuse 'reflectance'                       */
+    float specular_reflectance[3];  /* rough*: 'specularReflectance' (default 1)   */
+    float specular_transmittance[3];/* roughdielectric (default 1)                 */
+    float eta[3], k[3];             /* roughconductor: RGB eta/k, before /extEta   */
+    float ext_eta;                  /* roughconductor 'extEta' (air = 1.000277)    */
+    float int_ior, ext_ior;         /* roughdielectric (bk7 = 1.5046, air)         */
+} mtsgpu_bsdf_desc;
+
+enum { MTSGPU_EMITTER_AREA = 0, MTSGPU_EMITTER_ENVMAP = 1 };
+
+typedef struct {
+    int32_t type;                   /* MTSGPU_EMITTER_*                            */
+    float radiance[3];              /* area.cpp 'radiance'                         */
+    float sampling_weight;          /* 'samplingWeight' (emitter.cpp:103)          */
+    /* envmap (envmap.cpp): linear RGB lat-long image, row-major, top row first  */
+    const float *env_rgb;           /* 3*env_width*env_height floats, or NULL      */
+    uint32_t env_width, env_height;
+    float env_scale;                /* 'scale'                                     */
+    float env_to_world[16];         /* row-major 4x4 'toWorld'                     */
+} mtsgpu_emitter_desc;
+
+typedef struct {
+    const float *positions;         /* 3*num_vertices, world space                 */
+    const float *normals;           /* 3*num_vertices or NULL                      */
+    const float *texcoords;         /* 2*num_vertices or NULL                      */
+    const uint32_t *indices;        /* 3*num_triangles                             */
+    uint32_t num_vertices, num_triangles;
+    int32_t bsdf;                   /* index into bsdfs, -1: Shape::configure default */
+    int32_t emitter;                /* index into emitters (area), -1: none        */
+    int32_t face_normals;           /* 'faceNormals'                               */
+    int32_t flip_normals;           /* 'flipNormals'                               */
+} mtsgpu_mesh_desc;
+
+enum { MTSGPU_FOV_X = 0, MTSGPU_FOV_Y = 1, MTSGPU_FOV_DIAGONAL = 2,
+       MTSGPU_FOV_SMALLER = 3, MTSGPU_FOV_LARGER = 4 };
+
+typedef struct {                    /* perspective.cpp + librender/sensor.cpp      */
+    float fov;                      /* degrees                                     */
+    int32_t fov_axis;               /* MTSGPU_FOV_*                                */
+    float near_clip, far_clip;      /* defaults 1e-2, 1e4                          */
+    float to_world[16];             /* row-major camera-to-world                   */
+    uint32_t film_width, film_height;
+} mtsgpu_sensor_desc;
+
+typedef struct {
+    const mtsgpu_mesh_desc *meshes;       uint32_t num_meshes;
+    const mtsgpu_bsdf_desc *bsdfs;        uint32_t num_bsdfs;
+    const mtsgpu_emitter_desc *emitters;  uint32_t num_emitters; /* scene order */
+    mtsgpu_sensor_desc sensor;
+} mtsgpu_scene_desc;
+
+/* ---- render parameters ------------------------------------------------- */
+enum { MTSGPU_RFILTER_BOX = 0, MTSGPU_RFILTER_GAUSSIAN = 1 };
+
+typedef struct {
+    uint32_t spp;                   /* sampler 'sampleCount'                       */
+    uint64_t scramble;              /* sobol 'scramble' (0: none)                  */
+    int32_t max_depth;              /* 'maxDepth' (-1 = infinite)                  */
+    int32_t rr_depth;               /* 'rrDepth' (5)                               */
+    int32_t strict_normals;         /* 'strictNormals'                             */
+    int32_t hide_emitters;          /* 'hideEmitters'                              */
+    int32_t has_alpha;              /* film has an alpha channel (EOpacity)        */
+    int32_t rfilter;                /* MTSGPU_RFILTER_*                            */
+    float rfilter_param;            /* box: radius (0.5); gaussian: stddev (0.5)   */
+    /* pixel window rendered by this call (image coordinates, crop = film) */
+    uint32_t x0, y0, width, height;
+    /* row interleave for tile sharding: render rows y with
+       ((y - y0) / row_block) % row_stride == row_phase (stride 1 = all rows) */
+    uint32_t row_block, row_stride, row_phase;
+    const volatile int32_t *cancel; /* polled between launches, may be NULL        */
+    uint32_t flags;                 /* MTSGPU_FLAG_*                               */
+} mtsgpu_render_params;
+
+/* render flags */
+#define MTSGPU_FLAG_TRAVERSAL_STATS 1u  /* count BVH node visits / TriAccel tests   */
+
+/* Film layout produced by mtsgpu_render: an ImageBlock of the full crop
+ * (film_width+2b) x (film_height+2b) pixels, 5 floats each {R,G,B,alpha,w},
+ * b = reconstruction-filter border (rfilter.cpp:50).  The buffer is
+ * overwritten (zeroed first).  Summing the films of disjoint windows gives
+ * the film of the union (the multi-GPU reduction). */
+
+/* Optional per-sample record (parity / debugging), one per (pixel, sample) of
+ * the window in row-major pixel order, sample-minor:
+ * {Li.r, Li.g, Li.b, alpha, samplePos.x, samplePos.y, depth, flags}. */
+#define MTSGPU_SAMPLE_RECORD_FLOATS 8
+
+typedef struct {
+    uint64_t samples;               /* Li() evaluations                            */
+    uint64_t rays;                  /* closest-hit rays traced                     */
+    uint64_t shadow_rays;           /* shadow rays traced                          */
+    uint64_t path_length_sum;       /* sum of rRec.depth at exit (path.cpp:290)    */
+    uint64_t node_visits;           /* BVH nodes visited (stats builds)            */
+    uint64_t tri_tests;             /* TriAccel tests (stats builds)               */
+    double kernel_ms;               /* device time of the render launches          */
+} mtsgpu_stats;
+
+typedef struct mtsgpu_ctx mtsgpu_ctx;
+
+/* Create a context on HIP device `device` (-1: current). */
+int mtsgpu_create(int device, mtsgpu_ctx **out);
+/* Configure + upload a scene (copies everything; replaces any previous one). */
+int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene);
+/* Border size b of the film for the given filter parameters. */
+int mtsgpu_film_border(int32_t rfilter, float rfilter_param);
+/* Render the window into `film` (host memory, layout above).  `samples` may be
+ * NULL; otherwise it receives width*height*spp records.  Blocking. */
+int mtsgpu_render(mtsgpu_ctx *ctx, const mtsgpu_render_params *params,
+                  float *film, float *samples, mtsgpu_stats *stats);
+/* Same, but `film` is a device pointer (HBM-resident, no PCIe copy); used by
+ * the multi-GPU path to reduce films over RCCL.  `stream` is a hipStream_t
+ * (NULL: the context's stream); the call returns after the work is enqueued
+ * and the stream has been synchronised. */
+int mtsgpu_render_device(mtsgpu_ctx *ctx, const mtsgpu_render_params *params,
+                         float *film_device, void *stream, mtsgpu_stats *stats);
+/* Diagnostics (tests): device arithmetic probe -- for each i, out[8i..8i+7] =
+ * {a/b, sqrt|a|, sin a, cos a, acos(clamp a), atan2(a,b), exp(-|a|), a*b+a}
+ * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */
+int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *out, int n);
+int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4);
+/* Last error message of this context (or of the last failed create). */
+const char *mtsgpu_last_error(mtsgpu_ctx *ctx);
+void mtsgpu_destroy(mtsgpu_ctx *ctx);
+int mtsgpu_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTSGPU_H */

@@ -1,0 +1,92 @@
+"""ctypes mirror of include/mtsgpu.h (the C-ABI of libmtsgpu.so).
+
+Plain data layouts only: the structs below are what a Mitsuba-side caller
+hands across the boundary.  Keep in sync with include/mtsgpu.h.
+"""
+import ctypes as C
+
+import numpy as np
+
+OK, EINVAL, EHIP, ENOMEM, ESTATE, EDIM, ECANCEL, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
+STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTATE: 'ESTATE',
+                EDIM: 'EDIM', ECANCEL: 'ECANCEL', ENODEV: 'ENODEV'}
+
+BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC = 0, 1, 2
+DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
+EMITTER_AREA, EMITTER_ENVMAP = 0, 1
+FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
+RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
+SAMPLE_RECORD_FLOATS = 8
+
+_f3 = C.c_float * 3
+_f16 = C.c_float * 16
+
+
+class BsdfDesc(C.Structure):
+    _fields_ = [('type', C.c_int32), ('distribution', C.c_int32), ('sample_visible', C.c_int32),
+                ('ensure_energy_conservation', C.c_int32),
+                ('alpha_u', C.c_float), ('alpha_v', C.c_float),
+                ('reflectance', _f3), ('specular_reflectance', _f3), ('specular_transmittance', _f3),
+                ('eta', _f3), ('k', _f3), ('ext_eta', C.c_float),
+                ('int_ior', C.c_float), ('ext_ior', C.c_float)]
+
+
+class EmitterDesc(C.Structure):
+    _fields_ = [('type', C.c_int32), ('radiance', _f3), ('sampling_weight', C.c_float),
+                ('env_rgb', C.POINTER(C.c_float)), ('env_width', C.c_uint32), ('env_height', C.c_uint32),
+                ('env_scale', C.c_float), ('env_to_world', _f16)]
+
+
+class MeshDesc(C.Structure):
+    _fields_ = [('positions', C.POINTER(C.c_float)), ('normals', C.POINTER(C.c_float)),
+                ('texcoords', C.POINTER(C.c_float)), ('indices', C.POINTER(C.c_uint32)),
+                ('num_vertices', C.c_uint32), ('num_triangles', C.c_uint32),
+                ('bsdf', C.c_int32), ('emitter', C.c_int32),
+                ('face_normals', C.c_int32), ('flip_normals', C.c_int32)]
+
+
+class SensorDesc(C.Structure):
+    _fields_ = [('fov', C.c_float), ('fov_axis', C.c_int32), ('near_clip', C.c_float),
+                ('far_clip', C.c_float), ('to_world', _f16),
+                ('film_width', C.c_uint32), ('film_height', C.c_uint32)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [('meshes', C.POINTER(MeshDesc)), ('num_meshes', C.c_uint32),
+                ('bsdfs', C.POINTER(BsdfDesc)), ('num_bsdfs', C.c_uint32),
+                ('emitters', C.POINTER(EmitterDesc)), ('num_emitters', C.c_uint32),
+                ('sensor', SensorDesc)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [('spp', C.c_uint32), ('scramble', C.c_uint64), ('max_depth', C.c_int32),
+                ('rr_depth', C.c_int32), ('strict_normals', C.c_int32), ('hide_emitters', C.c_int32),
+                ('has_alpha', C.c_int32), ('rfilter', C.c_int32), ('rfilter_param', C.c_float),
+                ('x0', C.c_uint32), ('y0', C.c_uint32), ('width', C.c_uint32), ('height', C.c_uint32),
+                ('row_block', C.c_uint32), ('row_stride', C.c_uint32), ('row_phase', C.c_uint32),
+                ('cancel', C.POINTER(C.c_int32)), ('flags', C.c_uint32)]
+
+
+FLAG_TRAVERSAL_STATS = 1
+
+
+class Stats(C.Structure):
+    _fields_ = [('samples', C.c_uint64), ('rays', C.c_uint64), ('shadow_rays', C.c_uint64),
+                ('path_length_sum', C.c_uint64), ('node_visits', C.c_uint64),
+                ('tri_tests', C.c_uint64), ('kernel_ms', C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+def fptr(a):
+    """float32 C-contiguous numpy array -> POINTER(c_float) (None passes NULL)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def uptr(a):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))

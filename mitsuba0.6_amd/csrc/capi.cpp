@@ -1,0 +1,340 @@
+// capi.cpp -- the C-ABI of libmtsgpu.so (include/mtsgpu.h).
+//
+// Replaces, for the `path` integrator, SamplingIntegrator::render ->
+// BlockedRenderProcess -> BlockRenderer::process -> renderBlock
+// (src/librender/integrator.cpp:95-188, renderproc.cpp:68-149): one call
+// renders a pixel window with a persistent kernel and returns the ImageBlock
+// (full crop + filter border) that Film::put would have accumulated.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mtsgpu.h"
+#include "layout.h"
+#include "scene_build.h"
+
+hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
+hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
+hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
+int mtsg_path_kernel_occupancy(int *blocksPerCU);
+
+namespace {
+
+thread_local std::string g_create_error;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, std::max<size_t>(n, 16));
+        if (e == hipSuccess) bytes = std::max<size_t>(n, 16);
+        return e;
+    }
+};
+
+}  // namespace
+
+struct mtsgpu_ctx {
+    int device = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string err;
+    bool have_scene = false;
+    HostScene host;
+    MtsgDeviceScene dscene;
+    DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
+    DevBuf film_own, film_spill, samples, counters;
+};
+
+namespace {
+
+int fail(mtsgpu_ctx *ctx, int code, const std::string &msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int hip_fail(mtsgpu_ctx *ctx, hipError_t e, const char *what) {
+    return fail(ctx, e == hipErrorOutOfMemory ? MTSGPU_ENOMEM : MTSGPU_EHIP,
+                std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+hipError_t upload(DevBuf &b, const std::vector<T> &v, hipStream_t s) {
+    hipError_t e = b.ensure(v.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    if (v.empty()) return hipSuccess;
+    return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtsgpu_abi_version(void) { return MTSGPU_ABI_VERSION; }
+
+int mtsgpu_create(int device, mtsgpu_ctx **out) {
+    if (!out) return MTSGPU_EINVAL;
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) {
+        g_create_error = std::string("no HIP device: ") + hipGetErrorString(e);
+        return MTSGPU_ENODEV;
+    }
+    if (device < 0) {
+        e = hipGetDevice(&device);
+        if (e != hipSuccess) device = 0;
+    }
+    if (device >= count) { g_create_error = "device index out of range"; return MTSGPU_ENODEV; }
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) {
+        g_create_error = std::string("hipGetDeviceProperties: ") + hipGetErrorString(e);
+        return MTSGPU_EHIP;
+    }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_create_error = std::string("libmtsgpu.so is built for gfx950, device is ") + prop.gcnArchName;
+        return MTSGPU_ENODEV;
+    }
+    mtsgpu_ctx *ctx = new mtsgpu_ctx();
+    ctx->device = device;
+    ctx->num_cus = prop.multiProcessorCount;
+    if ((e = hipSetDevice(device)) != hipSuccess || (e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreate(&ctx->ev0)) != hipSuccess || (e = hipEventCreate(&ctx->ev1)) != hipSuccess) {
+        g_create_error = std::string("HIP init: ") + hipGetErrorString(e);
+        delete ctx;
+        return MTSGPU_EHIP;
+    }
+    *out = ctx;
+    return MTSGPU_OK;
+}
+
+int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
+    if (!ctx || !scene) return MTSGPU_EINVAL;
+    ctx->have_scene = false;
+    std::string err;
+    int rc = mtsg_configure_scene(scene, ctx->host, err);
+    if (rc) return fail(ctx, rc, err);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    HostScene &H = ctx->host;
+    hipStream_t s = ctx->stream;
+    if ((e = upload(ctx->nodes, H.nodes, s)) != hipSuccess || (e = upload(ctx->tris, H.tris, s)) != hipSuccess ||
+        (e = upload(ctx->prim_vtx, H.prim_vtx, s)) != hipSuccess || (e = upload(ctx->dpdu, H.dpdu, s)) != hipSuccess ||
+        (e = upload(ctx->positions, H.positions, s)) != hipSuccess || (e = upload(ctx->normals, H.normals, s)) != hipSuccess ||
+        (e = upload(ctx->shapes, H.shapes, s)) != hipSuccess || (e = upload(ctx->bsdfs, H.bsdfs, s)) != hipSuccess ||
+        (e = upload(ctx->emitters, H.emitters, s)) != hipSuccess || (e = upload(ctx->area_cdf, H.area_cdf, s)) != hipSuccess ||
+        (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, mtsg_sobol_matrices(), s)) != hipSuccess)
+        return hip_fail(ctx, e, "scene upload");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "scene upload sync");
+    MtsgDeviceScene &D = ctx->dscene;
+    std::memset(&D, 0, sizeof D);
+    D.nodes = (const MtsgNode *)ctx->nodes.p;
+    D.tris = (const MtsgTri *)ctx->tris.p;
+    D.prim_vtx = (const uint32_t *)ctx->prim_vtx.p;
+    D.dpdu = (const float *)ctx->dpdu.p;
+    D.positions = (const float *)ctx->positions.p;
+    D.normals = (const float *)ctx->normals.p;
+    D.shapes = (const MtsgShape *)ctx->shapes.p;
+    D.bsdfs = (const MtsgBsdf *)ctx->bsdfs.p;
+    D.emitters = (const MtsgEmitter *)ctx->emitters.p;
+    D.area_cdf = (const float *)ctx->area_cdf.p;
+    D.em_cdf = (const float *)ctx->em_cdf.p;
+    D.sobol = (const uint32_t *)ctx->sobol.p;
+    D.num_emitters = (uint32_t)H.emitters.size();
+    D.num_prims = (uint32_t)H.tris.size();
+    D.em_norm = H.em_norm;
+    for (int a = 0; a < 3; ++a) { D.aabb_min[a] = H.aabb_min[a]; D.aabb_max[a] = H.aabb_max[a]; }
+    D.cam = H.cam;
+    ctx->have_scene = true;
+    return MTSGPU_OK;
+}
+
+int mtsgpu_film_border(int32_t rfilter, float rfilter_param) {
+    MtsgFilter f;
+    std::string err;
+    if (mtsg_configure_filter(rfilter, rfilter_param, f, err)) return MTSGPU_EINVAL;
+    return f.border;
+}
+
+static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *film_host, float *film_dev,
+                       float *samples_host, hipStream_t stream, mtsgpu_stats *stats) {
+    if (!ctx || !P) return MTSGPU_EINVAL;
+    if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "render called before a successful upload_scene");
+    if (P->spp == 0) return fail(ctx, MTSGPU_EINVAL, "sampleCount must be positive");
+    if (P->rr_depth <= 0) return fail(ctx, MTSGPU_EINVAL, "'rrDepth' must be set to a value greater than zero!");
+    if (P->max_depth <= 0 && P->max_depth != -1)
+        return fail(ctx, MTSGPU_EINVAL, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
+    const HostScene &H = ctx->host;
+    if ((uint64_t)P->x0 + P->width > H.film_w || (uint64_t)P->y0 + P->height > H.film_h)
+        return fail(ctx, MTSGPU_EINVAL, "render window exceeds the film");
+    if (P->cancel && *P->cancel) return fail(ctx, MTSGPU_ECANCEL, "cancelled");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    if (!stream) stream = ctx->stream;
+
+    MtsgLaunch L;
+    std::memset(&L, 0, sizeof L);
+    L.scene = ctx->dscene;
+    std::string err;
+    if (mtsg_configure_filter(P->rfilter, P->rfilter_param, L.filter, err)) return fail(ctx, MTSGPU_EINVAL, err);
+    // SobolSampler::setFilmResolution(cropSize, bucketed = true) (sobol.cpp:147-158)
+    const uint32_t mx = std::max(H.film_w, H.film_h);
+    uint32_t r = mx - 1;
+    r |= r >> 1; r |= r >> 2; r |= r >> 4; r |= r >> 8; r |= r >> 16; r += 1;
+    uint32_t m = 0;
+    while ((1u << m) < r) ++m;
+    L.resolution = (float)r;
+    mtsg_sobol_lookup_table(m, L.lut);
+    uint64_t scr = P->scramble;
+    if (scr) scr = mtsg_sample_tea((uint32_t)scr, (uint32_t)(scr >> 32), 4);   // sobol.cpp:93-101
+    L.scramble = (uint32_t)scr;
+    L.scramble64 = scr;
+    L.spp = P->spp;
+    L.max_depth = P->max_depth;
+    L.rr_depth = P->rr_depth;
+    L.strict_normals = P->strict_normals;
+    L.hide_emitters = P->hide_emitters;
+    L.has_alpha = P->has_alpha;
+    L.film_w = (int)H.film_w;
+    L.film_h = (int)H.film_h;
+    L.fw = (int)H.film_w + 2 * L.filter.border;
+    L.fh = (int)H.film_h + 2 * L.filter.border;
+    L.x0 = P->x0; L.y0 = P->y0; L.width = P->width; L.height = P->height;
+    L.row_block = P->row_block ? P->row_block : 1;
+    L.row_stride = P->row_stride ? P->row_stride : 1;
+    L.row_phase = P->row_phase % L.row_stride;
+    // active rows of the window under the interleave
+    uint32_t active = 0;
+    for (uint32_t y = 0; y < P->height; ++y)
+        if ((y / L.row_block) % L.row_stride == L.row_phase) ++active;
+    // tasks enumerate rows compacted over the interleave; map r -> y in the kernel
+    const uint32_t rowsCompact = ((P->height + L.row_block - 1) / L.row_block + L.row_stride - 1) / L.row_stride * L.row_block;
+    const uint32_t tilesX = (P->width + 7) / 8, tilesY = (rowsCompact + 7) / 8;
+    L.num_tasks = tilesX * tilesY * 64;
+    (void)active;
+
+    const size_t filmFloats = (size_t)L.fw * L.fh * 5;
+    if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||
+        (e = ctx->counters.ensure(16 * 8)) != hipSuccess)
+        return hip_fail(ctx, e, "film allocation");
+    float *own = film_dev ? film_dev : (float *)ctx->film_own.p;
+    const size_t nsamp = samples_host ? (size_t)P->width * P->height * P->spp * MTSGPU_SAMPLE_RECORD_FLOATS : 0;
+    if (nsamp) {
+        if ((e = ctx->samples.ensure(nsamp * 4)) != hipSuccess) return hip_fail(ctx, e, "sample buffer");
+        if ((e = hipMemsetAsync(ctx->samples.p, 0, nsamp * 4, stream)) != hipSuccess) return hip_fail(ctx, e, "memset");
+    }
+    if ((e = hipMemsetAsync(own, 0, filmFloats * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->film_spill.p, 0, filmFloats * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->counters.p, 0, 16 * 8, stream)) != hipSuccess)
+        return hip_fail(ctx, e, "memset");
+    L.film_own = own;
+    L.film_spill = (float *)ctx->film_spill.p;
+    L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
+    unsigned long long *cnt = (unsigned long long *)ctx->counters.p;
+    L.counters = cnt;
+    L.task_counter = (uint32_t *)(cnt + 8);
+
+    int bpc = 0;
+    mtsg_path_kernel_occupancy(&bpc);
+    if (bpc <= 0) bpc = 1;
+    int grid = ctx->num_cus * bpc;
+    const uint64_t lanesNeeded = (uint64_t)L.num_tasks;
+    const int maxGrid = (int)std::max<uint64_t>(1, (lanesNeeded + 255) / 256);
+    grid = std::min(grid, maxGrid);
+    const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
+    if ((e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
+    if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
+    if ((e = hipEventRecord(ctx->ev1, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
+    if ((e = mtsg_launch_finalize(own, L.film_spill, filmFloats, stream)) != hipSuccess) return hip_fail(ctx, e, "finalize launch");
+    unsigned long long hc[16];
+    if ((e = hipMemcpyAsync(hc, cnt, sizeof hc, hipMemcpyDeviceToHost, stream)) != hipSuccess) return hip_fail(ctx, e, "counters");
+    if (film_host && (e = hipMemcpyAsync(film_host, own, filmFloats * 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hip_fail(ctx, e, "film copy");
+    if (nsamp && (e = hipMemcpyAsync(samples_host, ctx->samples.p, nsamp * 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hip_fail(ctx, e, "sample copy");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel");
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    if (stats) {
+        stats->samples = hc[0];
+        stats->rays = hc[1];
+        stats->shadow_rays = hc[2];
+        stats->path_length_sum = hc[3];
+        stats->node_visits = stats_mode ? hc[4] : 0;
+        stats->tri_tests = stats_mode ? hc[5] : 0;
+        stats->kernel_ms = ms;
+    }
+    if (hc[6]) return fail(ctx, MTSGPU_EDIM, "Lookup dimension exceeds the direction number table size! You may have to "
+                                             "reduce the 'maxDepth' parameter of your integrator.");
+    if (P->cancel && *P->cancel) return fail(ctx, MTSGPU_ECANCEL, "cancelled");
+    return MTSGPU_OK;
+}
+
+int mtsgpu_render(mtsgpu_ctx *ctx, const mtsgpu_render_params *params, float *film, float *samples, mtsgpu_stats *stats) {
+    if (!film) return fail(ctx, MTSGPU_EINVAL, "film buffer is NULL");
+    return render_impl(ctx, params, film, nullptr, samples, nullptr, stats);
+}
+
+int mtsgpu_render_device(mtsgpu_ctx *ctx, const mtsgpu_render_params *params, float *film_device, void *stream,
+                         mtsgpu_stats *stats) {
+    if (!film_device) return fail(ctx, MTSGPU_EINVAL, "film buffer is NULL");
+    return render_impl(ctx, params, nullptr, film_device, nullptr, (hipStream_t)stream, stats);
+}
+
+const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
+
+void mtsgpu_destroy(mtsgpu_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+                      &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
+                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters};
+    for (DevBuf *b : bufs) b->release();
+    if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+    if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+// diagnostics: device arithmetic probe (tests/test_gpu_arith.py)
+int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *out, int n) {
+    if (!ctx || n <= 0) return MTSGPU_EINVAL;
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&da, n * 4)) != hipSuccess || (e = hipMalloc(&db, n * 4)) != hipSuccess ||
+        (e = hipMalloc(&dout, (size_t)n * 32)) != hipSuccess)
+        return hip_fail(ctx, e, "malloc");
+    (void)hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice);
+    e = mtsg_launch_arith_probe(da, db, dout, n, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 32, hipMemcpyDeviceToHost);
+    (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
+    return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "arith probe");
+}
+
+// diagnostics: BVH statistics of the uploaded scene
+int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4) {
+    if (!ctx || !ctx->have_scene || !info4) return MTSGPU_EINVAL;
+    info4[0] = (uint32_t)ctx->host.nodes.size();
+    info4[1] = (uint32_t)ctx->host.tris.size();
+    info4[2] = ctx->host.bvh_depth;
+    info4[3] = (uint32_t)ctx->num_cus;
+    return MTSGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,496 @@
+// dbsdf.h -- device BSDFs of the path: diffuse, roughconductor, roughdielectric
+// and the MicrofacetDistribution they share (Beckmann, GGX, Phong/AS).
+//
+//   src/bsdfs/diffuse.cpp:110-150        src/bsdfs/microfacet.h:67-670
+//   src/bsdfs/roughconductor.cpp:257-410 src/bsdfs/roughdielectric.cpp:270-615
+//   src/libcore/util.cpp:651-771 (Fresnel, reflect, refract)
+//   src/libcore/math.cpp:25-95 (erf, erfinv, hypot2)
+#pragma once
+#include "dmath.h"
+#include "layout.h"
+
+enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
+enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2 };
+
+__device__ __forceinline__ float tan_theta(f3 v) {           // frame.h:117-122
+    float temp = 1 - v.z * v.z;
+    if (temp <= 0.0f) return 0.0f;
+    return dsqrt(temp) / v.z;
+}
+__device__ __forceinline__ float sin_theta2(f3 v) { return 1.0f - v.z * v.z; }
+
+// ---- warps (warp.cpp:43-102) --------------------------------------------
+__device__ __forceinline__ f3 square_to_cosine_hemisphere(float sx, float sy) {
+    float r1 = 2.0f * sx - 1.0f;
+    float r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) {
+        r = phi = 0;
+    } else if (r1 * r1 > r2 * r2) {
+        r = r1;
+        phi = (D_PI / 4.0f) * (r2 / r1);
+    } else {
+        r = r2;
+        phi = (D_PI / 2.0f) - (r1 / r2) * (D_PI / 4.0f);
+    }
+    float c, s;
+    d_sincos(phi, &s, &c);
+    float px = r * c, py = r * s;
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return mk(px, py, z);
+}
+
+// ---- math.cpp --------------------------------------------------------------
+__device__ __noinline__ float m_erfinv(float x) {
+    float w = -d_fastlog(((float)1 - x) * ((float)1 + x));
+    float p;
+    if (w < (float)5) {
+        w = w - (float)2.5;
+        p = (float)2.81022636e-08;
+        p = (float)3.43273939e-07 + p * w;
+        p = (float)-3.5233877e-06 + p * w;
+        p = (float)-4.39150654e-06 + p * w;
+        p = (float)0.00021858087 + p * w;
+        p = (float)-0.00125372503 + p * w;
+        p = (float)-0.00417768164 + p * w;
+        p = (float)0.246640727 + p * w;
+        p = (float)1.50140941 + p * w;
+    } else {
+        w = dsqrt(w) - (float)3;
+        p = (float)-0.000200214257;
+        p = (float)0.000100950558 + p * w;
+        p = (float)0.00134934322 + p * w;
+        p = (float)-0.00367342844 + p * w;
+        p = (float)0.00573950773 + p * w;
+        p = (float)-0.0076224613 + p * w;
+        p = (float)0.00943887047 + p * w;
+        p = (float)1.00167406 + p * w;
+        p = (float)2.83297682 + p * w;
+    }
+    return p * x;
+}
+__device__ __forceinline__ float m_erf(float x) {
+    float a1 = (float)0.254829592, a2 = (float)-0.284496736, a3 = (float)1.421413741;
+    float a4 = (float)-1.453152027, a5 = (float)1.061405429, p = (float)0.3275911;
+    float sign = signum(x);
+    x = fabsf(x);
+    float t = (float)1.0 / ((float)1.0 + p * x);
+    float y = (float)1.0 - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * d_fastexp(-x * x);
+    return sign * y;
+}
+__device__ __forceinline__ float m_hypot2(float a, float b) {
+    float r;
+    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * dsqrt(1.0f + r * r); }
+    else if (b != 0.0f) { r = a / b; r = fabsf(b) * dsqrt(1.0f + r * r); }
+    else r = 0.0f;
+    return r;
+}
+
+// ---- MicrofacetDistribution -----------------------------------------------
+struct Distr { int type; float alphaU, alphaV; int sampleVisible; float expU, expV; };
+
+__device__ __forceinline__ void distr_phong_exp(Distr &d) {      // microfacet.h:673-676
+    d.expU = smax(2.0f / (d.alphaU * d.alphaU) - 2.0f, 0.0f);
+    d.expV = smax(2.0f / (d.alphaV * d.alphaV) - 2.0f, 0.0f);
+}
+__device__ __forceinline__ Distr distr_make(int type, float au, float av, int sv) {  // :89-97
+    Distr d;
+    d.type = type; d.alphaU = smax(au, 1e-4f); d.alphaV = smax(av, 1e-4f);
+    d.sampleVisible = sv; d.expU = d.expV = 0.0f;
+    if (type == DISTR_PHONG) distr_phong_exp(d);
+    return d;
+}
+__device__ __forceinline__ bool distr_iso(const Distr &d) { return d.alphaU == d.alphaV; }
+
+__device__ __forceinline__ float distr_interp_phong(const Distr &d, f3 v) {   // :538-549
+    float st2 = sin_theta2(v);
+    if (distr_iso(d) || st2 <= 0x1p-128f) return d.expU;
+    float inv = 1 / st2;
+    return d.expU * (v.x * v.x * inv) + d.expV * (v.y * v.y * inv);
+}
+
+__device__ __noinline__ float distr_eval(const Distr &d, f3 m) {   // :191-238
+    if (m.z <= 0) return 0.0f;
+    float cosTheta2 = m.z * m.z;
+    float be = ((m.x * m.x) / (d.alphaU * d.alphaU) + (m.y * m.y) / (d.alphaV * d.alphaV)) / cosTheta2;
+    float result;
+    if (d.type == DISTR_BECKMANN) {
+        result = d_fastexp(-be) / (D_PI * d.alphaU * d.alphaV * cosTheta2 * cosTheta2);
+    } else if (d.type == DISTR_GGX) {
+        float root = ((float)1 + be) * cosTheta2;
+        result = (float)1 / (D_PI * d.alphaU * d.alphaV * root * root);
+    } else {
+        float exponent = distr_interp_phong(d, m);
+        result = dsqrt((d.expU + 2) * (d.expV + 2)) * D_INV_TWOPI * d_powf(m.z, exponent);
+    }
+    if (result * m.z < 1e-20f) result = 0;
+    return result;
+}
+
+__device__ __forceinline__ float distr_project_roughness(const Distr &d, f3 v) {   // :526-536
+    float invSinTheta2 = 1 / sin_theta2(v);
+    if (distr_iso(d) || invSinTheta2 <= 0) return d.alphaU;
+    float cosPhi2 = v.x * v.x * invSinTheta2;
+    float sinPhi2 = v.y * v.y * invSinTheta2;
+    return dsqrt(cosPhi2 * d.alphaU * d.alphaU + sinPhi2 * d.alphaV * d.alphaV);
+}
+
+__device__ __noinline__ float distr_smithG1(const Distr &d, f3 v, f3 m) {   // :477-518
+    if (dot(v, m) * v.z <= 0) return 0.0f;
+    float tanTheta = fabsf(tan_theta(v));
+    if (tanTheta == 0.0f) return 1.0f;
+    float alpha = distr_project_roughness(d, v);
+    if (d.type == DISTR_GGX) {
+        float root = alpha * tanTheta;
+        return 2.0f / (1.0f + m_hypot2((float)1.0f, root));
+    }
+    float a = 1.0f / (alpha * tanTheta);
+    if (a >= 1.6f) return 1.0f;
+    float aSqr = a * a;
+    return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+}
+
+__device__ __forceinline__ void distr_first_quadrant(const Distr &d, float u1, float &phi, float &exponent) {
+    float c, s;                                                           // :679-688
+    phi = d_atan(dsqrt((d.expU + 2.0f) / (d.expV + 2.0f)) * d_tan(D_PI * u1 * 0.5f));
+    d_sincos(phi, &s, &c);
+    exponent = d.expU * c * c + d.expV * s * s;
+}
+
+__device__ __noinline__ f3 distr_sample_all(const Distr &d, float sx, float sy, float &pdf) {  // :287-402
+    float cosThetaM = 0.0f, sinPhiM, cosPhiM, alphaSqr;
+    if (d.type != DISTR_PHONG) {
+        if (distr_iso(d)) {
+            d_sincos((2.0f * D_PI) * sy, &sinPhiM, &cosPhiM);
+            alphaSqr = d.alphaU * d.alphaU;
+        } else {
+            float phiM = d_atan(d.alphaV / d.alphaU * d_tan(D_PI + 2 * D_PI * sy)) + D_PI * floorf(2 * sy + 0.5f);
+            d_sincos(phiM, &sinPhiM, &cosPhiM);
+            float cosSc = cosPhiM / d.alphaU, sinSc = sinPhiM / d.alphaV;
+            alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
+        }
+        if (d.type == DISTR_BECKMANN) {
+            float tanThetaMSqr = alphaSqr * -d_fastlog(1.0f - sx);
+            cosThetaM = 1.0f / dsqrt(1.0f + tanThetaMSqr);
+            pdf = (1.0f - sx) / (D_PI * d.alphaU * d.alphaV * cosThetaM * cosThetaM * cosThetaM);
+        } else {
+            float tanThetaMSqr = alphaSqr * sx / (1.0f - sx);
+            cosThetaM = 1.0f / dsqrt(1.0f + tanThetaMSqr);
+            float temp = 1 + tanThetaMSqr / alphaSqr;
+            pdf = D_INV_PI / (d.alphaU * d.alphaV * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+        }
+    } else {
+        float phiM, exponent;
+        if (distr_iso(d)) {
+            phiM = (2.0f * D_PI) * sy;
+            exponent = d.expU;
+        } else {
+            if (sy < 0.25f) {
+                distr_first_quadrant(d, 4 * sy, phiM, exponent);
+            } else if (sy < 0.5f) {
+                distr_first_quadrant(d, 4 * (0.5f - sy), phiM, exponent);
+                phiM = D_PI - phiM;
+            } else if (sy < 0.75f) {
+                distr_first_quadrant(d, 4 * (sy - 0.5f), phiM, exponent);
+                phiM += D_PI;
+            } else {
+                distr_first_quadrant(d, 4 * (1 - sy), phiM, exponent);
+                phiM = 2 * D_PI - phiM;
+            }
+        }
+        d_sincos(phiM, &sinPhiM, &cosPhiM);
+        cosThetaM = d_powf(sx, 1.0f / (exponent + 2.0f));
+        pdf = dsqrt((d.expU + 2.0f) * (d.expV + 2.0f)) * D_INV_TWOPI * d_powf(cosThetaM, exponent + 1.0f);
+    }
+    if (pdf < 1e-20f) pdf = 0;
+    float sinThetaM = dsqrt(smax((float)0, 1 - cosThetaM * cosThetaM));
+    return mk(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+}
+
+__device__ __noinline__ void distr_sample_visible11(const Distr &d, float thetaI, float sx, float sy,
+                                                    float &slx, float &sly) {   // :573-670
+    const float SQRT_PI_INV = 1 / dsqrt(D_PI);
+    if (d.type == DISTR_BECKMANN) {
+        if (thetaI < 1e-4f) {
+            float s, c;
+            float r = dsqrt(-d_fastlog(1.0f - sx));
+            d_sincos(2 * D_PI * sy, &s, &c);
+            slx = r * c; sly = r * s;
+            return;
+        }
+        float tanThetaI = d_tan(thetaI);
+        float cotThetaI = 1 / tanThetaI;
+        float a = -1, c = m_erf(cotThetaI);
+        float sample_x = smax(sx, (float)1e-6f);
+        float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+        float b = c - (1 + c) * d_powf(1 - sample_x, fit);
+        float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * d_expf(-cotThetaI * cotThetaI));
+        int it = 0;
+        while (++it < 10) {
+            if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+            float invErf = m_erfinv(b);
+            float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * d_expf(-invErf * invErf)) - sample_x;
+            float derivative = normalization * (1 - invErf * tanThetaI);
+            if (fabsf(value) < 1e-5f) break;
+            if (value > 0) c = b; else a = b;
+            b -= value / derivative;
+        }
+        slx = m_erfinv(b);
+        sly = m_erfinv(2.0f * smax(sy, (float)1e-6f) - 1.0f);
+        return;
+    }
+    if (thetaI < 1e-4f) {                                                       // GGX
+        float s, c;
+        float r = safe_sqrt(sx / (1 - sx));
+        d_sincos(2 * D_PI * sy, &s, &c);
+        slx = r * c; sly = r * s;
+        return;
+    }
+    float tanThetaI = d_tan(thetaI);
+    float a = 1 / tanThetaI;
+    float G1 = 2.0f / (1.0f + safe_sqrt(1.0f + 1.0f / (a * a)));
+    float A = 2.0f * sx / G1 - 1.0f;
+    if (fabsf(A) == 1) A -= signum(A) * D_EPSILON;
+    float tmp = 1.0f / (A * A - 1.0f);
+    float B = tanThetaI;
+    float D = safe_sqrt(B * B * tmp * tmp - (A * A - B * B) * tmp);
+    float slope_x_1 = B * tmp - D;
+    float slope_x_2 = B * tmp + D;
+    slx = (A < 0.0f || slope_x_2 > 1.0f / tanThetaI) ? slope_x_1 : slope_x_2;
+    float S;
+    if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
+    else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
+    float z = (sy * (sy * (sy * (-(float)0.365728915865723) + (float)0.790235037209296) - (float)0.424965825137544) + (float)0.000152998850436920) /
+              (sy * (sy * (sy * (sy * (float)0.169507819808272 - (float)0.397203533833404) - (float)0.232500544458471) + (float)1) - (float)0.539825872510702);
+    sly = S * z * dsqrt(1.0f + slx * slx);
+}
+
+__device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float sx, float sy) {  // :421-460
+    f3 wi = normalize(mk(d.alphaU * _wi.x, d.alphaV * _wi.y, _wi.z));
+    float theta = 0, phi = 0;
+    if (wi.z < (float)0.99999) {
+        theta = d_acos(wi.z);
+        phi = d_atan2(wi.y, wi.x);
+    }
+    float sinPhi, cosPhi;
+    d_sincos(phi, &sinPhi, &cosPhi);
+    float slx, sly;
+    distr_sample_visible11(d, theta, sx, sy, slx, sly);
+    float nx = cosPhi * slx - sinPhi * sly;
+    float ny = sinPhi * slx + cosPhi * sly;
+    nx *= d.alphaU;
+    ny *= d.alphaV;
+    float normalization = (float)1 / dsqrt(nx * nx + ny * ny + (float)1.0);
+    return mk(-nx * normalization, -ny * normalization, normalization);
+}
+
+__device__ __forceinline__ float distr_pdf_visible(const Distr &d, f3 wi, f3 m) {   // :462-466
+    if (wi.z == 0) return 0.0f;
+    return distr_smithG1(d, wi, m) * absdot(wi, m) * distr_eval(d, m) / fabsf(wi.z);
+}
+__device__ __forceinline__ float distr_pdf(const Distr &d, f3 wi, f3 m) {           // :270-276
+    if (d.sampleVisible) return distr_pdf_visible(d, wi, m);
+    return distr_eval(d, m) * m.z;
+}
+__device__ __forceinline__ f3 distr_sample(const Distr &d, f3 wi, float sx, float sy, float &pdf) {
+    if (d.sampleVisible) {                                                          // :243-253
+        f3 m = distr_sample_visible(d, wi, sx, sy);
+        pdf = distr_pdf_visible(d, wi, m);
+        return m;
+    }
+    return distr_sample_all(d, sx, sy, pdf);
+}
+__device__ __forceinline__ void distr_scale_alpha(Distr &d, float v) {              // :181-186
+    d.alphaU *= v; d.alphaV *= v;
+    if (d.type == DISTR_PHONG) distr_phong_exp(d);
+}
+
+// ---- Fresnel (util.cpp) -------------------------------------------------
+__device__ __forceinline__ float fresnel_dielectric_ext(float cosThetaI_, float &cosThetaT_, float eta) {
+    if (eta == 1) { cosThetaT_ = -cosThetaI_; return 0.0f; }
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta,
+          cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) { cosThetaT_ = 0.0f; return 1.0f; }
+    float cosThetaI = fabsf(cosThetaI_);
+    float cosThetaT = dsqrt(cosThetaTSqr);
+    float Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    float Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    cosThetaT_ = (cosThetaI_ > 0) ? -cosThetaT : cosThetaT;
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+__device__ __forceinline__ f3 s_safe_sqrt(f3 a) { return mk(safe_sqrt(a.x), safe_sqrt(a.y), safe_sqrt(a.z)); }
+__device__ __noinline__ f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {   // util.cpp:739-761
+    float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
+    f3 temp1 = sub(sub(mulv(eta, eta), mulv(k, k)), mk(sinThetaI2, sinThetaI2, sinThetaI2));
+    f3 a2pb2 = s_safe_sqrt(add(mulv(temp1, temp1), mul(mulv(mulv(mulv(k, k), eta), eta), 4)));
+    f3 a = s_safe_sqrt(mul(add(a2pb2, temp1), 0.5f));
+    f3 term1 = add(a2pb2, mk(cosThetaI2, cosThetaI2, cosThetaI2));
+    f3 term2 = mul(a, 2 * cosThetaI);
+    f3 Rs2 = divv(sub(term1, term2), add(term1, term2));
+    f3 term3 = add(mul(a2pb2, cosThetaI2), mk(sinThetaI4, sinThetaI4, sinThetaI4));
+    f3 term4 = mul(term2, sinThetaI2);
+    f3 Rp2 = divv(mulv(Rs2, sub(term3, term4)), add(term3, term4));
+    return mul(add(Rp2, Rs2), 0.5f);
+}
+__device__ __forceinline__ f3 reflect_v(f3 wi, f3 n) { return sub(mul(n, 2 * dot(wi, n)), wi); }
+__device__ __forceinline__ f3 refract_v(f3 wi, f3 n, float eta, float cosThetaT) {
+    if (cosThetaT < 0) eta = 1 / eta;
+    return sub(mul(n, dot(wi, n) * eta + cosThetaT), mul(wi, eta));
+}
+
+__device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+
+// ---- BSDF::eval / pdf / sample --------------------------------------------
+__device__ __noinline__ f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
+    const f3 zero = mk(0, 0, 0);
+    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
+        if (wi.z <= 0 || wo.z <= 0) return zero;
+        return mul(ld3(b.refl), D_INV_PI * wo.z);
+    }
+    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:257-292
+        if (wi.z <= 0 || wo.z <= 0) return zero;
+        f3 H = normalize(add(wo, wi));
+        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        float D = distr_eval(d, H);
+        if (D == 0) return zero;
+        f3 F = mulv(fresnel_conductor_exact(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+        float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+        float model = D * G / (4.0f * wi.z);
+        return mul(F, model);
+    }
+    if (wi.z == 0) return zero;                                            // roughdielectric.cpp:270-346
+    bool reflect = wi.z * wo.z > 0;
+    f3 H;
+    if (reflect) {
+        H = normalize(add(wo, wi));
+    } else {
+        float eta = wi.z > 0 ? b.eta : b.inv_eta;
+        H = normalize(add(wi, mul(wo, eta)));
+    }
+    H = mul(H, signum(H.z));
+    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+    float D = distr_eval(d, H);
+    if (D == 0) return zero;
+    float ct;
+    float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
+    float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+    if (reflect) {
+        float value = F * D * G / (4.0f * fabsf(wi.z));
+        return mul(ld3(b.spec_r), value);
+    }
+    float eta = wi.z > 0.0f ? b.eta : b.inv_eta;
+    float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
+    float value = ((1 - F) * D * G * eta * eta * dot(wi, H) * dot(wo, H)) / (wi.z * sqrtDenom * sqrtDenom);
+    float factor = (wi.z > 0 ? b.inv_eta : b.eta);
+    return mul(ld3(b.spec_t), fabsf(value * factor * factor));
+}
+
+__device__ __noinline__ float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
+    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
+        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+        return D_INV_PI * wo.z;
+    }
+    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:294-319
+        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+        f3 H = normalize(add(wo, wi));
+        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        if (b.sample_visible) return distr_eval(d, H) * distr_smithG1(d, wi, H) / (4.0f * wi.z);
+        return distr_pdf(d, wi, H) / (4 * absdot(wo, H));
+    }
+    bool reflect = wi.z * wo.z > 0;                                        // roughdielectric.cpp:348-405
+    f3 H;
+    float dwh_dwo;
+    if (reflect) {
+        H = normalize(add(wo, wi));
+        dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+    } else {
+        float eta = wi.z > 0 ? b.eta : b.inv_eta;
+        H = normalize(add(wi, mul(wo, eta)));
+        float sqrtDenom = dot(wi, H) + eta * dot(wo, H);
+        dwh_dwo = (eta * eta * dot(wo, H)) / (sqrtDenom * sqrtDenom);
+    }
+    H = mul(H, signum(H.z));
+    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+    if (!b.sample_visible) distr_scale_alpha(d, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
+    float prob = distr_pdf(d, mul(wi, signum(wi.z)), H);
+    float ct;
+    float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
+    prob *= reflect ? F : (1 - F);
+    return fabsf(prob * dwh_dwo);
+}
+
+// BSDF::sample(bRec, pdf, sample): roughdielectric consumes one more 1D sample
+// for the lobe choice (roughdielectric.cpp:554); it is passed in as `u1d` by
+// the caller, which draws it from the sampler only for that BSDF.
+struct BSample { f3 wo; f3 weight; float pdf; float eta; int sampledType; };
+
+__device__ __noinline__ BSample bsdf_sample(const MtsgBsdf &b, f3 wi, float sx, float sy, float u1d) {
+    BSample r;
+    r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
+    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150
+        if (wi.z <= 0) return r;
+        r.wo = square_to_cosine_hemisphere(sx, sy);
+        r.eta = 1.0f;
+        r.sampledType = MTSG_F_DIFF_REFL;
+        r.pdf = D_INV_PI * r.wo.z;
+        r.weight = ld3(b.refl);
+        return r;
+    }
+    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:357-406
+        if (wi.z < 0) return r;
+        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        float pdf;
+        f3 m = distr_sample(d, wi, sx, sy, pdf);
+        r.pdf = pdf;
+        if (pdf == 0) return r;
+        r.wo = reflect_v(wi, m);
+        r.eta = 1.0f;
+        r.sampledType = MTSG_F_GLOSSY_REFL;
+        if (r.wo.z <= 0) return r;
+        f3 F = mulv(fresnel_conductor_exact(dot(wi, m), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+        float weight;
+        if (b.sample_visible) weight = distr_smithG1(d, r.wo, m);
+        else weight = distr_eval(d, m) * (distr_smithG1(d, wi, m) * distr_smithG1(d, r.wo, m)) * dot(wi, m) / (pdf * wi.z);
+        r.pdf = pdf / (4.0f * dot(r.wo, m));
+        r.weight = mul(F, weight);
+        return r;
+    }
+    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);   // roughdielectric.cpp:525-615
+    Distr sd = d;
+    if (!b.sample_visible) distr_scale_alpha(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
+    float microfacetPDF;
+    f3 m = distr_sample(sd, mul(wi, signum(wi.z)), sx, sy, microfacetPDF);
+    if (microfacetPDF == 0) return r;
+    float pdf = microfacetPDF;
+    float cosThetaT;
+    float F = fresnel_dielectric_ext(dot(wi, m), cosThetaT, b.eta);
+    f3 weight = mk(1.0f, 1.0f, 1.0f);
+    bool sampleReflection = true;
+    if (u1d > F) { sampleReflection = false; pdf *= 1 - F; }
+    else pdf *= F;
+    float dwh_dwo;
+    if (sampleReflection) {
+        r.wo = reflect_v(wi, m);
+        r.eta = 1.0f;
+        r.sampledType = MTSG_F_GLOSSY_REFL;
+        if (wi.z * r.wo.z <= 0) { r.pdf = pdf; return r; }
+        weight = mulv(weight, ld3(b.spec_r));
+        dwh_dwo = 1.0f / (4.0f * dot(r.wo, m));
+    } else {
+        if (cosThetaT == 0) { r.pdf = pdf; return r; }
+        r.wo = refract_v(wi, m, b.eta, cosThetaT);
+        r.eta = cosThetaT < 0 ? b.eta : b.inv_eta;
+        r.sampledType = MTSG_F_GLOSSY_TRANS;
+        if (wi.z * r.wo.z >= 0) { r.pdf = pdf; return r; }
+        float factor = cosThetaT < 0 ? b.inv_eta : b.eta;
+        weight = mulv(weight, mul(ld3(b.spec_t), factor * factor));
+        float sqrtDenom = dot(wi, m) + r.eta * dot(r.wo, m);
+        dwh_dwo = (r.eta * r.eta * dot(r.wo, m)) / (sqrtDenom * sqrtDenom);
+    }
+    if (b.sample_visible) weight = mul(weight, distr_smithG1(d, r.wo, m));
+    else weight = mul(weight, fabsf(distr_eval(d, m) * (distr_smithG1(d, wi, m) * distr_smithG1(d, r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z)));
+    r.pdf = pdf * fabsf(dwh_dwo);
+    r.weight = weight;
+    return r;
+}

@@ -1,0 +1,69 @@
+// dmath.h -- device-side arithmetic of the path (gfx950).
+//
+// Single-precision, evaluated in the reference's expression order (the whole
+// library is built with -ffp-contract=off: the reference's x86 SSE build has
+// no FMA).  Division and sqrt are IEEE correctly rounded
+// (-fhip-fp32-correctly-rounded-divide-sqrt).  Transcendentals the reference
+// takes from glibc are computed in double precision and rounded once to float
+// (math::fastexp/fastlog already are double in the reference,
+// include/mitsuba/core/math.h:175-216).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define D_EPSILON 1e-4f            // constants.h:28
+#define D_SHADOW_EPSILON 1e-3f     // constants.h:29
+#define D_PI 3.14159265358979323846f
+#define D_INV_PI 0.31830988618379067154f
+#define D_INV_TWOPI 0.15915494309189533577f
+#define D_ONE_MINUS_EPS 0x1.fffffep-1f
+
+struct f3 { float x, y, z; };
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mul(f3 a, float f) { return mk(a.x * f, a.y * f, a.z * f); }
+__device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 divv(f3 a, f3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
+__device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ f3 divs(f3 a, float f) { float r = 1.0f / f; return mul(a, r); }  // vector.h:535-541
+__device__ __forceinline__ float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ float absdot(f3 a, f3 b) { return fabsf(dot(a, b)); }
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {
+    return mk((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x));
+}
+__device__ __forceinline__ float len2(f3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ float dsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float len(f3 a) { return dsqrt(len2(a)); }
+__device__ __forceinline__ f3 normalize(f3 a) { return divs(a, len(a)); }
+__device__ __forceinline__ bool is_zero(f3 a) { return a.x == 0 && a.y == 0 && a.z == 0; }
+__device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+// std::max / std::min semantics
+__device__ __forceinline__ float smax(float a, float b) { return (a < b) ? b : a; }
+__device__ __forceinline__ float smin(float a, float b) { return (b < a) ? b : a; }
+__device__ __forceinline__ float safe_sqrt(float v) { return dsqrt(smax(0.0f, v)); }   // math.h:260
+__device__ __forceinline__ float signum(float v) { return copysignf(1.0f, v); }         // math.h:270
+__device__ __forceinline__ float smaxc(f3 s) { float r = s.x; r = smax(r, s.y); r = smax(r, s.z); return r; }
+
+// libm (glibc in the reference) -> double precision, rounded once
+__device__ __forceinline__ void d_sincos(float x, float *s, float *c) {
+    double sd, cd;
+    sincos((double)x, &sd, &cd);
+    *s = (float)sd; *c = (float)cd;
+}
+__device__ __forceinline__ float d_acos(float x) { return (float)acos((double)x); }
+__device__ __forceinline__ float d_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ __forceinline__ float d_tan(float x) { return (float)tan((double)x); }
+__device__ __forceinline__ float d_atan(float x) { return (float)atan((double)x); }
+__device__ __forceinline__ float d_expf(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float d_powf(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __forceinline__ float d_fastexp(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float d_fastlog(float x) { return (float)log((double)x); }
+
+struct Frame { f3 s, t, n; };
+__device__ __forceinline__ f3 to_local(const Frame &f, f3 v) { return mk(dot(v, f.s), dot(v, f.t), dot(v, f.n)); }
+__device__ __forceinline__ f3 to_world(const Frame &f, f3 v) {
+    return add(add(mul(f.s, v.x), mul(f.t, v.y)), mul(f.n, v.z));
+}

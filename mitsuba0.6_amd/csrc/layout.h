@@ -1,0 +1,130 @@
+// layout.h -- HBM layout of a configured scene, shared by the host builder
+// (scene_build.cpp) and the gfx950 kernels (path_kernel.hip).
+//
+// Everything is flat SoA/AoS arrays addressed by 32-bit indices:
+//   nodes     BVH2, 64 B per node, both children's boxes in one node (one
+//             node fetch = 4 x 16 B loads, tests two boxes)
+//   tris      48 B per primitive in BVH leaf order: the reference's TriAccel
+//             (triaccel.h:36-51) with {shapeIndex, primIndex} replaced by the
+//             global primitive id (tie-break key) and the shape id
+//   prim_vtx  per global primitive: vertex ids (global) + shape id
+//   dpdu      per global primitive: UV tangent (trimesh.cpp:683-739) or p1-p0
+//   vertices  positions / shading normals (zero-filled where a shape has none)
+#pragma once
+#include <stdint.h>
+
+#define MTSG_MAX_STACK 64     // BVH builder keeps depth < MTSG_MAX_STACK
+#define MTSG_LEAF_MAX 8       // primitives per leaf
+#define MTSG_SOBOL_DIMS 1024
+#define MTSG_SOBOL_SIZE 52
+#define MTSG_FILTER_RES 31
+#define MTSG_BLOCK_SIZE 32
+
+// node child reference: >= 0 inner node index; < 0 leaf: ~ref = first << 4 | count
+static inline int32_t mtsg_leaf_ref(uint32_t first, uint32_t count) {
+    return ~(int32_t)((first << 4) | count);
+}
+
+struct MtsgNode {            // 64 B (Aila-Laine layout)
+    float c0lox, c0hix, c0loy, c0hiy;
+    float c1lox, c1hix, c1loy, c1hiy;
+    float c0loz, c0hiz, c1loz, c1hiz;
+    int32_t c0, c1, pad0, pad1;
+};
+
+struct MtsgTri {             // 48 B
+    uint32_t k;
+    float n_u, n_v, n_d;
+    float a_u, a_v, b_nu, b_nv;
+    float c_nu, c_nv;
+    uint32_t prim;           // global primitive index (shape order, triangle order)
+    uint32_t shape;
+};
+
+enum {
+    MTSG_F_NULL = 0x00001, MTSG_F_DIFF_REFL = 0x00002, MTSG_F_DIFF_TRANS = 0x00004,
+    MTSG_F_GLOSSY_REFL = 0x00008, MTSG_F_GLOSSY_TRANS = 0x00010, MTSG_F_DELTA_REFL = 0x00020,
+    MTSG_F_DELTA_TRANS = 0x00040, MTSG_F_FRONT = 0x01000, MTSG_F_BACK = 0x02000
+};
+#define MTSG_F_SMOOTH (MTSG_F_DIFF_REFL | MTSG_F_DIFF_TRANS | MTSG_F_GLOSSY_REFL | MTSG_F_GLOSSY_TRANS)
+#define MTSG_F_TRANSMISSION (MTSG_F_DIFF_TRANS | MTSG_F_GLOSSY_TRANS | MTSG_F_DELTA_TRANS | MTSG_F_NULL)
+#define MTSG_F_DELTA (MTSG_F_NULL | MTSG_F_DELTA_REFL | MTSG_F_DELTA_TRANS)
+
+struct MtsgBsdf {            // configured BSDF (after ctor + configure)
+    int32_t type, flags, distr, sample_visible;
+    float alpha_u, alpha_v;  // texture average, clamped (microfacet.h:89-97)
+    float eta, inv_eta;      // roughdielectric
+    float refl[3], spec_r[3], spec_t[3], eta3[3], k3[3];
+    float pad;
+};
+
+struct MtsgShape {
+    int32_t bsdf, emitter, has_normals, pad;
+};
+
+struct MtsgEmitter {
+    int32_t type, shape;
+    uint32_t tri_first, tri_count;   // global prim range of the emitting mesh
+    uint32_t cdf_offset;             // into area_cdf (tri_count + 1 entries)
+    float inv_area, weight, pad;
+    float radiance[3], pad2;
+};
+
+struct MtsgCamera {
+    float sample_to_camera[16];
+    float to_world[16];
+    float inv_res_x, inv_res_y, near_clip, far_clip;
+    float dx[3], dy[3];
+};
+
+struct MtsgFilter {
+    float radius, scale;
+    int32_t border, type;
+    float values[MTSG_FILTER_RES + 1];
+};
+
+struct MtsgDeviceScene {
+    const MtsgNode *nodes;
+    const MtsgTri *tris;
+    const uint32_t *prim_vtx;   // 4 per primitive: v0, v1, v2, shape
+    const float *dpdu;          // 3 per primitive
+    const float *positions;     // 3 per vertex
+    const float *normals;       // 3 per vertex
+    const MtsgShape *shapes;
+    const MtsgBsdf *bsdfs;
+    const MtsgEmitter *emitters;
+    const float *area_cdf;
+    const float *em_cdf;        // num_emitters + 1
+    const uint32_t *sobol;      // MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE
+    uint32_t num_emitters, num_prims;
+    float em_norm, pad;
+    float aabb_min[3], aabb_max[3];
+    MtsgCamera cam;
+};
+
+// look_up tables for one film resolution (host-precomputed GF(2) inverse)
+struct MtsgLookup {
+    uint32_t m;                 // log2 resolution (0: identity enumeration)
+    uint32_t inv[32];
+    uint32_t ycol[64];
+};
+
+struct MtsgLaunch {
+    MtsgDeviceScene scene;
+    MtsgFilter filter;
+    MtsgLookup lut;
+    float resolution;           // sobol m_resolution
+    uint32_t scramble;          // sobol m_scramble (after TEA), low 32 bits used by sampleSingle
+    uint64_t scramble64;
+    uint32_t spp;
+    int32_t max_depth, rr_depth, strict_normals, hide_emitters, has_alpha;
+    int32_t film_w, film_h, fw, fh;   // image size and film size incl. borders
+    uint32_t x0, y0, width, height;
+    uint32_t row_block, row_stride, row_phase;
+    uint32_t num_tasks;               // pixels in the window after row interleave
+    float *film_own;                  // fw*fh*5: own-pixel sums (written once per pixel)
+    float *film_spill;                // fw*fh*5: splats into other pixels (atomics)
+    float *samples;                   // optional per-sample records
+    uint32_t *task_counter;           // global work queue head
+    unsigned long long *counters;     // [0] samples [1] rays [2] shadow [3] pathlen [4] nodes [5] tests [6] dim errors
+};

@@ -1,0 +1,744 @@
+// path_kernel.hip -- the MI355X (gfx950) hot path of Mitsuba 0.6's `path`
+// integrator: SamplingIntegrator::renderBlock's per-sample loop
+// (src/librender/integrator.cpp:140-188) around MIPathTracer::Li
+// (src/integrators/path/path.cpp:119-294), as one persistent HIP kernel.
+//
+// Execution model:
+//  * one lane = one pixel task at a time (all `spp` samples of that pixel, in
+//    sample order, so the pixel's own film sum is accumulated in registers in
+//    exactly the reference's order);
+//  * a lane whose path ends starts the next sample immediately (path
+//    regeneration), and a lane whose pixel is done pulls the next pixel from a
+//    global queue with one wave-aggregated atomic;
+//  * each loop iteration traces exactly one ray per active lane (primary,
+//    shadow or extension) through a shared BVH2 traversal, then advances that
+//    lane's path state machine to its next ray;
+//  * traversal stacks live in LDS, lane-strided (conflict-free).
+#include <hip/hip_runtime.h>
+
+#include "dbsdf.h"
+#include "layout.h"
+
+#define BLOCK 256
+#define STACK 32
+
+// ---------------------------------------------------------------------------
+// Sobol sampler (samplers/sobol.cpp:147-258, sobolseq.h:43-130)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sobol_sample(const uint32_t *__restrict__ M, uint64_t index, uint32_t dim,
+                                             uint32_t scramble) {
+    uint32_t result = scramble;
+    const uint32_t *row = M + dim * MTSG_SOBOL_SIZE;
+    while (index) {                      // XOR over the set bits of index (order-free)
+        uint32_t b = (uint32_t)__builtin_ctzll(index);
+        result ^= row[b];
+        index &= index - 1;
+    }
+    float v = (float)result * (1.0f / 4294967296.0f);
+    return smin(v, D_ONE_MINUS_EPS);
+}
+
+// sobol::look_up restated as the GF(2) solve it encodes (host precomputes inv/ycol)
+__device__ __forceinline__ uint64_t sobol_lookup(const MtsgLookup &L, uint32_t frame, uint32_t px, uint32_t py,
+                                                 uint64_t scramble) {
+    const uint32_t m = L.m;
+    uint32_t s = (uint32_t)((scramble & 0xFFFFFFFFull) >> (32 - m));
+    uint32_t mask = (1u << m) - 1u;
+    uint32_t sx = (px ^ s) & mask, sy = (py ^ s) & mask;
+    uint32_t jlo = __builtin_bitreverse32(sx) >> (32 - m);
+    uint64_t index = ((uint64_t)frame << (2 * m)) | jlo;
+    uint32_t K = 0;
+    uint64_t bits = index;
+    while (bits) {
+        uint32_t b = (uint32_t)__builtin_ctzll(bits);
+        K ^= L.ycol[b];
+        bits &= bits - 1;
+    }
+    uint32_t rhs = (sy ^ K) & mask, jhi = 0;
+    for (uint32_t t = 0; t < m; ++t) jhi |= (uint32_t)(__builtin_popcount(L.inv[t] & rhs) & 1) << t;
+    return index | ((uint64_t)jhi << m);
+}
+
+struct SamplerState {
+    uint64_t sobolIndex;
+    uint32_t sampleIndex;
+    uint32_t dim;
+    bool err;
+};
+
+// ---------------------------------------------------------------------------
+// per-lane path state
+// ---------------------------------------------------------------------------
+enum { ST_NEWSAMPLE = 0, ST_PRIMARY = 1, ST_SHADOW = 2, ST_EXT = 3, ST_DONE = 4 };
+
+struct Hit {
+    int valid;
+    float t;
+    f3 p, geoN, wi;
+    Frame sh;
+    int shape;
+};
+
+// ---------------------------------------------------------------------------
+// BVH2 traversal
+// ---------------------------------------------------------------------------
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool traverse(const MtsgDeviceScene &S, f3 o, f3 d, float mint, float maxt,
+                                         int *__restrict__ stk, uint32_t &bestSlot, float &bu, float &bv,
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
+    // reciprocal direction for the (conservative) node tests; exact zeros use
+    // +-1e30 so that 0 * inf never produces NaN (TriAccel uses the exact ray)
+    const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
+    const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
+    const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
+    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
+    (void)ox; (void)oy; (void)oz;
+    bool found = false;
+    uint32_t bestPrim = 0;
+    bt = maxt;
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        if (node >= 0) {
+            if (STATS) nodes++;
+            const MtsgNode *n = S.nodes + node;
+            const float4 a = *reinterpret_cast<const float4 *>(&n->c0lox);
+            const float4 b = *reinterpret_cast<const float4 *>(&n->c1lox);
+            const float4 c = *reinterpret_cast<const float4 *>(&n->c0loz);
+            const int4 e = *reinterpret_cast<const int4 *>(&n->c0);
+            // child 0
+            float t0x = (a.x - o.x) * ix, t1x = (a.y - o.x) * ix;
+            float t0y = (a.z - o.y) * iy, t1y = (a.w - o.y) * iy;
+            float t0z = (c.x - o.z) * iz, t1z = (c.y - o.z) * iz;
+            float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+            float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            // child 1
+            float u0x = (b.x - o.x) * ix, u1x = (b.y - o.x) * ix;
+            float u0y = (b.z - o.y) * iy, u1y = (b.w - o.y) * iy;
+            float u0z = (c.z - o.z) * iz, u1z = (c.w - o.z) * iz;
+            float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
+            float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
+            const bool h0 = n0 <= f0, h1 = n1 <= f1;
+            if (h0 && h1) {
+                int nearC = e.x, farC = e.y;
+                if (n1 < n0) { nearC = e.y; farC = e.x; }
+                stk[sp * BLOCK] = farC;
+                ++sp;
+                node = nearC;
+                continue;
+            } else if (h0) {
+                node = e.x;
+                continue;
+            } else if (h1) {
+                node = e.y;
+                continue;
+            }
+        } else {
+            const uint32_t ref = (uint32_t)(~node);
+            const uint32_t first = ref >> 4, count = ref & 15u;
+            for (uint32_t i = first; i < first + count; ++i) {
+                if (STATS) tests++;
+                const MtsgTri *tr = S.tris + i;
+                const float4 q0 = *reinterpret_cast<const float4 *>(&tr->k);
+                const float4 q1 = *reinterpret_cast<const float4 *>(&tr->a_u);
+                const float4 q2 = *reinterpret_cast<const float4 *>(&tr->c_nu);
+                const uint32_t k = __float_as_uint(q0.x);
+                // TriAccel::rayIntersect (triaccel.h:92-160)
+                float o_u, o_v, o_k, d_u, d_v, d_k;
+                if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+                else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+                else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+                else continue;
+                const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
+                const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
+                const float c_nu = q2.x, c_nv = q2.y;
+                const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+                if (t < mint || t > bt) continue;
+                const float hu = o_u + t * d_u - a_u;
+                const float hv = o_v + t * d_v - a_v;
+                const float u = hv * b_nu + hu * b_nv;
+                const float v = hu * c_nu + hv * c_nv;
+                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                    if (ANY) return true;
+                    const uint32_t prim = __float_as_uint(q2.z);
+                    // ties (t == bt): the larger primitive index wins
+                    if (!found || t < bt || prim > bestPrim) {
+                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+                    }
+                }
+            }
+        }
+        if (sp == 0) break;
+        --sp;
+        node = stk[sp * BLOCK];
+    }
+    return found;
+}
+
+// AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
+__device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, float &nearT, float &farT) {
+    nearT = -INFINITY; farT = INFINITY;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float origin = comp(o, i), di = comp(d, i);
+        const float minVal = S.aabb_min[i], maxVal = S.aabb_max[i];
+        if (di == 0) {
+            if (origin < minVal || origin > maxVal) return false;
+        } else {
+            const float rcp = (float)1 / di;                 // ray.dRcp (ray.h:86-93)
+            float t1 = (minVal - origin) * rcp;
+            float t2 = (maxVal - origin) * rcp;
+            if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
+            nearT = smax(t1, nearT);
+            farT = smin(t2, farT);
+            if (!(nearT <= farT)) return false;
+        }
+    }
+    return true;
+}
+
+// ShapeKDTree::rayIntersect (skdtree.cpp:112-142 closest, :207-226 shadow):
+// scene-AABB clip + adaptive ray epsilon -> [mint, maxt] for the traversal
+__device__ __forceinline__ bool ray_interval(const MtsgDeviceScene &S, f3 o, f3 d, float rmint, float rmaxt,
+                                             bool shadow, float &mint, float &maxt) {
+    if (!aabb_clip(S, o, d, mint, maxt)) return false;
+    float rayMinT = rmint;
+    if (rayMinT == D_EPSILON) {
+        if (shadow) rayMinT *= smax(smax(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+        else rayMinT *= smax(smax(smax(fabsf(o.x), fabsf(o.y)), fabsf(o.z)), D_EPSILON);
+    }
+    if (rayMinT > mint) mint = rayMinT;
+    if (rmaxt < maxt) maxt = rmaxt;
+    return maxt > mint;
+}
+
+// computeShadingFrame (util.cpp:603-608)
+__device__ __forceinline__ Frame shading_frame(f3 n, f3 dpdu) {
+    Frame f;
+    f.n = n;
+    f.s = normalize(sub(dpdu, mul(f.n, dot(f.n, dpdu))));
+    f.t = cross(f.n, f.s);
+    return f;
+}
+
+// fillIntersectionRecord<true> (skdtree.h:343-429)
+__device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot, float u, float v, float t, f3 d,
+                                         Hit &h) {
+    const uint32_t prim = S.tris[slot].prim;
+    const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
+    h.valid = 1;
+    h.t = t;
+    h.shape = (int)pv.w;
+    const float bx = 1 - u - v, by = u, bz = v;
+    const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
+             p2 = ld3(S.positions + 3 * (size_t)pv.z);
+    h.p = add(add(mul(p0, bx), mul(p1, by)), mul(p2, bz));
+    const f3 side1 = sub(p1, p0), side2 = sub(p2, p0);
+    f3 faceNormal = cross(side1, side2);
+    const float length = len(faceNormal);
+    if (!is_zero(faceNormal)) faceNormal = divs(faceNormal, length);
+    const f3 dpdu = ld3(S.dpdu + 3 * (size_t)prim);
+    f3 shN;
+    if (S.shapes[h.shape].has_normals) {
+        const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
+                 n2 = ld3(S.normals + 3 * (size_t)pv.z);
+        shN = normalize(add(add(mul(n0, bx), mul(n1, by)), mul(n2, bz)));
+        if (dot(faceNormal, shN) < 0) faceNormal = neg(faceNormal);
+    } else {
+        shN = faceNormal;
+    }
+    h.geoN = faceNormal;
+    h.sh = shading_frame(shN, dpdu);
+    h.wi = to_local(h.sh, neg(d));
+}
+
+// DiscreteDistribution::sample/sampleReuse (core/pmf.h:124-169)
+__device__ __forceinline__ uint32_t dd_sample_reuse(const float *__restrict__ cdf, uint32_t n, float &value,
+                                                   float *pdf) {
+    uint32_t lo = 0, hi = n + 1;                          // std::lower_bound
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (cdf[mid] < value) lo = mid + 1; else hi = mid;
+    }
+    int idx = (int)lo - 1;
+    if (idx < 0) idx = 0;
+    uint32_t index = (uint32_t)idx;
+    if (index > n - 1) index = n - 1;
+    while (cdf[index + 1] - cdf[index] == 0 && index < n - 1) ++index;
+    const float c0 = cdf[index], c1 = cdf[index + 1];
+    if (pdf) *pdf = c1 - c0;
+    value = (value - c0) / (c1 - c0);
+    return index;
+}
+
+// ---------------------------------------------------------------------------
+// film splat: ImageBlock::put (render/imageblock.h:124-204) into the 32x32
+// block that owns pixel (px, py); own-pixel weight goes to the lane's
+// registers, other touched pixels to the spill film (atomics)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float filter_disc(const MtsgFilter &F, float x) {
+    int i = (int)fabsf(x * F.scale);
+    if (MTSG_FILTER_RES < i) i = MTSG_FILTER_RES;
+    return F.values[i];
+}
+
+__device__ __forceinline__ void film_splat(const MtsgLaunch &L, int px, int py, float sx, float sy,
+                                           const float *val, float *own) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+        if (!isfinite(val[i]) || val[i] < 0) return;
+    const MtsgFilter &F = L.filter;
+    const int b = F.border;
+    const int bx = (px / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE, by = (py / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE;
+    const int bw = MTSG_BLOCK_SIZE + 2 * b;
+    const float posx = sx - 0.5f - (float)(bx - b), posy = sy - 0.5f - (float)(by - b);
+    int minx = (int)ceilf(posx - F.radius), miny = (int)ceilf(posy - F.radius);
+    int maxx = (int)floorf(posx + F.radius), maxy = (int)floorf(posy + F.radius);
+    if (minx < 0) minx = 0;
+    if (miny < 0) miny = 0;
+    if (maxx > bw - 1) maxx = bw - 1;
+    if (maxy > bw - 1) maxy = bw - 1;
+    for (int y = miny; y <= maxy; ++y) {
+        const float wy = filter_disc(F, (float)y - posy);
+        for (int x = minx; x <= maxx; ++x) {
+            const float weight = filter_disc(F, (float)x - posx) * wy;
+            const int gx = x + bx, gy = y + by;
+            if (gx >= L.fw || gy >= L.fh) continue;
+            if (gx == px + b && gy == py + b) {
+#pragma unroll
+                for (int k = 0; k < 5; ++k) own[k] += weight * val[k];
+            } else {
+                float *dst = L.film_spill + ((size_t)gy * L.fw + gx) * 5;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) atomicAdd(dst + k, weight * val[k]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// the persistent path kernel
+// ---------------------------------------------------------------------------
+struct PathVars {
+    f3 L, thr;
+    float eta;
+    int depth;
+    bool scattered, emitted;
+    float alpha;
+    // vertex
+    Hit its;
+    f3 rayD;          // direction of the ray that produced `its`
+    // pending NEE / BSDF sample
+    f3 neeC;          // throughput*value*bsdfVal*weight, committed if unoccluded
+    f3 refN;          // DirectSamplingRecord::refN of the current vertex
+    f3 bsdfWeight;
+    float bsdfPdf, bsdfEta;
+    int sampledType;
+};
+
+__device__ __forceinline__ float next1d(const MtsgLaunch &L, SamplerState &s) {
+    if (s.dim >= MTSG_SOBOL_DIMS) { s.err = true; return 0.0f; }        // sobol.cpp:219-229
+    return sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
+}
+__device__ __forceinline__ void next2d(const MtsgLaunch &L, SamplerState &s, int px, int py, float &u,
+                                       float &v) {                                 // sobol.cpp:231-250
+    if (s.dim + 1 >= 5 && s.dim < 5) s.dim = 5;
+    if (s.dim + 1 >= MTSG_SOBOL_DIMS) { s.err = true; u = v = 0.0f; return; }
+    if (s.dim == 0 && s.sobolIndex != (uint64_t)s.sampleIndex) {
+        u = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble) * L.resolution - (float)px;
+        v = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble) * L.resolution - (float)py;
+    } else {
+        u = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
+        v = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
+    }
+}
+
+__device__ __forceinline__ f3 xf_point(const float *m, f3 p) {         // transform.h:108-125
+    float x = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float y = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float z = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float w = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    if (w == 1.0f) return mk(x, y, z);
+    return divs(mk(x, y, z), w);
+}
+
+__device__ __forceinline__ f3 area_Le(const MtsgDeviceScene &S, const Hit &h, f3 d) {   // area.cpp:104-109
+    const MtsgEmitter &e = S.emitters[S.shapes[h.shape].emitter];
+    if (dot(h.sh.n, d) <= 0) return mk(0, 0, 0);
+    return ld3(e.radiance);
+}
+
+// decode task -> pixel (tile-major 8x8 over the window's active rows)
+__device__ __forceinline__ bool task_pixel(const MtsgLaunch &L, uint32_t task, int &px, int &py) {
+    const uint32_t tilesX = (L.width + 7) / 8;
+    const uint32_t tile = task >> 6, in = task & 63;
+    const uint32_t lx = (tile % tilesX) * 8 + (in & 7);
+    const uint32_t r = (tile / tilesX) * 8 + (in >> 3);
+    if (lx >= L.width) return false;
+    const uint32_t rb = L.row_block, rs = L.row_stride;
+    const uint32_t blk = r / rb, off = r % rb;
+    const uint32_t ly = (blk * rs + L.row_phase) * rb + off;
+    if (ly >= L.height) return false;
+    px = (int)(L.x0 + lx);
+    py = (int)(L.y0 + ly);
+    return true;
+}
+
+template <bool SAMPLES, bool STATS>
+__global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
+    __shared__ int stack_mem[STACK * BLOCK];
+    int *stk = stack_mem + threadIdx.x;
+    const MtsgDeviceScene &S = L.scene;
+    const uint32_t lane = threadIdx.x & 63;
+
+    unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
+
+    int state = ST_NEWSAMPLE;
+    bool haveTask = false;
+    int px = 0, py = 0;
+    uint32_t j = 0;
+    float own[5] = {0, 0, 0, 0, 0};
+    SamplerState smp;
+    smp.sobolIndex = 0; smp.sampleIndex = 0; smp.dim = 0; smp.err = false;
+    PathVars P;
+    float sx = 0, sy = 0;
+    // current ray
+    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);
+    float rmint = 0, rmaxt = 0;
+    uint32_t sampleSlot = 0;
+
+    while (true) {
+        // ---- A: start samples / fetch tasks --------------------------------
+        if (state == ST_NEWSAMPLE) {
+            if (haveTask && j >= L.spp) {
+                float *dst = L.film_own + ((size_t)(py + L.filter.border) * L.fw + (px + L.filter.border)) * 5;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) dst[k] = own[k];
+                haveTask = false;
+            }
+        }
+        // wave-aggregated task fetch
+        while (true) {
+            const bool need = (state == ST_NEWSAMPLE) && !haveTask;
+            const unsigned long long mask = __ballot(need);
+            if (mask == 0) break;
+            uint32_t base = 0;
+            const int leader = __ffsll((long long)mask) - 1;
+            if ((int)lane == leader) base = atomicAdd(L.task_counter, (uint32_t)__popcll(mask));
+            base = __shfl(base, leader);
+            if (need) {
+                const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+                const uint32_t task = base + rank;
+                if (task >= L.num_tasks) {
+                    state = ST_DONE;
+                } else if (task_pixel(L, task, px, py)) {
+                    haveTask = true;
+                    j = 0;
+                    sampleSlot = 0;
+#pragma unroll
+                    for (int k = 0; k < 5; ++k) own[k] = 0.0f;
+                }
+            }
+        }
+        if (state == ST_NEWSAMPLE) {
+            // SamplingIntegrator::renderBlock inner loop body (integrator.cpp:165-186)
+            smp.dim = 0;
+            smp.sampleIndex = j;
+            smp.err = false;
+            if (L.lut.m > 1) smp.sobolIndex = sobol_lookup(L.lut, j, (uint32_t)px, (uint32_t)py, L.scramble64);
+            else smp.sobolIndex = j;
+            float u, v;
+            next2d(L, smp, px, py, u, v);
+            sx = (float)px + u;
+            sy = (float)py + v;
+            // PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298)
+            const MtsgCamera &cam = S.cam;
+            const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+            const f3 dl = normalize(nearP);
+            const float invZ = 1.0f / dl.z;
+            rmint = cam.near_clip * invZ;
+            rmaxt = cam.far_clip * invZ;
+            const float *W = cam.to_world;
+            ro = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
+                    W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);
+            rd = mk(W[0] * dl.x + W[1] * dl.y + W[2] * dl.z, W[4] * dl.x + W[5] * dl.y + W[6] * dl.z,
+                    W[8] * dl.x + W[9] * dl.y + W[10] * dl.z);
+            // Li() prologue (path.cpp:119-133)
+            P.L = mk(0, 0, 0);
+            P.thr = mk(1.0f, 1.0f, 1.0f);
+            P.eta = 1.0f;
+            P.depth = 1;
+            P.scattered = false;
+            P.emitted = true;
+            state = ST_PRIMARY;
+        }
+        if (__all(state == ST_DONE)) break;
+
+        // ---- B: trace one ray per active lane ------------------------------
+        bool hit = false;
+        uint32_t slot = 0;
+        float hu = 0, hv = 0, ht = 0;
+        if (state == ST_PRIMARY || state == ST_EXT || state == ST_SHADOW) {
+            const bool shadow = state == ST_SHADOW;
+            if (shadow) cShadow++; else cRays++;
+            float mint, maxt;
+            if (ray_interval(S, ro, rd, rmint, rmaxt, shadow, mint, maxt)) {
+                if (shadow)
+                    hit = traverse<true, STATS>(S, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                else
+                    hit = traverse<false, STATS>(S, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+            }
+        }
+
+        // ---- C: advance the path state machine ------------------------------
+        bool vertex = false;      // run the top-of-loop body of Li() for P.its
+        bool endPath = false;
+        if (state == ST_PRIMARY) {
+            // rRec.rayIntersect (records.inl:117-144)
+            if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+            P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
+            P.rayD = rd;
+            vertex = true;
+        } else if (state == ST_SHADOW) {
+            if (!hit) P.L = add(P.L, P.neeC);
+            state = ST_EXT;   // continue with the BSDF sample below
+        } else if (state == ST_EXT) {
+            // after scene->rayIntersect(ray, its) (path.cpp:226-286)
+            if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+            if (!P.its.valid) {
+                endPath = true;   // no environment emitter: break before the throughput update
+            } else {
+                bool hitEmitter = false;
+                f3 value = mk(0, 0, 0);
+                const MtsgShape &sh = S.shapes[P.its.shape];
+                f3 dn = mk(0, 0, 0);
+                int em = -1;
+                if (sh.emitter >= 0) {
+                    value = area_Le(S, P.its, neg(rd));
+                    dn = P.its.sh.n;
+                    em = sh.emitter;
+                    hitEmitter = true;
+                }
+                P.thr = mulv(P.thr, P.bsdfWeight);
+                P.eta *= P.bsdfEta;
+                if (hitEmitter) {
+                    float lumPdf = 0;
+                    if (!(P.sampledType & MTSG_F_DELTA)) {
+                        // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126
+                        const MtsgEmitter &e = S.emitters[em];
+                        float pdf = 0.0f;
+                        if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0)
+                            pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
+                        lumPdf = pdf * (e.weight * S.em_norm);
+                    }
+                    float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                    P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
+                }
+                P.emitted = false;
+                if (P.depth++ >= L.rr_depth) {
+                    const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
+                    if (next1d(L, smp) >= q) endPath = true;
+                    else P.thr = divs(P.thr, q);
+                }
+                if (smp.err) endPath = true;
+                if (!endPath) { P.rayD = rd; vertex = true; }
+            }
+        }
+
+        bool needBsdf = false;
+        if (vertex) {
+            // loop head of Li() (path.cpp:135-200)
+            if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
+                endPath = true;
+            } else if (!P.its.valid) {
+                endPath = true;   // primary miss, no environment emitter
+            } else {
+                const MtsgShape &sh = S.shapes[P.its.shape];
+                const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
+                if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
+                    P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(P.rayD))));
+                if ((P.depth >= L.max_depth && L.max_depth > 0) ||
+                    (L.strict_normals && dot(P.rayD, P.its.geoN) * P.its.wi.z >= 0)) {
+                    endPath = true;
+                } else {
+                    P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
+                    needBsdf = true;
+                    if (bsdf.flags & MTSG_F_SMOOTH) {
+                        // Scene::sampleEmitterDirect (scene.cpp:828-852)
+                        float ex, ey;
+                        next2d(L, smp, px, py, ex, ey);
+                        float emPdf;
+                        const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
+                        const MtsgEmitter &e = S.emitters[ei];
+                        // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
+                        float py2 = ey;
+                        const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
+                        const uint32_t prim = e.tri_first + lt;
+                        const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
+                        const float a = safe_sqrt(1.0f - ex);
+                        const float bx = 1 - a, by = a * py2;
+                        const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
+                                 p2 = ld3(S.positions + 3 * (size_t)pv.z);
+                        const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
+                        const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
+                        f3 ln;
+                        if (S.shapes[e.shape].has_normals) {
+                            const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
+                                     n2 = ld3(S.normals + 3 * (size_t)pv.z);
+                            ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
+                        } else {
+                            ln = normalize(cross(sideA, sideB));
+                        }
+                        float pdf = e.inv_area;
+                        // Shape::sampleDirect (shape.cpp:102-115)
+                        f3 dd = sub(lp, P.its.p);
+                        const float distSquared = len2(dd);
+                        const float dist = dsqrt(distSquared);
+                        dd = divs(dd, dist);
+                        const float dp = absdot(dd, ln);
+                        pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+                        // AreaLight::sampleDirect (area.cpp:158-173)
+                        f3 value = mk(0, 0, 0);
+                        if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+                        else pdf = 0.0f;
+                        if (pdf != 0) {
+                            // the shadow ray's verdict is applied after the trace; everything
+                            // else of the NEE estimate is visibility-independent (path.cpp:176-199)
+                            const float dpdf = pdf * emPdf;
+                            value = divs(value, emPdf);
+                            f3 c = mk(0, 0, 0);
+                            if (!is_zero(value)) {
+                                const f3 wo = to_local(P.its.sh, dd);
+                                const f3 bsdfVal = bsdf_eval(bsdf, P.its.wi, wo);
+                                if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
+                                    const float bsdfPdf = bsdf_pdf(bsdf, P.its.wi, wo);
+                                    const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
+                                    const float weight = pa / (pa + pb);
+                                    c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
+                                }
+                            }
+                            P.neeC = c;
+                            ro = P.its.p;
+                            rd = dd;
+                            rmint = D_EPSILON;
+                            rmaxt = dist * (1 - D_SHADOW_EPSILON);
+                            state = ST_SHADOW;
+                            needBsdf = false;   // BSDF sampling resumes after the shadow trace
+                        }
+                    }
+                }
+            }
+        }
+        // BSDF sampling (path.cpp:206-226): after a shadow ray, or at a vertex
+        // that issued none
+        const bool doBsdf = !endPath && ((state == ST_EXT && !vertex) || (vertex && needBsdf));
+        if (doBsdf) {
+            state = ST_EXT;
+            const MtsgBsdf &bsdf = S.bsdfs[S.shapes[P.its.shape].bsdf];
+            float bx, by;
+            next2d(L, smp, px, py, bx, by);
+            float u1d = 0.0f;
+            if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(L, smp);   // roughdielectric.cpp:554
+            const BSample bs = bsdf_sample(bsdf, P.its.wi, bx, by, u1d);
+            if (is_zero(bs.weight) || smp.err) {
+                endPath = true;
+            } else {
+                P.scattered |= bs.sampledType != MTSG_F_NULL;
+                const f3 wo = to_world(P.its.sh, bs.wo);
+                if (L.strict_normals && dot(P.its.geoN, wo) * bs.wo.z <= 0) {
+                    endPath = true;
+                } else {
+                    P.bsdfWeight = bs.weight;
+                    P.bsdfPdf = bs.pdf;
+                    P.bsdfEta = bs.eta;
+                    P.sampledType = bs.sampledType;
+                    ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
+                    rd = wo;
+                    rmint = D_EPSILON;
+                    rmaxt = INFINITY;
+                }
+            }
+        }
+
+        if (endPath) {
+            // block->put(samplePos, spec, alpha); sampler->advance() (integrator.cpp:184-186)
+            const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
+            film_splat(L, px, py, sx, sy, val, own);
+            if (SAMPLES) {
+                const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
+                float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
+                rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
+                rec[4] = sx; rec[5] = sy; rec[6] = (float)P.depth; rec[7] = smp.err ? 1.0f : 0.0f;
+            }
+            cLen += (unsigned long long)P.depth;
+            cSamples++;
+            if (smp.err) cErr++;
+            ++j;
+            state = ST_NEWSAMPLE;
+        }
+    }
+    // flush a task finished in the last iteration
+    if (haveTask && j >= L.spp) {
+        float *dst = L.film_own + ((size_t)(py + L.filter.border) * L.fw + (px + L.filter.border)) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dst[k] = own[k];
+    }
+    (void)sampleSlot;
+    atomicAdd(L.counters + 0, cSamples);
+    atomicAdd(L.counters + 1, cRays);
+    atomicAdd(L.counters + 2, cShadow);
+    atomicAdd(L.counters + 3, cLen);
+    if (STATS) {
+        atomicAdd(L.counters + 4, cNodes);
+        atomicAdd(L.counters + 5, cTests);
+    }
+    if (cErr) atomicAdd(L.counters + 6, cErr);
+}
+
+__global__ void film_finalize(float *__restrict__ own, const float *__restrict__ spill, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) own[i] += spill[i];
+}
+
+// element-wise IEEE checks of the device arithmetic the path relies on
+__global__ void arith_probe(const float *a, const float *b, float *out, int n) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s, c;
+    d_sincos(a[i], &s, &c);
+    out[8 * i + 0] = a[i] / b[i];
+    out[8 * i + 1] = dsqrt(fabsf(a[i]));
+    out[8 * i + 2] = s;
+    out[8 * i + 3] = c;
+    out[8 * i + 4] = d_acos(fminf(fmaxf(a[i], -1.0f), 1.0f));
+    out[8 * i + 5] = d_atan2(a[i], b[i]);
+    out[8 * i + 6] = d_fastexp(-fabsf(a[i]));
+    out[8 * i + 7] = a[i] * b[i] + a[i];
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (called by capi.cpp)
+// ---------------------------------------------------------------------------
+hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
+    if (samples && stats) hipLaunchKernelGGL((path_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, L);
+    else if (samples) hipLaunchKernelGGL((path_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, L);
+    else if (stats) hipLaunchKernelGGL((path_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, L);
+    else hipLaunchKernelGGL((path_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, L);
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream) {
+    const int threads = 256;
+    const int blocks = (int)((n + threads - 1) / threads);
+    if (blocks > 0) hipLaunchKernelGGL(film_finalize, dim3(blocks), dim3(threads), 0, stream, own, spill, n);
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream) {
+    hipLaunchKernelGGL(arith_probe, dim3((n + 255) / 256), dim3(256), 0, stream, a, b, out, n);
+    return hipGetLastError();
+}
+
+int mtsg_path_kernel_occupancy(int *blocksPerCU) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false>, BLOCK, 0);
+}

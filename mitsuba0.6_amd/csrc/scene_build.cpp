@@ -1,0 +1,687 @@
+// scene_build.cpp -- host configure() for the MI355X path integrator.
+//
+// Derives, from the scene description of include/mtsgpu.h, everything the
+// reference computes in its configure()/initialize() steps, then lays it out
+// for HBM (layout.h):
+//   camera        librender/sensor.cpp:95-107,239-305, sensors/perspective.cpp:126-163
+//   BSDFs         bsdfs/diffuse.cpp:75-101, roughconductor.cpp:168-240,
+//                 roughdielectric.cpp:183-256, librender/bsdf.cpp:88-113
+//   meshes        TriMesh::configure / computeNormals / computeUVTangents /
+//                 prepareSamplingTable (librender/trimesh.cpp:361-739)
+//   default BSDFs Shape::configure (librender/shape.cpp:48-75)
+//   emitter PDF   Scene::initialize (librender/scene.cpp:376-381)
+//   TriAccel      skdtree.cpp:74-109, render/triaccel.h:58-90
+//   scene bounds  gkdtree.h:996-1001,1211-1217 (MTS_KD_AABB_EPSILON)
+// The acceleration structure is a binned-SAH BVH2 instead of the reference's
+// SAH kd-tree: traversal returns the same closest hit.
+#include "scene_build.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "sobol_params.inc"
+
+namespace {
+
+inline float fmax_std(float a, float b) { return (a < b) ? b : a; }   // std::max
+inline float fmin_std(float a, float b) { return (b < a) ? b : a; }   // std::min
+
+struct V { float x, y, z; };
+inline V v(float x, float y, float z) { V r = {x, y, z}; return r; }
+inline V operator+(V a, V b) { return v(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline V operator-(V a, V b) { return v(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline V operator*(V a, float f) { return v(a.x * f, a.y * f, a.z * f); }
+inline V vdiv(V a, float f) { float r = 1.0f / f; return a * r; }
+inline float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V cross(V a, V b) { return v((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x)); }
+inline float length(V a) { return std::sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+inline V normalize(V a) { return vdiv(a, length(a)); }
+inline float at(V a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+inline float avg3(float a) { float r = 0.0f; r += a; r += a; r += a; return r * (1.0f / 3); }   // Spectrum::average
+
+const float kPi = 3.14159265358979323846f;
+
+// ---- 4x4 transforms (core/matrix.h:744-756, matrix.inl:138-193, transform.cpp) ----
+struct M4 { float m[4][4]; };
+M4 mul(const M4 &a, const M4 &b) {
+    M4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float sum = 0;
+            for (int k = 0; k < 4; ++k) sum += a.m[i][k] * b.m[k][j];
+            r.m[i][j] = sum;
+        }
+    return r;
+}
+bool invert(const M4 &src, M4 &t) {
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    t = src;
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        float big = 0;
+        for (int j = 0; j < 4; j++)
+            if (ipiv[j] != 1)
+                for (int k = 0; k < 4; k++) {
+                    if (ipiv[k] == 0) {
+                        if (std::fabs(t.m[j][k]) >= big) { big = std::fabs(t.m[j][k]); irow = j; icol = k; }
+                    } else if (ipiv[k] > 1) {
+                        return false;
+                    }
+                }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) std::swap(t.m[irow][k], t.m[icol][k]);
+        indxr[i] = irow; indxc[i] = icol;
+        if (t.m[icol][icol] == 0) return false;
+        float pivinv = 1.f / t.m[icol][icol];
+        t.m[icol][icol] = 1.f;
+        for (int j = 0; j < 4; j++) t.m[icol][j] *= pivinv;
+        for (int j = 0; j < 4; j++)
+            if (j != icol) {
+                float save = t.m[j][icol];
+                t.m[j][icol] = 0;
+                for (int k = 0; k < 4; k++) t.m[j][k] -= t.m[icol][k] * save;
+            }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) std::swap(t.m[k][indxr[j]], t.m[k][indxc[j]]);
+    return true;
+}
+struct Xf { M4 t, inv; };
+M4 diag(float a, float b, float c, float d) {
+    M4 r; std::memset(&r, 0, sizeof r);
+    r.m[0][0] = a; r.m[1][1] = b; r.m[2][2] = c; r.m[3][3] = d;
+    return r;
+}
+Xf compose(const Xf &a, const Xf &b) { return Xf{mul(a.t, b.t), mul(b.inv, a.inv)}; }
+Xf scale(float x, float y, float z) { return Xf{diag(x, y, z, 1), diag(1.0f / x, 1.0f / y, 1.0f / z, 1)}; }
+Xf translate(float x, float y, float z) {
+    Xf r{diag(1, 1, 1, 1), diag(1, 1, 1, 1)};
+    r.t.m[0][3] = x; r.t.m[1][3] = y; r.t.m[2][3] = z;
+    r.inv.m[0][3] = -x; r.inv.m[1][3] = -y; r.inv.m[2][3] = -z;
+    return r;
+}
+inline float deg2rad(float x) { return x * (kPi / 180.0f); }
+inline float rad2deg(float x) { return x * (180.0f / kPi); }
+V xf_point(const M4 &m, V p) {
+    float x = m.m[0][0] * p.x + m.m[0][1] * p.y + m.m[0][2] * p.z + m.m[0][3];
+    float y = m.m[1][0] * p.x + m.m[1][1] * p.y + m.m[1][2] * p.z + m.m[1][3];
+    float z = m.m[2][0] * p.x + m.m[2][1] * p.y + m.m[2][2] * p.z + m.m[2][3];
+    float w = m.m[3][0] * p.x + m.m[3][1] * p.y + m.m[3][2] * p.z + m.m[3][3];
+    if (w == 1.0f) return v(x, y, z);
+    return vdiv(v(x, y, z), w);
+}
+
+int configure_camera(const mtsgpu_sensor_desc &s, MtsgCamera &cam, std::string &err) {
+    if (s.film_width == 0 || s.film_height == 0) { err = "film size must be positive"; return MTSGPU_EINVAL; }
+    const float aspect = (float)s.film_width / (float)s.film_height;
+    float xfov = s.fov;
+    int axis = s.fov_axis;
+    if (axis == MTSGPU_FOV_SMALLER) axis = aspect > 1 ? MTSGPU_FOV_Y : MTSGPU_FOV_X;
+    else if (axis == MTSGPU_FOV_LARGER) axis = aspect > 1 ? MTSGPU_FOV_X : MTSGPU_FOV_Y;
+    if (axis == MTSGPU_FOV_Y) {
+        xfov = rad2deg(2 * std::atan(std::tan(0.5f * deg2rad(s.fov)) * aspect));
+    } else if (axis == MTSGPU_FOV_DIAGONAL) {
+        float diagonal = 2 * std::tan(0.5f * deg2rad(s.fov));
+        float width = diagonal / std::sqrt(1.0f + 1.0f / (aspect * aspect));
+        xfov = rad2deg(2 * std::atan(width * 0.5f));
+    } else if (axis != MTSGPU_FOV_X) {
+        err = "The 'fovAxis' parameter must be set to one of 'smaller', 'larger', 'diagonal', 'x', or 'y'!";
+        return MTSGPU_EINVAL;
+    }
+    if (!(xfov > 0 && xfov < 180)) { err = "The horizontal field of view must be in the interval (0, 180)!"; return MTSGPU_EINVAL; }
+    if (!(s.near_clip > 0)) { err = "The 'nearClip' parameter must be greater than zero!"; return MTSGPU_EINVAL; }
+    if (!(s.near_clip < s.far_clip)) { err = "The 'nearClip' parameter must be less than 'farClip'!"; return MTSGPU_EINVAL; }
+    // Transform::perspective (transform.cpp:99-123)
+    float recip = 1.0f / (s.far_clip - s.near_clip);
+    float cot = 1.0f / std::tan(deg2rad(xfov / 2.0f));
+    M4 P; std::memset(&P, 0, sizeof P);
+    P.m[0][0] = cot; P.m[1][1] = cot;
+    P.m[2][2] = s.far_clip * recip; P.m[2][3] = -s.near_clip * s.far_clip * recip;
+    P.m[3][2] = 1;
+    Xf persp;
+    persp.t = P;
+    if (!invert(P, persp.inv)) { err = "Unable to invert singular matrix"; return MTSGPU_EINVAL; }
+    // perspective.cpp:146-151 (crop = film)
+    Xf a = scale(1.0f / 1.0f, 1.0f / 1.0f, 1.0f);
+    Xf b = translate(-0.0f, -0.0f, 0.0f);
+    Xf c = scale(-0.5f, -0.5f * aspect, 1.0f);
+    Xf d = translate(-1.0f, -1.0f / aspect, 0.0f);
+    Xf camToSample = compose(compose(compose(compose(a, b), c), d), persp);
+    const M4 &s2c = camToSample.inv;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            cam.sample_to_camera[i * 4 + j] = s2c.m[i][j];
+            cam.to_world[i * 4 + j] = s.to_world[i * 4 + j];
+        }
+    cam.inv_res_x = (float)1 / (float)s.film_width;
+    cam.inv_res_y = (float)1 / (float)s.film_height;
+    cam.near_clip = s.near_clip;
+    cam.far_clip = s.far_clip;
+    V o0 = xf_point(s2c, v(0.0f, 0.0f, 0.0f));
+    V dx = xf_point(s2c, v(cam.inv_res_x, 0.0f, 0.0f)) - o0;
+    V dy = xf_point(s2c, v(0.0f, cam.inv_res_y, 0.0f)) - o0;
+    cam.dx[0] = dx.x; cam.dx[1] = dx.y; cam.dx[2] = dx.z;
+    cam.dy[0] = dy.x; cam.dy[1] = dy.y; cam.dy[2] = dy.z;
+    return MTSGPU_OK;
+}
+
+float energy_scale(const float *s, int ensure) {   // BSDF::ensureEnergyConservation (bsdf.cpp:88-113)
+    if (!ensure) return 1.0f;
+    float mx = s[0];
+    mx = fmax_std(mx, s[1]);
+    mx = fmax_std(mx, s[2]);
+    if (mx > 1.0f) return 0.99f * (1.0f / mx);
+    return 1.0f;
+}
+
+int configure_bsdf(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::string &err) {
+    std::memset(&b, 0, sizeof b);
+    b.type = d.type;
+    if (d.type == MTSGPU_BSDF_DIFFUSE) {
+        float sc = energy_scale(d.reflectance, d.ensure_energy_conservation);
+        for (int i = 0; i < 3; ++i) b.refl[i] = sc != 1.0f ? d.reflectance[i] * sc : d.reflectance[i];
+        float mx = fmax_std(fmax_std(b.refl[0], b.refl[1]), b.refl[2]);
+        b.flags = mx > 0 ? (MTSG_F_DIFF_REFL | MTSG_F_FRONT) : 0;
+        return MTSGPU_OK;
+    }
+    if (d.type != MTSGPU_BSDF_ROUGHCONDUCTOR && d.type != MTSGPU_BSDF_ROUGHDIELECTRIC) {
+        err = "unsupported BSDF type"; return MTSGPU_EINVAL;
+    }
+    if (d.distribution < 0 || d.distribution > 2) {
+        err = "Specified an invalid distribution, must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!";
+        return MTSGPU_EINVAL;
+    }
+    b.distr = d.distribution;
+    b.sample_visible = d.distribution == MTSGPU_DISTR_PHONG ? 0 : d.sample_visible;
+    const float au = fmax_std(d.alpha_u, 1e-4f), av = fmax_std(d.alpha_v, 1e-4f);
+    b.alpha_u = avg3(au);
+    b.alpha_v = avg3(av);
+    float sc = energy_scale(d.specular_reflectance, d.ensure_energy_conservation);
+    for (int i = 0; i < 3; ++i) b.spec_r[i] = sc != 1.0f ? d.specular_reflectance[i] * sc : d.specular_reflectance[i];
+    if (d.type == MTSGPU_BSDF_ROUGHCONDUCTOR) {
+        const float r = 1.0f / d.ext_eta;
+        for (int i = 0; i < 3; ++i) { b.eta3[i] = d.eta[i] * r; b.k3[i] = d.k[i] * r; }
+        b.flags = MTSG_F_GLOSSY_REFL | MTSG_F_FRONT;
+    } else {
+        if (d.int_ior < 0 || d.ext_ior < 0 || d.int_ior == d.ext_ior) {
+            err = "The interior and exterior indices of refraction must be positive and differ!";
+            return MTSGPU_EINVAL;
+        }
+        b.eta = d.int_ior / d.ext_ior;
+        b.inv_eta = 1 / b.eta;
+        float st = energy_scale(d.specular_transmittance, d.ensure_energy_conservation);
+        for (int i = 0; i < 3; ++i) b.spec_t[i] = st != 1.0f ? d.specular_transmittance[i] * st : d.specular_transmittance[i];
+        b.flags = MTSG_F_GLOSSY_REFL | MTSG_F_GLOSSY_TRANS | MTSG_F_FRONT | MTSG_F_BACK;
+    }
+    return MTSGPU_OK;
+}
+
+// unitAngle (core/util.h:309-314)
+float unit_angle(V a, V b) {
+    if (dot(a, b) < 0) return kPi - 2 * std::asin(0.5f * length(b + a));
+    return 2 * std::asin(0.5f * length(b - a));
+}
+
+// coordinateSystem (util.cpp:592-601)
+void coordinate_system(V a, V &b, V &c) {
+    if (std::fabs(a.x) > std::fabs(a.y)) {
+        float invLen = 1.0f / std::sqrt(a.x * a.x + a.z * a.z);
+        c = v(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        float invLen = 1.0f / std::sqrt(a.y * a.y + a.z * a.z);
+        c = v(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    b = cross(c, a);
+}
+
+// ---- BVH2 (binned SAH) ------------------------------------------------------
+struct BBox {
+    float lo[3], hi[3];
+    void reset() { for (int a = 0; a < 3; ++a) { lo[a] = FLT_MAX; hi[a] = -FLT_MAX; } }
+    void grow(const BBox &b) { for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], b.lo[a]); hi[a] = std::max(hi[a], b.hi[a]); } }
+    void growp(const float *p) { for (int a = 0; a < 3; ++a) { lo[a] = std::min(lo[a], p[a]); hi[a] = std::max(hi[a], p[a]); } }
+    float area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (dx < 0) return 0;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct BuildPrim { BBox box; float c[3]; uint32_t id; };
+
+const uint32_t kMaxDepth = 28;   // traversal stack (LDS) holds < 32 entries
+
+struct Builder {
+    std::vector<BuildPrim> &prims;
+    std::vector<MtsgNode> &nodes;
+    std::vector<uint32_t> order;
+    float absEps;
+    uint32_t maxDepth = 0;
+    explicit Builder(std::vector<BuildPrim> &p, std::vector<MtsgNode> &n) : prims(p), nodes(n) {}
+
+    void inflate(BBox &b) const {
+        for (int a = 0; a < 3; ++a) {
+            float e = (b.hi[a] - b.lo[a]) * 1e-4f + 1e-6f * (std::fabs(b.lo[a]) + std::fabs(b.hi[a])) + absEps;
+            b.lo[a] -= e; b.hi[a] += e;
+        }
+    }
+    BBox bounds(uint32_t first, uint32_t count) const {
+        BBox b; b.reset();
+        for (uint32_t i = first; i < first + count; ++i) b.grow(prims[order[i]].box);
+        return b;
+    }
+    // returns child reference for the range
+    int32_t build(uint32_t first, uint32_t count, uint32_t depth) {
+        maxDepth = std::max(maxDepth, depth);
+        if (count <= 2 || (count <= MTSG_LEAF_MAX && depth >= kMaxDepth - 1))
+            return mtsg_leaf_ref(first, count);
+        // switch to median splits early enough that depth stays <= kMaxDepth
+        uint32_t lg = 0;
+        while ((2u << lg) * 2 < count) ++lg;   // ~log2(count / 2)
+        const bool forceMedian = depth + lg + 2 >= kMaxDepth;
+        BBox cb; cb.reset();
+        for (uint32_t i = first; i < first + count; ++i) cb.growp(prims[order[i]].c);
+        const int NB = 32;
+        float bestCost = FLT_MAX; int bestAxis = -1, bestSplit = -1;
+        const BBox nb = bounds(first, count);
+        const float leafCost = (float)count;
+        for (int axis = 0; axis < 3; ++axis) {
+            const float ext = cb.hi[axis] - cb.lo[axis];
+            if (!(ext > 0)) continue;
+            BBox bb[NB]; uint32_t bc[NB] = {0};
+            for (int i = 0; i < NB; ++i) bb[i].reset();
+            const float k = NB / ext;
+            for (uint32_t i = first; i < first + count; ++i) {
+                const BuildPrim &p = prims[order[i]];
+                int bi = std::min(NB - 1, (int)((p.c[axis] - cb.lo[axis]) * k));
+                bb[bi].grow(p.box); bc[bi]++;
+            }
+            BBox lb[NB]; uint32_t lc[NB];
+            BBox acc; acc.reset(); uint32_t n = 0;
+            for (int i = 0; i < NB; ++i) { acc.grow(bb[i]); n += bc[i]; lb[i] = acc; lc[i] = n; }
+            acc.reset(); n = 0;
+            for (int i = NB - 1; i > 0; --i) {
+                acc.grow(bb[i]); n += bc[i];
+                if (lc[i - 1] == 0 || n == 0) continue;
+                const float cost = 1.0f + (lb[i - 1].area() * lc[i - 1] + acc.area() * n) / std::max(nb.area(), 1e-30f);
+                if (cost < bestCost) { bestCost = cost; bestAxis = axis; bestSplit = i; }
+            }
+        }
+        uint32_t mid;
+        if (bestAxis < 0 || (count <= MTSG_LEAF_MAX && bestCost >= leafCost)) {
+            if (count <= MTSG_LEAF_MAX) return mtsg_leaf_ref(first, count);
+            // degenerate centroids: median split on index order
+            mid = first + count / 2;
+        } else {
+            const float ext = cb.hi[bestAxis] - cb.lo[bestAxis];
+            const float k = NB / ext;
+            auto it = std::partition(order.begin() + first, order.begin() + first + count, [&](uint32_t id) {
+                int bi = std::min(NB - 1, (int)((prims[id].c[bestAxis] - cb.lo[bestAxis]) * k));
+                return bi < bestSplit;
+            });
+            mid = (uint32_t)(it - order.begin());
+            if (mid == first || mid == first + count) mid = first + count / 2;
+        }
+        if (forceMedian) {
+            // keep the tree shallow: median split on the widest centroid axis
+            int axis = 0;
+            for (int a = 1; a < 3; ++a) if (cb.hi[a] - cb.lo[a] > cb.hi[axis] - cb.lo[axis]) axis = a;
+            mid = first + count / 2;
+            std::nth_element(order.begin() + first, order.begin() + mid, order.begin() + first + count,
+                             [&](uint32_t x, uint32_t y) { return prims[x].c[axis] < prims[y].c[axis]; });
+        }
+        const uint32_t id = (uint32_t)nodes.size();
+        nodes.push_back(MtsgNode());
+        BBox b0 = bounds(first, mid - first), b1 = bounds(mid, first + count - mid);
+        inflate(b0); inflate(b1);
+        const int32_t c0 = build(first, mid - first, depth + 1);
+        const int32_t c1 = build(mid, first + count - mid, depth + 1);
+        MtsgNode &n = nodes[id];
+        n.c0lox = b0.lo[0]; n.c0hix = b0.hi[0]; n.c0loy = b0.lo[1]; n.c0hiy = b0.hi[1];
+        n.c1lox = b1.lo[0]; n.c1hix = b1.hi[0]; n.c1loy = b1.lo[1]; n.c1hiy = b1.hi[1];
+        n.c0loz = b0.lo[2]; n.c0hiz = b0.hi[2]; n.c1loz = b1.lo[2]; n.c1hiz = b1.hi[2];
+        n.c0 = c0; n.c1 = c1; n.pad0 = n.pad1 = 0;
+        return (int32_t)id;
+    }
+};
+
+}  // namespace
+
+// ---- Sobol ------------------------------------------------------------------
+const std::vector<uint32_t> &mtsg_sobol_matrices() {
+    static std::vector<uint32_t> M;
+    if (!M.empty()) return M;
+    M.assign((size_t)MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE, 0u);
+    for (int k = 0; k < MTSG_SOBOL_SIZE; ++k) M[k] = (uint32_t)(((uint64_t)1 << (MTSG_SOBOL_SIZE - 1 - k)) >> 20);
+    const size_t n = sizeof(kJoeKuoParams) / sizeof(kJoeKuoParams[0]);
+    size_t i = 0;
+    uint64_t m[MTSG_SOBOL_SIZE];
+    while (i < n) {
+        const uint32_t d = kJoeKuoParams[i], s = kJoeKuoParams[i + 1], a = kJoeKuoParams[i + 2];
+        for (uint32_t t = 0; t < s; ++t) m[t] = kJoeKuoParams[i + 3 + t];
+        i += 3 + s;
+        // Sobol' recurrence: m_k = 2a_1 m_{k-1} ^ ... ^ 2^{s-1} a_{s-1} m_{k-s+1} ^ 2^s m_{k-s} ^ m_{k-s}
+        for (uint32_t k = s; k < MTSG_SOBOL_SIZE; ++k) {
+            uint64_t val = m[k - s] ^ (m[k - s] << s);
+            for (uint32_t t = 1; t < s; ++t)
+                if ((a >> (s - 1 - t)) & 1) val ^= m[k - t] << t;
+            m[k] = val;
+        }
+        for (int k = 0; k < MTSG_SOBOL_SIZE; ++k)
+            M[(size_t)(d - 1) * MTSG_SOBOL_SIZE + k] = (uint32_t)((m[k] << (MTSG_SOBOL_SIZE - 1 - k)) >> 20);
+    }
+    return M;
+}
+
+void mtsg_sobol_lookup_table(uint32_t m, MtsgLookup &L) {
+    std::memset(&L, 0, sizeof L);
+    L.m = m;
+    if (m <= 1 || m > 31) return;
+    const std::vector<uint32_t> &M = mtsg_sobol_matrices();
+    for (int b = 0; b < 64; ++b) L.ycol[b] = b < MTSG_SOBOL_SIZE ? (M[MTSG_SOBOL_SIZE + b] >> (32 - m)) : 0u;
+    uint32_t A[32], I[32];
+    for (uint32_t r = 0; r < m; ++r) {
+        A[r] = 0; I[r] = 1u << r;
+        for (uint32_t t = 0; t < m; ++t) A[r] |= ((L.ycol[m + t] >> r) & 1u) << t;
+    }
+    for (uint32_t c = 0; c < m; ++c) {
+        uint32_t piv = c;
+        while (piv < m && !((A[piv] >> c) & 1u)) ++piv;
+        if (piv == m) continue;   // cannot happen for a (0,2)-sequence
+        std::swap(A[c], A[piv]); std::swap(I[c], I[piv]);
+        for (uint32_t r = 0; r < m; ++r)
+            if (r != c && ((A[r] >> c) & 1u)) { A[r] ^= A[c]; I[r] ^= I[c]; }
+    }
+    for (uint32_t t = 0; t < m; ++t) L.inv[t] = I[t];
+}
+
+uint64_t mtsg_sample_tea(uint32_t v0, uint32_t v1, int rounds) {   // core/qmc.h:146-156
+    uint32_t sum = 0;
+    for (int i = 0; i < rounds; ++i) {
+        sum += 0x9e3779b9;
+        v0 += ((v1 << 4) + 0xA341316C) ^ (v1 + sum) ^ ((v1 >> 5) + 0xC8013EA4);
+        v1 += ((v0 << 4) + 0xAD90777D) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7E95761E);
+    }
+    return ((uint64_t)v1 << 32) + v0;
+}
+
+// ---- reconstruction filter (libcore/rfilter.cpp:37-55, rfilters/box.cpp, gaussian.cpp) ----
+int mtsg_configure_filter(int32_t type, float param, MtsgFilter &f, std::string &err) {
+    float stddev = 0;
+    std::memset(&f, 0, sizeof f);
+    f.type = type;
+    if (type == MTSGPU_RFILTER_BOX) f.radius = param + 1e-5f;
+    else if (type == MTSGPU_RFILTER_GAUSSIAN) { stddev = param; f.radius = 4 * stddev; }
+    else { err = "unknown reconstruction filter"; return MTSGPU_EINVAL; }
+    if (!(f.radius > 0)) { err = "filter radius must be positive"; return MTSGPU_EINVAL; }
+    float sum = 0.0f;
+    for (int i = 0; i < MTSG_FILTER_RES; ++i) {
+        float x = (f.radius * i) / MTSG_FILTER_RES, value;
+        if (type == MTSGPU_RFILTER_BOX) {
+            value = std::fabs(x) <= f.radius ? 1.0f : 0.0f;
+        } else {
+            float alpha = -1.0f / (2.0f * stddev * stddev);
+            value = fmax_std(0.0f, (float)std::exp((double)(alpha * x * x)) -
+                                       (float)std::exp((double)(alpha * f.radius * f.radius)));
+        }
+        f.values[i] = value;
+        sum += value;
+    }
+    f.values[MTSG_FILTER_RES] = 0.0f;
+    f.scale = MTSG_FILTER_RES / f.radius;
+    f.border = (int)std::ceil(f.radius - 0.5f);
+    sum *= 2 * f.radius / MTSG_FILTER_RES;
+    float normalization = 1.0f / sum;
+    for (int i = 0; i < MTSG_FILTER_RES; ++i) f.values[i] *= normalization;
+    return MTSGPU_OK;
+}
+
+// ---- scene ---------------------------------------------------------------
+int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &err) {
+    if (!D) { err = "null scene"; return MTSGPU_EINVAL; }
+    S = HostScene();
+    int rc = configure_camera(D->sensor, S.cam, err);
+    if (rc) return rc;
+    S.film_w = D->sensor.film_width;
+    S.film_h = D->sensor.film_height;
+    const uint32_t nb = D->num_bsdfs;
+    S.bsdfs.resize(nb + 2);
+    for (uint32_t i = 0; i < nb; ++i)
+        if ((rc = configure_bsdf(D->bsdfs[i], S.bsdfs[i], err))) return rc;
+    {   // Shape::configure defaults (shape.cpp:48-70): black for emitters, 0.5 otherwise
+        mtsgpu_bsdf_desc dd; std::memset(&dd, 0, sizeof dd);
+        dd.type = MTSGPU_BSDF_DIFFUSE; dd.ensure_energy_conservation = 1;
+        configure_bsdf(dd, S.bsdfs[nb], err);
+        dd.reflectance[0] = dd.reflectance[1] = dd.reflectance[2] = 0.5f;
+        configure_bsdf(dd, S.bsdfs[nb + 1], err);
+    }
+    if (D->num_emitters == 0) { err = "scene has no emitters (the sunsky fallback is out of scope)"; return MTSGPU_EINVAL; }
+    S.emitters.resize(D->num_emitters);
+    for (uint32_t i = 0; i < D->num_emitters; ++i) {
+        const mtsgpu_emitter_desc &e = D->emitters[i];
+        MtsgEmitter &o = S.emitters[i];
+        std::memset(&o, 0, sizeof o);
+        o.type = e.type;
+        o.shape = -1;
+        o.weight = e.sampling_weight;
+        for (int k = 0; k < 3; ++k) o.radiance[k] = e.radiance[k];
+        if (e.type != MTSGPU_EMITTER_AREA) { err = "only area emitters are supported in this build"; return MTSGPU_EINVAL; }
+    }
+    // meshes
+    uint32_t prims = 0, verts = 0;
+    for (uint32_t i = 0; i < D->num_meshes; ++i) {
+        const mtsgpu_mesh_desc &m = D->meshes[i];
+        if (m.num_triangles == 0 || !m.positions || !m.indices) { err = "Encountered an empty triangle mesh!"; return MTSGPU_EINVAL; }
+        prims += m.num_triangles; verts += m.num_vertices;
+    }
+    S.positions.resize((size_t)verts * 3);
+    S.normals.assign((size_t)verts * 3, 0.0f);
+    S.prim_vtx.resize((size_t)prims * 4);
+    S.dpdu.resize((size_t)prims * 3);
+    S.shapes.resize(D->num_meshes);
+    std::vector<BuildPrim> bp(prims);
+    std::vector<MtsgTri> tacc(prims);
+    float amin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, amax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    uint32_t voff = 0, poff = 0;
+    for (uint32_t si = 0; si < D->num_meshes; ++si) {
+        const mtsgpu_mesh_desc &m = D->meshes[si];
+        const uint32_t nv = m.num_vertices, nt = m.num_triangles;
+        std::vector<V> P(nv), N;
+        for (uint32_t k = 0; k < nv; ++k) P[k] = v(m.positions[3 * k], m.positions[3 * k + 1], m.positions[3 * k + 2]);
+        std::vector<uint32_t> idx(m.indices, m.indices + 3 * (size_t)nt);
+        for (uint32_t k = 0; k < 3 * nt; ++k)
+            if (idx[k] >= nv) { err = "triangle index out of range"; return MTSGPU_EINVAL; }
+        MtsgShape &sh = S.shapes[si];
+        sh.emitter = m.emitter;
+        if (m.emitter >= (int)D->num_emitters) { err = "emitter index out of range"; return MTSGPU_EINVAL; }
+        if (m.bsdf >= (int)nb) { err = "bsdf index out of range"; return MTSGPU_EINVAL; }
+        sh.bsdf = m.bsdf >= 0 ? m.bsdf : (m.emitter >= 0 ? (int)nb : (int)nb + 1);
+        // TriMesh::computeNormals (trimesh.cpp:608-681)
+        bool hasNormals = false;
+        if (m.face_normals) {
+            if (m.flip_normals)
+                for (uint32_t t = 0; t < nt; ++t) std::swap(idx[3 * t], idx[3 * t + 1]);
+        } else if (m.normals) {
+            hasNormals = true;
+            N.resize(nv);
+            for (uint32_t k = 0; k < nv; ++k) {
+                N[k] = v(m.normals[3 * k], m.normals[3 * k + 1], m.normals[3 * k + 2]);
+                if (m.flip_normals) N[k] = N[k] * -1;
+            }
+        } else {
+            hasNormals = true;
+            N.assign(nv, v(0, 0, 0));
+            for (uint32_t t = 0; t < nt; t++) {
+                V n = v(0, 0, 0);
+                for (int j = 0; j < 3; ++j) {
+                    const V v0 = P[idx[3 * t + j]], v1 = P[idx[3 * t + (j + 1) % 3]], v2 = P[idx[3 * t + (j + 2) % 3]];
+                    const V sideA = v1 - v0, sideB = v2 - v0;
+                    if (j == 0) {
+                        n = cross(sideA, sideB);
+                        float len = length(n);
+                        if (len == 0) break;
+                        n = vdiv(n, len);
+                    }
+                    float angle = unit_angle(normalize(sideA), normalize(sideB));
+                    N[idx[3 * t + j]] = N[idx[3 * t + j]] + n * angle;
+                }
+            }
+            for (uint32_t k = 0; k < nv; k++) {
+                float len = length(N[k]);
+                if (m.flip_normals) len *= -1;
+                if (len != 0) N[k] = vdiv(N[k], len);
+                else N[k] = v(1, 0, 0);
+            }
+        }
+        sh.has_normals = hasNormals ? 1 : 0;
+        for (uint32_t k = 0; k < nv; ++k) {
+            S.positions[3 * (voff + k)] = P[k].x; S.positions[3 * (voff + k) + 1] = P[k].y; S.positions[3 * (voff + k) + 2] = P[k].z;
+            if (hasNormals) {
+                S.normals[3 * (voff + k)] = N[k].x; S.normals[3 * (voff + k) + 1] = N[k].y; S.normals[3 * (voff + k) + 2] = N[k].z;
+            }
+        }
+        // TriMesh::computeUVTangents (trimesh.cpp:683-739); dpdu = p1 - p0 without texcoords (skdtree.h:376-382)
+        for (uint32_t t = 0; t < nt; ++t) {
+            const uint32_t i0 = idx[3 * t], i1 = idx[3 * t + 1], i2 = idx[3 * t + 2];
+            const V v0 = P[i0], v1 = P[i1], v2 = P[i2];
+            V dp = v1 - v0;
+            if (m.texcoords) {
+                dp = v(0, 0, 0);
+                const float *uv = m.texcoords;
+                const V dP1 = v1 - v0, dP2 = v2 - v0;
+                const float du1 = uv[2 * i1] - uv[2 * i0], dv1 = uv[2 * i1 + 1] - uv[2 * i0 + 1];
+                const float du2 = uv[2 * i2] - uv[2 * i0], dv2 = uv[2 * i2 + 1] - uv[2 * i0 + 1];
+                const V n = cross(dP1, dP2);
+                const float len = length(n);
+                if (len != 0) {
+                    const float det = du1 * dv2 - dv1 * du2;
+                    if (det == 0) {
+                        V b, c;
+                        coordinate_system(vdiv(n, len), b, c);
+                        dp = b;
+                    } else {
+                        const float invDet = 1.0f / det;
+                        dp = (dP1 * dv2 - dP2 * dv1) * invDet;
+                    }
+                }
+            }
+            const uint32_t p = poff + t;
+            S.dpdu[3 * p] = dp.x; S.dpdu[3 * p + 1] = dp.y; S.dpdu[3 * p + 2] = dp.z;
+            S.prim_vtx[4 * p] = voff + i0; S.prim_vtx[4 * p + 1] = voff + i1; S.prim_vtx[4 * p + 2] = voff + i2;
+            S.prim_vtx[4 * p + 3] = si;
+            // TriAccel::load (triaccel.h:58-90)
+            MtsgTri &ta = tacc[p];
+            std::memset(&ta, 0, sizeof ta);
+            static const int waldModulo[4] = {1, 2, 0, 1};
+            const V A = v0, B = v1, C = v2;
+            const V b = C - A, c = B - A, Nn = cross(c, b);
+            ta.k = 0;
+            for (int j = 0; j < 3; j++)
+                if (std::fabs(at(Nn, j)) > std::fabs(at(Nn, (int)ta.k))) ta.k = (uint32_t)j;
+            const int u = waldModulo[ta.k], w = waldModulo[ta.k + 1];
+            const float n_k = at(Nn, (int)ta.k), denom = at(b, u) * at(c, w) - at(b, w) * at(c, u);
+            if (denom == 0) {
+                ta.k = 3;
+            } else {
+                ta.n_u = at(Nn, u) / n_k;
+                ta.n_v = at(Nn, w) / n_k;
+                ta.n_d = dot(A, Nn) / n_k;
+                ta.b_nu = at(b, u) / denom;
+                ta.b_nv = -at(b, w) / denom;
+                ta.a_u = at(A, u);
+                ta.a_v = at(A, w);
+                ta.c_nu = at(c, w) / denom;
+                ta.c_nv = -at(c, u) / denom;
+            }
+            ta.prim = p;
+            ta.shape = si;
+            BuildPrim &q = bp[p];
+            q.id = p;
+            q.box.reset();
+            const float pa[3] = {A.x, A.y, A.z}, pb[3] = {B.x, B.y, B.z}, pc[3] = {C.x, C.y, C.z};
+            q.box.growp(pa); q.box.growp(pb); q.box.growp(pc);
+            for (int a = 0; a < 3; ++a) {
+                q.c[a] = 0.5f * (q.box.lo[a] + q.box.hi[a]);
+                amin[a] = std::min(amin[a], q.box.lo[a]);
+                amax[a] = std::max(amax[a], q.box.hi[a]);
+            }
+        }
+        if (m.emitter >= 0) {
+            MtsgEmitter &e = S.emitters[m.emitter];
+            if (e.shape >= 0) { err = "Tried to attach multiple emitters to a shape!"; return MTSGPU_EINVAL; }
+            e.shape = (int)si;
+            e.tri_first = poff;
+            e.tri_count = nt;
+            e.cdf_offset = (uint32_t)S.area_cdf.size();
+            // TriMesh::prepareSamplingTable (trimesh.cpp:389-404), DiscreteDistribution (pmf.h)
+            std::vector<float> cdf(nt + 1);
+            cdf[0] = 0.0f;
+            for (uint32_t t = 0; t < nt; ++t) {
+                const V p0 = P[idx[3 * t]], p1 = P[idx[3 * t + 1]], p2 = P[idx[3 * t + 2]];
+                cdf[t + 1] = cdf[t] + 0.5f * length(cross(p1 - p0, p2 - p0));   // Triangle::surfaceArea
+            }
+            const float sum = cdf[nt];
+            if (sum > 0) {
+                const float norm = 1.0f / sum;
+                for (uint32_t t = 1; t < nt + 1; ++t) cdf[t] *= norm;
+                cdf[nt] = 1.0f;
+            }
+            e.inv_area = 1.0f / sum;
+            S.area_cdf.insert(S.area_cdf.end(), cdf.begin(), cdf.end());
+        }
+        voff += nv;
+        poff += nt;
+    }
+    for (const MtsgEmitter &e : S.emitters)
+        if (e.type == MTSGPU_EMITTER_AREA && e.shape < 0) { err = "area emitter without a shape"; return MTSGPU_EINVAL; }
+    // emitter PDF (scene.cpp:376-381)
+    S.em_cdf.assign(S.emitters.size() + 1, 0.0f);
+    for (size_t i = 0; i < S.emitters.size(); ++i) S.em_cdf[i + 1] = S.em_cdf[i] + S.emitters[i].weight;
+    {
+        const size_t n = S.emitters.size();
+        const float sum = S.em_cdf[n];
+        if (sum > 0) {
+            S.em_norm = 1.0f / sum;
+            for (size_t i = 1; i < n + 1; ++i) S.em_cdf[i] *= S.em_norm;
+            S.em_cdf[n] = 1.0f;
+        } else {
+            S.em_norm = 0.0f;
+        }
+    }
+    // scene bounds, slightly enlarged (gkdtree.h:1211-1217)
+    const float eps = 1e-3f;
+    for (int a = 0; a < 3; ++a) {
+        amin[a] -= (amax[a] - amin[a]) * eps + eps;
+        amax[a] += (amax[a] - amin[a]) * eps + eps;
+        S.aabb_min[a] = amin[a]; S.aabb_max[a] = amax[a];
+    }
+    // BVH
+    Builder B(bp, S.nodes);
+    B.order.resize(prims);
+    for (uint32_t i = 0; i < prims; ++i) B.order[i] = i;
+    float diag = 0;
+    for (int a = 0; a < 3; ++a) diag += (amax[a] - amin[a]) * (amax[a] - amin[a]);
+    B.absEps = 1e-7f * std::sqrt(diag) + 1e-30f;
+    S.nodes.reserve(prims + 2);
+    const int32_t rootRef = B.build(0, prims, 0);   // the first inner node created is node 0
+    if (rootRef < 0) {
+        // whole scene in one leaf: a root node holding that leaf and an empty one
+        BBox b = B.bounds(0, prims);
+        B.inflate(b);
+        MtsgNode n;
+        n.c0lox = b.lo[0]; n.c0hix = b.hi[0]; n.c0loy = b.lo[1]; n.c0hiy = b.hi[1]; n.c0loz = b.lo[2]; n.c0hiz = b.hi[2];
+        n.c1lox = n.c1hix = n.c1loy = n.c1hiy = n.c1loz = n.c1hiz = 0;
+        n.c0 = rootRef; n.c1 = mtsg_leaf_ref(0, 0); n.pad0 = n.pad1 = 0;
+        S.nodes.push_back(n);
+    }
+    S.bvh_depth = B.maxDepth;
+    if (B.maxDepth + 1 >= 32) { err = "BVH too deep for the traversal stack"; return MTSGPU_EINVAL; }
+    // triangles in leaf order
+    S.tris.resize(prims);
+    for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];
+    return MTSGPU_OK;
+}

@@ -1,0 +1,142 @@
+"""`PathTracer`: the host-side mirror of the reference's `path` Integrator plugin.
+
+Mirrors MIPathTracer / MonteCarloIntegrator (src/integrators/path/path.cpp:110-
+117, src/librender/integrator.cpp:190-225): same property names and the same
+errors (raised as ValueError where the reference calls Log(EError)).  Rendering
+goes through libmtsgpu.so's C-ABI; there is no CPU fallback -- without the HIP
+library or a gfx950 device every call raises `NativeUnavailable`.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import LIB_PATH, abi
+from .scene import PathIntegrator, film_border
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class MtsgpuError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__('%s (%d): %s' % (abi.STATUS_NAMES.get(code, '?'), code, msg))
+        self.code = code
+
+
+EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
+           'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info']
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libmtsgpu.so (the in-tree build).  Raises NativeUnavailable if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise NativeUnavailable('libmtsgpu.so not built: %s (run __graft_entry__.build())' % p)
+    L = C.CDLL(p)
+    P = C.POINTER
+    L.mtsgpu_create.argtypes = [C.c_int, P(C.c_void_p)]
+    L.mtsgpu_upload_scene.argtypes = [C.c_void_p, P(abi.SceneDesc)]
+    L.mtsgpu_film_border.argtypes = [C.c_int32, C.c_float]
+    L.mtsgpu_render.argtypes = [C.c_void_p, P(abi.RenderParams), P(C.c_float), P(C.c_float), P(abi.Stats)]
+    L.mtsgpu_render_device.argtypes = [C.c_void_p, P(abi.RenderParams), C.c_void_p, C.c_void_p, P(abi.Stats)]
+    L.mtsgpu_last_error.argtypes = [C.c_void_p]
+    L.mtsgpu_last_error.restype = C.c_char_p
+    L.mtsgpu_destroy.argtypes = [C.c_void_p]
+    L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
+    L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
+    if L.mtsgpu_abi_version() != 1:
+        raise NativeUnavailable('ABI version mismatch')
+    if path is None:
+        _lib = L
+    return L
+
+
+class Context:
+    """One libmtsgpu context (one HIP device)."""
+
+    def __init__(self, device=-1):
+        self.L = load_library()
+        h = C.c_void_p()
+        rc = self.L.mtsgpu_create(device, C.byref(h))
+        if rc != 0:
+            raise NativeUnavailable('mtsgpu_create failed: %s' % self.L.mtsgpu_last_error(None).decode())
+        self.h = h
+        self.scene = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise MtsgpuError(rc, self.L.mtsgpu_last_error(self.h).decode())
+
+    def upload(self, scene):
+        d = scene.desc()
+        self._check(self.L.mtsgpu_upload_scene(self.h, C.byref(d)))
+        self.scene = scene
+
+    def scene_info(self):
+        info = (C.c_uint32 * 4)()
+        self._check(self.L.mtsgpu_debug_scene_info(self.h, info))
+        return {'nodes': info[0], 'prims': info[1], 'depth': info[2], 'cus': info[3]}
+
+    def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False):
+        """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict)."""
+        sc = self.scene
+        W, H = sc.sensor.width, sc.sensor.height
+        x0, y0, w, h = window if window else (0, 0, W, H)
+        p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+        if traversal_stats:
+            p.flags |= abi.FLAG_TRAVERSAL_STATS
+        b = film_border(integ.rfilter, integ.rfilterParam)
+        film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
+        smp = np.zeros((w * h * integ.sampleCount, abi.SAMPLE_RECORD_FLOATS), np.float32) if samples else None
+        st = abi.Stats()
+        self._check(self.L.mtsgpu_render(self.h, C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)),
+                                          smp.ctypes.data_as(C.POINTER(C.c_float)) if samples else None,
+                                          C.byref(st)))
+        return film, smp, st.as_dict()
+
+    def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0)):
+        sc = self.scene
+        W, H = sc.sensor.width, sc.sensor.height
+        x0, y0, w, h = window if window else (0, 0, W, H)
+        p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+        st = abi.Stats()
+        self._check(self.L.mtsgpu_render_device(self.h, C.byref(p), C.c_void_p(film_ptr),
+                                                 C.c_void_p(stream_ptr) if stream_ptr else None, C.byref(st)))
+        return st.as_dict()
+
+    def debug_arith(self, a, b):
+        a = np.ascontiguousarray(a, np.float32)
+        b = np.ascontiguousarray(b, np.float32)
+        out = np.zeros((a.size, 8), np.float32)
+        self._check(self.L.mtsgpu_debug_arith(self.h, abi.fptr(a), abi.fptr(b), abi.fptr(out), a.size))
+        return out
+
+    def close(self):
+        if self.h:
+            self.L.mtsgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PathTracer(PathIntegrator):
+    """The `path` integrator (MIPathTracer) running on MI355X."""
+
+    def render(self, scene, ctx=None):
+        ctx = ctx or Context()
+        if ctx.scene is not scene:
+            ctx.upload(scene)
+        film, _, stats = ctx.render(self)
+        return film, stats

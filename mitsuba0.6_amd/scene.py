@@ -1,0 +1,252 @@
+"""Host-side scene model mirroring the reference's plugin properties.
+
+A `Scene` holds what Mitsuba 0.6 has after parsing and plugin construction
+(SceneHandler -> PluginManager::createObject, src/librender/scenehandler.cpp):
+world-space triangle meshes (the TriMesh that the obj/ply/serialized/cube shape
+plugins produce, with their `toWorld` already applied), BSDF and emitter
+parameters under the reference's property names, the perspective sensor, the
+film and the sampler.  `Scene.desc()` packs it into the C-ABI structs of
+include/mtsgpu.h; everything the reference derives in configure() is derived
+behind the ABI by libmtsgpu.so.
+"""
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import abi
+
+# IOR table entries used by the configs (src/bsdfs/ior.h:40-67)
+IOR = {'vacuum': 1.0, 'air': 1.000277, 'water': 1.3330, 'bk7': 1.5046, 'glass': 1.5046,
+       'diamond': 2.419, 'polypropylene': 1.49, 'acrylic glass': 1.49, 'fused quartz': 1.458}
+
+
+def lookup_ior(v):
+    if isinstance(v, str):
+        return IOR[v.lower()]
+    return float(v)
+
+
+@dataclass
+class BSDF:
+    """One of diffuse / roughconductor / roughdielectric with Mitsuba property names."""
+    type: str = 'diffuse'
+    reflectance: tuple = (0.5, 0.5, 0.5)
+    distribution: str = 'beckmann'
+    alpha: Optional[float] = None
+    alphaU: Optional[float] = None
+    alphaV: Optional[float] = None
+    sampleVisible: bool = True
+    specularReflectance: tuple = (1.0, 1.0, 1.0)
+    specularTransmittance: tuple = (1.0, 1.0, 1.0)
+    eta: tuple = (0.0, 0.0, 0.0)       # roughconductor RGB eta (see conductors.py)
+    k: tuple = (1.0, 1.0, 1.0)
+    material: Optional[str] = 'Cu'
+    extEta: object = 'air'
+    intIOR: object = 'bk7'
+    extIOR: object = 'air'
+    ensureEnergyConservation: bool = True
+
+    def to_desc(self):
+        d = abi.BsdfDesc()
+        d.type = {'diffuse': abi.BSDF_DIFFUSE, 'roughconductor': abi.BSDF_ROUGHCONDUCTOR,
+                  'roughdielectric': abi.BSDF_ROUGHDIELECTRIC}[self.type]
+        d.distribution = {'beckmann': abi.DISTR_BECKMANN, 'ggx': abi.DISTR_GGX,
+                          'phong': abi.DISTR_PHONG, 'as': abi.DISTR_PHONG}[self.distribution.lower()]
+        d.sample_visible = int(self.sampleVisible)
+        d.ensure_energy_conservation = int(self.ensureEnergyConservation)
+        # MicrofacetDistribution(props) defaults alphaU = alphaV = 0.1 (microfacet.h:99-101,117-130)
+        if self.alpha is not None:
+            au = av = float(self.alpha)
+        elif self.alphaU is not None or self.alphaV is not None:
+            if self.alphaU is None or self.alphaV is None:
+                raise ValueError("Microfacet model: both 'alphaU' and 'alphaV' must be specified.")
+            au, av = float(self.alphaU), float(self.alphaV)
+        else:
+            au = av = 0.1
+        d.alpha_u, d.alpha_v = au, av
+        d.reflectance[:] = self.reflectance
+        d.specular_reflectance[:] = self.specularReflectance
+        d.specular_transmittance[:] = self.specularTransmittance
+        if self.type == 'roughconductor':
+            if self.material is not None and self.material.lower() == 'none':
+                eta, k = (0.0, 0.0, 0.0), (1.0, 1.0, 1.0)
+            elif self.material is not None:
+                from .conductors import conductor_rgb
+                eta, k = conductor_rgb(self.material)
+            else:
+                eta, k = self.eta, self.k
+            d.eta[:] = eta
+            d.k[:] = k
+        d.ext_eta = lookup_ior(self.extEta)
+        d.int_ior = lookup_ior(self.intIOR)
+        d.ext_ior = lookup_ior(self.extIOR)
+        return d
+
+
+@dataclass
+class Emitter:
+    type: str = 'area'
+    radiance: tuple = (1.0, 1.0, 1.0)
+    samplingWeight: float = 1.0
+
+    def to_desc(self):
+        d = abi.EmitterDesc()
+        d.type = {'area': abi.EMITTER_AREA, 'envmap': abi.EMITTER_ENVMAP}[self.type]
+        d.radiance[:] = self.radiance
+        d.sampling_weight = self.samplingWeight
+        d.env_scale = 1.0
+        return d
+
+
+@dataclass
+class Mesh:
+    positions: np.ndarray                 # (n,3) float32, world space
+    indices: np.ndarray                   # (m,3) uint32
+    normals: Optional[np.ndarray] = None
+    texcoords: Optional[np.ndarray] = None
+    bsdf: int = -1
+    emitter: int = -1
+    faceNormals: bool = False
+    flipNormals: bool = False
+    name: str = ''
+
+
+@dataclass
+class Sensor:
+    fov: float = 39.3077
+    fovAxis: str = 'x'
+    nearClip: float = 1e-2
+    farClip: float = 1e4
+    toWorld: np.ndarray = field(default_factory=lambda: np.eye(4, dtype=np.float32))
+    width: int = 768
+    height: int = 576
+
+
+def look_at(origin, target, up):
+    """Transform::lookAt (src/libcore/transform.cpp:191-214), float32."""
+    p = np.asarray(origin, np.float32)
+    t = np.asarray(target, np.float32)
+    up = np.asarray(up, np.float32)
+
+    def normalize(v):
+        ln = np.float32(np.sqrt(np.float32(v[0] * v[0] + v[1] * v[1]) + np.float32(v[2] * v[2])))
+        r = np.float32(1.0) / ln
+        return (v * r).astype(np.float32)
+
+    def cross(a, b):
+        return np.array([a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2],
+                         a[0] * b[1] - a[1] * b[0]], np.float32)
+    d = normalize((t - p).astype(np.float32))
+    left = normalize(cross(up, d))
+    new_up = cross(d, left)
+    m = np.zeros((4, 4), np.float32)
+    m[:3, 0], m[:3, 1], m[:3, 2], m[:3, 3] = left, new_up, d, p
+    m[3, 3] = 1
+    return m
+
+
+class Scene:
+    """Scene after plugin construction (the C-ABI scene description)."""
+
+    def __init__(self, sensor: Sensor, meshes: List[Mesh], bsdfs: List[BSDF], emitters: List[Emitter], name=''):
+        self.sensor, self.meshes, self.bsdfs, self.emitters, self.name = sensor, meshes, bsdfs, emitters, name
+
+    @property
+    def num_triangles(self):
+        return sum(int(m.indices.shape[0]) for m in self.meshes)
+
+    def desc(self):
+        """Pack into abi.SceneDesc; the returned object keeps every buffer alive."""
+        keep = []
+        md = (abi.MeshDesc * len(self.meshes))()
+        for i, m in enumerate(self.meshes):
+            pos = np.ascontiguousarray(m.positions, np.float32)
+            idx = np.ascontiguousarray(m.indices, np.uint32)
+            nrm = None if m.normals is None else np.ascontiguousarray(m.normals, np.float32)
+            uv = None if m.texcoords is None else np.ascontiguousarray(m.texcoords, np.float32)
+            keep += [pos, idx, nrm, uv]
+            md[i].positions = abi.fptr(pos)
+            md[i].normals = abi.fptr(nrm)
+            md[i].texcoords = abi.fptr(uv)
+            md[i].indices = abi.uptr(idx)
+            md[i].num_vertices = pos.shape[0]
+            md[i].num_triangles = idx.shape[0]
+            md[i].bsdf, md[i].emitter = m.bsdf, m.emitter
+            md[i].face_normals, md[i].flip_normals = int(m.faceNormals), int(m.flipNormals)
+        bd = (abi.BsdfDesc * max(1, len(self.bsdfs)))()
+        for i, b in enumerate(self.bsdfs):
+            bd[i] = b.to_desc()
+        ed = (abi.EmitterDesc * max(1, len(self.emitters)))()
+        for i, e in enumerate(self.emitters):
+            ed[i] = e.to_desc()
+            if getattr(e, 'env_rgb', None) is not None:
+                img = np.ascontiguousarray(e.env_rgb, np.float32)
+                keep.append(img)
+                ed[i].env_rgb = abi.fptr(img)
+                ed[i].env_height, ed[i].env_width = img.shape[0], img.shape[1]
+        d = abi.SceneDesc()
+        d.meshes, d.num_meshes = md, len(self.meshes)
+        d.bsdfs, d.num_bsdfs = bd, len(self.bsdfs)
+        d.emitters, d.num_emitters = ed, len(self.emitters)
+        s = self.sensor
+        d.sensor.fov = s.fov
+        d.sensor.fov_axis = {'x': abi.FOV_X, 'y': abi.FOV_Y, 'diagonal': abi.FOV_DIAGONAL,
+                             'smaller': abi.FOV_SMALLER, 'larger': abi.FOV_LARGER}[s.fovAxis]
+        d.sensor.near_clip, d.sensor.far_clip = s.nearClip, s.farClip
+        d.sensor.to_world[:] = [float(x) for x in np.asarray(s.toWorld, np.float32).reshape(-1)]
+        d.sensor.film_width, d.sensor.film_height = s.width, s.height
+        d._keep = (keep, md, bd, ed)
+        return d
+
+
+@dataclass
+class PathIntegrator:
+    """Properties of the reference `path` plugin (MonteCarloIntegrator ctor,
+    src/librender/integrator.cpp:190-225) plus sampler/film settings."""
+    maxDepth: int = -1
+    rrDepth: int = 5
+    strictNormals: bool = False
+    hideEmitters: bool = False
+    sampleCount: int = 4           # sobol 'sampleCount' (sobol.cpp:87)
+    scramble: int = 0
+    rfilter: str = 'gaussian'      # film default (film.cpp:93)
+    rfilterParam: float = 0.5      # box radius / gaussian stddev
+    hasAlpha: bool = False         # hdrfilm pixelFormat default "rgb" (hdrfilm.cpp:216)
+
+    def __post_init__(self):
+        if self.rrDepth <= 0:
+            raise ValueError("'rrDepth' must be set to a value greater than zero!")
+        if self.maxDepth <= 0 and self.maxDepth != -1:
+            raise ValueError("'maxDepth' must be set to -1 (infinite) or a value greater than zero!")
+
+    def params(self, width, height, x0=0, y0=0, w=None, h=None, row_block=0, row_stride=1, row_phase=0):
+        p = abi.RenderParams()
+        p.spp = self.sampleCount
+        p.scramble = self.scramble
+        p.max_depth, p.rr_depth = self.maxDepth, self.rrDepth
+        p.strict_normals, p.hide_emitters = int(self.strictNormals), int(self.hideEmitters)
+        p.has_alpha = int(self.hasAlpha)
+        p.rfilter = {'box': abi.RFILTER_BOX, 'gaussian': abi.RFILTER_GAUSSIAN}[self.rfilter]
+        p.rfilter_param = self.rfilterParam
+        p.x0, p.y0 = x0, y0
+        p.width = width - x0 if w is None else w
+        p.height = height - y0 if h is None else h
+        p.row_block, p.row_stride, p.row_phase = row_block, row_stride, row_phase
+        return p
+
+
+def film_border(rfilter, param):
+    """ReconstructionFilter border size (rfilter.cpp:50)."""
+    import math
+    radius = np.float32(param) + np.float32(1e-5) if rfilter == 'box' else np.float32(4) * np.float32(param)
+    return int(math.ceil(np.float32(radius - np.float32(0.5))))
+
+
+def develop(film, border):
+    """Divide accumulated RGB by the filter weight (film develop); returns (H,W,3)."""
+    f = film[border:film.shape[0] - border, border:film.shape[1] - border]
+    w = f[..., 4:5]
+    with np.errstate(divide='ignore', invalid='ignore'):
+        rgb = np.where(w != 0, f[..., :3] / w, 0.0)
+    return rgb.astype(np.float32)

@@ -1,0 +1,66 @@
+"""TEST INFRASTRUCTURE: ctypes binding of the CPU oracle (oracle/_build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, '_build', 'liboracle.so')
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        import sys
+        sys.path.insert(0, os.path.dirname(HERE))
+        from pkgimport import mitsuba_amd
+        m = mitsuba_amd()
+        abi = m.abi
+        L = C.CDLL(LIB)
+        L.oracle_sobol_init.argtypes = [C.c_char_p]
+        L.oracle_render.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.RenderParams),
+                                    C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(abi.Stats),
+                                    C.c_int, C.c_int]
+        L.oracle_sobol_sample.restype = C.c_float
+        L.oracle_sobol_sample.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.oracle_sobol_lookup.restype = C.c_uint64
+        L.oracle_sobol_lookup.argtypes = [C.c_uint32] * 4 + [C.c_uint64]
+        L.oracle_sobol_matrix.restype = C.c_uint32
+        L.oracle_sobol_matrix.argtypes = [C.c_uint32, C.c_uint32]
+        L.oracle_triaccel_load.argtypes = [C.POINTER(C.c_float)] * 4
+        L.oracle_triaccel_intersect.argtypes = [C.POINTER(C.c_float)] * 3 + [C.c_float, C.c_float, C.POINTER(C.c_float)]
+        L.oracle_camera.argtypes = [C.POINTER(abi.SensorDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 6 + [C.c_int]
+        L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 4 + [C.c_int]
+        rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
+        if rc != 0:
+            raise RuntimeError('oracle_sobol_init failed: %d' % rc)
+        _lib = L
+    return _lib
+
+
+def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0)):
+    """Render with the oracle; returns (film (H+2b, W+2b, 5), samples or None, stats dict)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    from pkgimport import mitsuba_amd
+    m = mitsuba_amd()
+    L = lib()
+    W, H = scene.sensor.width, scene.sensor.height
+    x0, y0, w, h = window if window else (0, 0, W, H)
+    p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+    b = m.film_border(integ.rfilter, integ.rfilterParam)
+    film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
+    smp = np.zeros((w * h * integ.sampleCount, m.abi.SAMPLE_RECORD_FLOATS), np.float32) if samples else None
+    st = m.abi.Stats()
+    d = scene.desc()
+    rc = L.oracle_render(C.byref(d), C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)),
+                         smp.ctypes.data_as(C.POINTER(C.c_float)) if samples else None,
+                         C.byref(st), libm_mode, threads)
+    if rc != 0:
+        raise RuntimeError('oracle_render failed: %d' % rc)
+    return film, smp, st.as_dict()

@@ -1,0 +1,1965 @@
+/*
+ * mts_oracle.c -- TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).
+ *
+ * A plain-C restatement of Mitsuba 0.6's unidirectional path tracer hot path
+ * (/root/reference = Yujie-G/mitsuba0.6).  Every function cites the reference
+ * lines it follows.  Arithmetic is single precision, evaluated in the same
+ * order as the reference expressions, compiled with -ffp-contract=off (the
+ * reference's x86 SSE build has no FMA).
+ *
+ * Pinning: the reference cannot be built here (every header includes boost,
+ * absent from the image), so this restatement is pinned by
+ *   - the reference's own known-answer test for the intersection record
+ *     (src/tests/test_dgeom.cpp:35-80) -> tests/test_oracle_kat.py;
+ *   - golden vectors computed from the reference's vendored Sobol tables
+ *     (src/samplers/sobolseq.cpp) -> tests/golden/sobol_golden.json;
+ *   - the reference's chi^2 / sample-vs-pdf consistency criteria
+ *     (src/tests/test_chisquare.cpp:94-215) -> tests/test_oracle_bsdf.py.
+ * Whole-path Li() output is "parity unpinned" against the reference binary
+ * (no reference test pins it); it is pinned against this
+ * restatement, which follows the reference line by line.
+ *
+ * libm: mode 0 calls the glibc float functions the reference calls
+ * (sincosf, acosf, atan2f, tanf, expf, powf, atanf) and double exp/log for
+ * math::fastexp/fastlog (include/mitsuba/core/math.h:175-216).  Mode 1 rounds
+ * the double-precision result to float, which is what the product's device
+ * code does; the difference between the two modes is reported as the libm
+ * noise floor.
+ */
+#define _GNU_SOURCE
+#include "mts_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* constants (include/mitsuba/core/constants.h:28-31,53-66)                  */
+/* ------------------------------------------------------------------------ */
+#define EPSILON 1e-4f
+#define SHADOW_EPSILON 1e-3f
+#define M_PI_F 3.14159265358979323846f
+#define INV_PI_F 0.31830988618379067154f
+#define INV_TWOPI_F 0.15915494309189533577f
+#define ONE_MINUS_EPS_F 0x1.fffffep-1f
+#define FILTER_RES 31 /* MTS_FILTER_RESOLUTION, rfilter.h:28 */
+#define BLOCK_SIZE 32 /* scene.cpp:24 */
+
+static int g_cr = 0; /* libm mode */
+
+/* std::max / std::min semantics (NaN handling matters) */
+static inline float smax(float a, float b) { return (a < b) ? b : a; }
+static inline float smin(float a, float b) { return (b < a) ? b : a; }
+
+/* ---- libm as called by the reference ---------------------------------- */
+static inline void o_sincos(float x, float *s, float *c) {
+    if (g_cr) { *s = (float)sin((double)x); *c = (float)cos((double)x); }
+    else sincosf(x, s, c);
+}
+static inline float o_acos(float x) { return g_cr ? (float)acos((double)x) : acosf(x); }
+static inline float o_atan2(float y, float x) { return g_cr ? (float)atan2((double)y, (double)x) : atan2f(y, x); }
+static inline float o_tan(float x) { return g_cr ? (float)tan((double)x) : tanf(x); }
+static inline float o_atan(float x) { return g_cr ? (float)atan((double)x) : atanf(x); }
+static inline float o_exp(float x) { return g_cr ? (float)exp((double)x) : expf(x); }
+static inline float o_pow(float x, float y) { return g_cr ? (float)pow((double)x, (double)y) : powf(x, y); }
+/* math::fastexp/fastlog (math.h:185-200): double precision in both modes */
+static inline float o_fastexp(float x) { return (float)exp((double)x); }
+static inline float o_fastlog(float x) { return (float)log((double)x); }
+/* math::safe_sqrt (math.h:260-262) */
+static inline float safe_sqrt(float v) { return sqrtf(smax(0.0f, v)); }
+/* math::signum (math.h:270-279) */
+static inline float signumf(float v) { return copysignf(1.0f, v); }
+
+/* ------------------------------------------------------------------------ */
+/* vectors, spectra, frames (core/vector.h, spectrum.h, frame.h)             */
+/* ------------------------------------------------------------------------ */
+typedef struct { float x, y, z; } V3;
+static inline V3 v3(float x, float y, float z) { V3 r = {x, y, z}; return r; }
+static inline V3 vadd(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static inline V3 vsub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+static inline V3 vmul(V3 a, float f) { return v3(a.x * f, a.y * f, a.z * f); }
+static inline V3 vmulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+static inline V3 vdivv(V3 a, V3 b) { return v3(a.x / b.x, a.y / b.y, a.z / b.z); }
+static inline V3 vneg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+/* operator/(T f): recip = 1/f (vector.h:535-541, spectrum.h:415-423) */
+static inline V3 vdiv(V3 a, float f) { float r = 1.0f / f; return vmul(a, r); }
+static inline float vdot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static inline float vabsdot(V3 a, V3 b) { return fabsf(vdot(a, b)); }
+static inline V3 vcross(V3 a, V3 b) {
+    return v3((a.y * b.z) - (a.z * b.y), (a.z * b.x) - (a.x * b.z), (a.x * b.y) - (a.y * b.x));
+}
+static inline float vlen2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+static inline float vlen(V3 a) { return sqrtf(vlen2(a)); }
+static inline V3 vnormalize(V3 a) { return vdiv(a, vlen(a)); }
+static inline int vzero(V3 a) { return a.x == 0 && a.y == 0 && a.z == 0; }
+static inline float vget(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+static inline void vset(V3 *a, int i, float f) { if (i == 0) a->x = f; else if (i == 1) a->y = f; else a->z = f; }
+/* Spectrum::max (spectrum.h:543-548) */
+static inline float smaxc(V3 s) { float r = s.x; r = smax(r, s.y); r = smax(r, s.z); return r; }
+/* Spectrum::average (spectrum.h:481-486) */
+static inline float savg(V3 s) { float r = 0.0f; r += s.x; r += s.y; r += s.z; return r * (1.0f / 3); }
+
+typedef struct { V3 s, t, n; } Frame;
+static inline V3 to_local(const Frame *f, V3 v) { return v3(vdot(v, f->s), vdot(v, f->t), vdot(v, f->n)); }
+static inline V3 to_world(const Frame *f, V3 v) {
+    return vadd(vadd(vmul(f->s, v.x), vmul(f->t, v.y)), vmul(f->n, v.z));
+}
+/* Frame::tanTheta (frame.h:117-122), sinTheta2 (:103-105) */
+static inline float tan_theta(V3 v) {
+    float temp = 1 - v.z * v.z;
+    if (temp <= 0.0f) return 0.0f;
+    return sqrtf(temp) / v.z;
+}
+static inline float sin_theta2(V3 v) { return 1.0f - v.z * v.z; }
+
+/* coordinateSystem (util.cpp:592-601) */
+static void coordinate_system(V3 a, V3 *b, V3 *c) {
+    if (fabsf(a.x) > fabsf(a.y)) {
+        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        *c = v3(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        *c = v3(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    *b = vcross(*c, a);
+}
+
+/* computeShadingFrame (util.cpp:603-608) */
+static void compute_shading_frame(V3 n, V3 dpdu, Frame *f) {
+    f->n = n;
+    f->s = vnormalize(vsub(dpdu, vmul(f->n, vdot(f->n, dpdu))));
+    f->t = vcross(f->n, f->s);
+}
+
+/* ------------------------------------------------------------------------ */
+/* 4x4 transforms (core/transform.h, transform.cpp, matrix.h/.inl)           */
+/* ------------------------------------------------------------------------ */
+typedef struct { float m[4][4]; } M4;
+typedef struct { M4 t, inv; } Xform;
+
+static M4 m4_mul(const M4 *a, const M4 *b) { /* matrix.h:744-756 */
+    M4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float sum = 0;
+            for (int k = 0; k < 4; ++k) sum += a->m[i][k] * b->m[k][j];
+            r.m[i][j] = sum;
+        }
+    return r;
+}
+
+static int m4_invert(const M4 *src, M4 *target) { /* matrix.inl:138-193 */
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    *target = *src;
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        float big = 0;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] != 1) {
+                for (int k = 0; k < 4; k++) {
+                    if (ipiv[k] == 0) {
+                        if (fabsf(target->m[j][k]) >= big) {
+                            big = fabsf(target->m[j][k]);
+                            irow = j; icol = k;
+                        }
+                    } else if (ipiv[k] > 1) return 0;
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) { float t = target->m[irow][k]; target->m[irow][k] = target->m[icol][k]; target->m[icol][k] = t; }
+        indxr[i] = irow; indxc[i] = icol;
+        if (target->m[icol][icol] == 0) return 0;
+        float pivinv = 1.f / target->m[icol][icol];
+        target->m[icol][icol] = 1.f;
+        for (int j = 0; j < 4; j++) target->m[icol][j] *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j != icol) {
+                float save = target->m[j][icol];
+                target->m[j][icol] = 0;
+                for (int k = 0; k < 4; k++) target->m[j][k] -= target->m[icol][k] * save;
+            }
+        }
+    }
+    for (int j = 3; j >= 0; j--) {
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) {
+                float t = target->m[k][indxr[j]]; target->m[k][indxr[j]] = target->m[k][indxc[j]]; target->m[k][indxc[j]] = t;
+            }
+    }
+    return 1;
+}
+
+static M4 m4_diag(float a, float b, float c, float d) {
+    M4 r; memset(&r, 0, sizeof r);
+    r.m[0][0] = a; r.m[1][1] = b; r.m[2][2] = c; r.m[3][3] = d;
+    return r;
+}
+static Xform xf_compose(const Xform *a, const Xform *b) { /* transform.cpp:28-31 */
+    Xform r; r.t = m4_mul(&a->t, &b->t); r.inv = m4_mul(&b->inv, &a->inv); return r;
+}
+static Xform xf_scale(float x, float y, float z) { /* transform.cpp:49-63 */
+    Xform r; r.t = m4_diag(x, y, z, 1); r.inv = m4_diag(1.0f / x, 1.0f / y, 1.0f / z, 1); return r;
+}
+static Xform xf_translate(float x, float y, float z) { /* transform.cpp:33-47 */
+    Xform r; r.t = m4_diag(1, 1, 1, 1); r.inv = r.t;
+    r.t.m[0][3] = x; r.t.m[1][3] = y; r.t.m[2][3] = z;
+    r.inv.m[0][3] = -x; r.inv.m[1][3] = -y; r.inv.m[2][3] = -z;
+    return r;
+}
+static inline float deg_to_rad(float v) { return v * (M_PI_F / 180.0f); } /* util.h:297 */
+static inline float rad_to_deg(float v) { return v * (180.0f / M_PI_F); } /* util.h:294 */
+static int xf_perspective(float fov, float clipNear, float clipFar, Xform *out) { /* transform.cpp:99-123 */
+    float recip = 1.0f / (clipFar - clipNear);
+    float cot = 1.0f / tanf(deg_to_rad(fov / 2.0f));
+    M4 t; memset(&t, 0, sizeof t);
+    t.m[0][0] = cot; t.m[1][1] = cot;
+    t.m[2][2] = clipFar * recip; t.m[2][3] = -clipNear * clipFar * recip;
+    t.m[3][2] = 1;
+    out->t = t;
+    return m4_invert(&t, &out->inv);
+}
+/* Transform::operator()(Point) (transform.h:108-125) */
+static V3 xf_point(const M4 *m, V3 p) {
+    float x = m->m[0][0] * p.x + m->m[0][1] * p.y + m->m[0][2] * p.z + m->m[0][3];
+    float y = m->m[1][0] * p.x + m->m[1][1] * p.y + m->m[1][2] * p.z + m->m[1][3];
+    float z = m->m[2][0] * p.x + m->m[2][1] * p.y + m->m[2][2] * p.z + m->m[2][3];
+    float w = m->m[3][0] * p.x + m->m[3][1] * p.y + m->m[3][2] * p.z + m->m[3][3];
+    if (w == 1.0f) return v3(x, y, z);
+    return vdiv(v3(x, y, z), w);
+}
+static V3 xf_point_affine(const M4 *m, V3 p) { /* transform.h:128-136 */
+    float x = m->m[0][0] * p.x + m->m[0][1] * p.y + m->m[0][2] * p.z + m->m[0][3];
+    float y = m->m[1][0] * p.x + m->m[1][1] * p.y + m->m[1][2] * p.z + m->m[1][3];
+    float z = m->m[2][0] * p.x + m->m[2][1] * p.y + m->m[2][2] * p.z + m->m[2][3];
+    return v3(x, y, z);
+}
+static V3 xf_vector(const M4 *m, V3 v) { /* transform.h:175-183 */
+    float x = m->m[0][0] * v.x + m->m[0][1] * v.y + m->m[0][2] * v.z;
+    float y = m->m[1][0] * v.x + m->m[1][1] * v.y + m->m[1][2] * v.z;
+    float z = m->m[2][0] * v.x + m->m[2][1] * v.y + m->m[2][2] * v.z;
+    return v3(x, y, z);
+}
+
+/* ------------------------------------------------------------------------ */
+/* perspective camera (perspective.cpp:126-163,271-298; sensor.cpp:95-107,   */
+/* 239-305)                                                                  */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    M4 sampleToCamera, toWorld;
+    float invResX, invResY, nearClip, farClip;
+    V3 dx, dy;
+} Camera;
+
+static int camera_configure(const mtsgpu_sensor_desc *s, Camera *cam) {
+    if (s->film_width == 0 || s->film_height == 0) return MTSGPU_EINVAL;
+    float aspect = (float)s->film_width / (float)s->film_height;
+    float xfov = s->fov;
+    int axis = s->fov_axis;
+    if (axis == MTSGPU_FOV_SMALLER) axis = aspect > 1 ? MTSGPU_FOV_Y : MTSGPU_FOV_X;
+    else if (axis == MTSGPU_FOV_LARGER) axis = aspect > 1 ? MTSGPU_FOV_X : MTSGPU_FOV_Y;
+    if (axis == MTSGPU_FOV_Y) {
+        xfov = rad_to_deg(2 * atanf(tanf(0.5f * deg_to_rad(s->fov)) * aspect));
+    } else if (axis == MTSGPU_FOV_DIAGONAL) {
+        float diagonal = 2 * tanf(0.5f * deg_to_rad(s->fov));
+        float width = diagonal / sqrtf(1.0f + 1.0f / (aspect * aspect));
+        xfov = rad_to_deg(2 * atanf(width * 0.5f));
+    }
+    if (!(xfov > 0 && xfov < 180)) return MTSGPU_EINVAL;
+    if (!(s->near_clip > 0) || !(s->near_clip < s->far_clip)) return MTSGPU_EINVAL;
+    /* crop = film: relSize = 1, relOffset = 0 */
+    Xform a = xf_scale(1.0f / 1.0f, 1.0f / 1.0f, 1.0f);
+    Xform b = xf_translate(-0.0f, -0.0f, 0.0f);
+    Xform c = xf_scale(-0.5f, -0.5f * aspect, 1.0f);
+    Xform d = xf_translate(-1.0f, -1.0f / aspect, 0.0f);
+    Xform p;
+    if (!xf_perspective(xfov, s->near_clip, s->far_clip, &p)) return MTSGPU_EINVAL;
+    Xform ab = xf_compose(&a, &b);
+    Xform abc = xf_compose(&ab, &c);
+    Xform abcd = xf_compose(&abc, &d);
+    Xform camToSample = xf_compose(&abcd, &p);
+    cam->sampleToCamera = camToSample.inv;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) cam->toWorld.m[i][j] = s->to_world[i * 4 + j];
+    cam->invResX = (float)1 / (float)s->film_width;
+    cam->invResY = (float)1 / (float)s->film_height;
+    cam->nearClip = s->near_clip;
+    cam->farClip = s->far_clip;
+    V3 o0 = xf_point(&cam->sampleToCamera, v3(0.0f, 0.0f, 0.0f));
+    cam->dx = vsub(xf_point(&cam->sampleToCamera, v3(cam->invResX, 0.0f, 0.0f)), o0);
+    cam->dy = vsub(xf_point(&cam->sampleToCamera, v3(0.0f, cam->invResY, 0.0f)), o0);
+    return MTSGPU_OK;
+}
+
+typedef struct {
+    V3 o, d, dRcp;
+    float mint, maxt;
+    int hasDiff;
+    V3 rxO, ryO, rxD, ryD;
+} Ray;
+
+static inline void ray_set_dir(Ray *r, V3 d) {
+    r->d = d;
+    r->dRcp = v3((float)1 / d.x, (float)1 / d.y, (float)1 / d.z);
+}
+static inline V3 ray_at(const Ray *r, float t) { return vadd(r->o, vmul(r->d, t)); }
+
+/* PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298) */
+static void camera_sample_ray(const Camera *cam, float sx, float sy, Ray *ray) {
+    V3 nearP = xf_point(&cam->sampleToCamera, v3(sx * cam->invResX, sy * cam->invResY, 0.0f));
+    V3 d = vnormalize(nearP);
+    float invZ = 1.0f / d.z;
+    ray->mint = cam->nearClip * invZ;
+    ray->maxt = cam->farClip * invZ;
+    ray->o = xf_point_affine(&cam->toWorld, v3(0.0f, 0.0f, 0.0f));
+    ray_set_dir(ray, xf_vector(&cam->toWorld, d));
+    ray->rxO = ray->ryO = ray->o;
+    ray->rxD = xf_vector(&cam->toWorld, vnormalize(vadd(nearP, cam->dx)));
+    ray->ryD = xf_vector(&cam->toWorld, vnormalize(vadd(nearP, cam->dy)));
+    ray->hasDiff = 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Sobol sampler (samplers/sobol.cpp:147-258, samplers/sobolseq.h:43-130)    */
+/* Direction numbers: Joe & Kuo (sobolseq.cpp:21-27), regenerated here from  */
+/* the published parameters with the Sobol' recurrence.                      */
+/* ------------------------------------------------------------------------ */
+#define SOBOL_DIMS 1024
+#define SOBOL_SIZE 52
+static uint32_t g_sobol[SOBOL_DIMS * SOBOL_SIZE];
+static int g_sobol_ready = 0;
+
+int oracle_sobol_init(const char *path) {
+    FILE *f = fopen(path, "r");
+    if (!f) return MTSGPU_EINVAL;
+    uint64_t m[SOBOL_SIZE];
+    for (int k = 0; k < SOBOL_SIZE; ++k) g_sobol[k] = (uint32_t)(((uint64_t)1 << (SOBOL_SIZE - 1 - k)) >> 20);
+    char line[1024];
+    int dims = 1;
+    while (fgets(line, sizeof line, f)) {
+        if (line[0] == '#' || line[0] == '\n') continue;
+        char *p = line;
+        long d = strtol(p, &p, 10), s = strtol(p, &p, 10), a = strtol(p, &p, 10);
+        if (d < 2 || d > SOBOL_DIMS || s < 1 || s > 20) { fclose(f); return MTSGPU_EINVAL; }
+        for (int i = 0; i < s; ++i) m[i] = (uint64_t)strtoull(p, &p, 10);
+        for (int k = (int)s; k < SOBOL_SIZE; ++k) {
+            uint64_t v = m[k - s] ^ (m[k - s] << s);
+            for (int i = 1; i < s; ++i)
+                if ((a >> (s - 1 - i)) & 1) v ^= m[k - i] << i;
+            m[k] = v;
+        }
+        for (int k = 0; k < SOBOL_SIZE; ++k)
+            g_sobol[(d - 1) * SOBOL_SIZE + k] = (uint32_t)((m[k] << (SOBOL_SIZE - 1 - k)) >> 20);
+        dims++;
+    }
+    fclose(f);
+    if (dims != SOBOL_DIMS) return MTSGPU_EINVAL;
+    g_sobol_ready = 1;
+    return MTSGPU_OK;
+}
+
+uint32_t oracle_sobol_matrix(uint32_t dim, uint32_t col) { return g_sobol[dim * SOBOL_SIZE + col]; }
+
+/* sobol::sampleSingle (sobolseq.h:43-57) */
+float oracle_sobol_sample(uint64_t index, uint32_t dim, uint32_t scramble) {
+    uint32_t result = scramble;
+    for (uint32_t i = dim * SOBOL_SIZE; index; index >>= 1, ++i)
+        if (index & 1) result ^= g_sobol[i];
+    return smin(result * (1.0f / (float)(1ULL << 32)), ONE_MINUS_EPS_F);
+}
+
+/* sobol::look_up (sobolseq.h:93-125): the index of the frame-th sample of the
+ * (0,2)-sequence in pixel (px,py) at resolution 2^m.  Restated as the GF(2)
+ * solve it encodes: the van der Corput coordinate fixes the low m index bits,
+ * the second Sobol coordinate fixes bits m..2m-1 through an m x m system. */
+typedef struct { uint32_t m; uint32_t inv[32]; uint32_t ycol[64]; } LookupTable;
+static LookupTable g_lut[32];
+static int g_lut_ready[32];
+
+static void lookup_prepare(uint32_t m) {
+    LookupTable *L = &g_lut[m];
+    L->m = m;
+    for (int b = 0; b < 64; ++b) L->ycol[b] = (b < SOBOL_SIZE) ? (g_sobol[SOBOL_SIZE + b] >> (32 - m)) : 0;
+    /* rows: A[r] bit t = bit r of ycol[m+t]; invert with [A | I] */
+    uint32_t A[32], I[32];
+    for (uint32_t r = 0; r < m; ++r) {
+        A[r] = 0; I[r] = 1u << r;
+        for (uint32_t t = 0; t < m; ++t) A[r] |= ((L->ycol[m + t] >> r) & 1u) << t;
+    }
+    for (uint32_t c = 0; c < m; ++c) {
+        uint32_t piv = c;
+        while (piv < m && !((A[piv] >> c) & 1u)) ++piv;
+        if (piv == m) { fprintf(stderr, "sobol look_up: singular system m=%u\n", m); abort(); }
+        uint32_t ta = A[c]; A[c] = A[piv]; A[piv] = ta;
+        uint32_t ti = I[c]; I[c] = I[piv]; I[piv] = ti;
+        for (uint32_t r = 0; r < m; ++r)
+            if (r != c && ((A[r] >> c) & 1u)) { A[r] ^= A[c]; I[r] ^= I[c]; }
+    }
+    /* now A = I, so x = Ainv*rhs: bit t of x = parity(I[t] & rhs) */
+    for (uint32_t t = 0; t < m; ++t) L->inv[t] = I[t];
+}
+
+uint64_t oracle_sobol_lookup(uint32_t m, uint32_t frame, uint32_t px, uint32_t py, uint64_t scramble) {
+    if (m == 0 || m > 31) return (uint64_t)frame;
+    if (!g_lut_ready[m]) { lookup_prepare(m); g_lut_ready[m] = 1; }
+    const LookupTable *L = &g_lut[m];
+    uint32_t s = (uint32_t)((scramble & 0xFFFFFFFFull) >> (32 - m));
+    uint32_t sx = px ^ s, sy = py ^ s;
+    uint32_t mask = (m == 32) ? 0xFFFFFFFFu : ((1u << m) - 1u);
+    sx &= mask; sy &= mask;
+    uint64_t jlo = 0;
+    for (uint32_t t = 0; t < m; ++t) jlo |= (uint64_t)((sx >> (m - 1 - t)) & 1u) << t;
+    uint64_t index = ((uint64_t)frame << (2 * m)) | jlo;
+    uint32_t K = 0;
+    for (uint32_t b = 0; b < 64; ++b)
+        if ((index >> b) & 1) K ^= L->ycol[b];
+    uint32_t rhs = (sy ^ K) & mask;
+    uint64_t jhi = 0;
+    for (uint32_t t = 0; t < m; ++t) jhi |= (uint64_t)(__builtin_parity(L->inv[t] & rhs)) << t;
+    return index | (jhi << m);
+}
+
+/* sampleTEA (core/qmc.h:146-156) */
+static uint64_t sample_tea(uint32_t v0, uint32_t v1, int rounds) {
+    uint32_t sum = 0;
+    for (int i = 0; i < rounds; ++i) {
+        sum += 0x9e3779b9;
+        v0 += ((v1 << 4) + 0xA341316C) ^ (v1 + sum) ^ ((v1 >> 5) + 0xC8013EA4);
+        v1 += ((v0 << 4) + 0xAD90777D) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7E95761E);
+    }
+    return ((uint64_t)v1 << 32) + v0;
+}
+
+typedef struct {
+    uint64_t scramble;
+    float resolution;
+    uint32_t logRes;
+    int px, py;
+    uint64_t sampleIndex, sobolIndex;
+    uint32_t dim;
+    int err;
+} Sampler;
+
+static void sampler_init(Sampler *s, uint64_t scramble, uint32_t w, uint32_t h) {
+    memset(s, 0, sizeof *s);
+    s->scramble = scramble;
+    if (scramble) s->scramble = sample_tea((uint32_t)scramble, (uint32_t)(scramble >> 32), 4);
+    /* setFilmResolution(cropSize, bucketed = true) (sobol.cpp:147-158, integrator.cpp:38-41) */
+    uint32_t v = w > h ? w : h;
+    uint32_t r = v - 1; r |= r >> 1; r |= r >> 2; r |= r >> 4; r |= r >> 8; r |= r >> 16; r += 1;
+    s->resolution = (float)r;
+    uint32_t lg = 0; while ((1u << lg) < r) ++lg;
+    s->logRes = lg;
+}
+
+static void sampler_set_index(Sampler *s, uint64_t idx) { /* sobol.cpp:204-217 */
+    s->dim = 0;
+    s->sampleIndex = idx;
+    if (s->logRes > 1 && s->px >= 0)
+        s->sobolIndex = oracle_sobol_lookup(s->logRes, (uint32_t)idx, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
+    else
+        s->sobolIndex = idx;
+}
+static void sampler_generate(Sampler *s, int px, int py) { s->px = px; s->py = py; sampler_set_index(s, 0); }
+
+static float next1d(Sampler *s) { /* sobol.cpp:219-229; arrays [5,5) are empty */
+    if (s->dim >= 5 && s->dim < 5) s->dim = 5;
+    if (s->dim >= SOBOL_DIMS) { s->err = 1; return 0.0f; }
+    return oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
+}
+static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
+    if (s->dim + 1 >= 5 && s->dim < 5) s->dim = 5;
+    if (s->dim + 1 >= SOBOL_DIMS) { s->err = 1; *u = *v = 0.0f; return; }
+    if (s->dim == 0 && s->sobolIndex != s->sampleIndex) {
+        *u = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble) * s->resolution - (float)s->px;
+        *v = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble) * s->resolution - (float)s->py;
+    } else {
+        *u = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
+        *v = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* warps (libcore/warp.cpp:43-102, include/mitsuba/core/warp.h:55-56)        */
+/* ------------------------------------------------------------------------ */
+static void square_to_disk_concentric(float sx, float sy, float *px, float *py) {
+    float r1 = 2.0f * sx - 1.0f;
+    float r2 = 2.0f * sy - 1.0f;
+    float phi, r;
+    if (r1 == 0 && r2 == 0) {
+        r = phi = 0;
+    } else if (r1 * r1 > r2 * r2) {
+        r = r1;
+        phi = (M_PI_F / 4.0f) * (r2 / r1);
+    } else {
+        r = r2;
+        phi = (M_PI_F / 2.0f) - (r1 / r2) * (M_PI_F / 4.0f);
+    }
+    float c, s;
+    o_sincos(phi, &s, &c);
+    *px = r * c;
+    *py = r * s;
+}
+static V3 square_to_cosine_hemisphere(float sx, float sy) {
+    float px, py;
+    square_to_disk_concentric(sx, sy, &px, &py);
+    float z = safe_sqrt(1.0f - px * px - py * py);
+    if (z == 0) z = 1e-10f;
+    return v3(px, py, z);
+}
+static inline float cosine_hemisphere_pdf(V3 d) { return INV_PI_F * d.z; }
+
+/* ------------------------------------------------------------------------ */
+/* math::erf / erfinv / hypot2 (libcore/math.cpp:25-95)                       */
+/* ------------------------------------------------------------------------ */
+static float m_erfinv(float x) {
+    float w = -o_fastlog(((float)1 - x) * ((float)1 + x));
+    float p;
+    if (w < (float)5) {
+        w = w - (float)2.5;
+        p = (float)2.81022636e-08;
+        p = (float)3.43273939e-07 + p * w;
+        p = (float)-3.5233877e-06 + p * w;
+        p = (float)-4.39150654e-06 + p * w;
+        p = (float)0.00021858087 + p * w;
+        p = (float)-0.00125372503 + p * w;
+        p = (float)-0.00417768164 + p * w;
+        p = (float)0.246640727 + p * w;
+        p = (float)1.50140941 + p * w;
+    } else {
+        w = sqrtf(w) - (float)3;
+        p = (float)-0.000200214257;
+        p = (float)0.000100950558 + p * w;
+        p = (float)0.00134934322 + p * w;
+        p = (float)-0.00367342844 + p * w;
+        p = (float)0.00573950773 + p * w;
+        p = (float)-0.0076224613 + p * w;
+        p = (float)0.00943887047 + p * w;
+        p = (float)1.00167406 + p * w;
+        p = (float)2.83297682 + p * w;
+    }
+    return p * x;
+}
+static float m_erf(float x) {
+    float a1 = (float)0.254829592, a2 = (float)-0.284496736, a3 = (float)1.421413741;
+    float a4 = (float)-1.453152027, a5 = (float)1.061405429, p = (float)0.3275911;
+    float sign = signumf(x);
+    x = fabsf(x);
+    float t = (float)1.0 / ((float)1.0 + p * x);
+    float y = (float)1.0 - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * o_fastexp(-x * x);
+    return sign * y;
+}
+static float m_hypot2(float a, float b) {
+    float r;
+    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * sqrtf(1.0f + r * r); }
+    else if (b != 0.0f) { r = a / b; r = fabsf(b) * sqrtf(1.0f + r * r); }
+    else r = 0.0f;
+    return r;
+}
+
+/* ------------------------------------------------------------------------ */
+/* MicrofacetDistribution (bsdfs/microfacet.h)                               */
+/* ------------------------------------------------------------------------ */
+typedef struct { int type; float alphaU, alphaV; int sampleVisible; float expU, expV; } Distr;
+
+static void distr_init(Distr *d, int type, float au, float av, int sv) { /* microfacet.h:89-97 */
+    d->type = type; d->alphaU = smax(au, 1e-4f); d->alphaV = smax(av, 1e-4f);
+    d->sampleVisible = sv; d->expU = d->expV = 0.0f;
+    if (type == MTSGPU_DISTR_PHONG) { /* computePhongExponent (:673-676) */
+        d->expU = smax(2.0f / (d->alphaU * d->alphaU) - 2.0f, 0.0f);
+        d->expV = smax(2.0f / (d->alphaV * d->alphaV) - 2.0f, 0.0f);
+    }
+}
+static inline int distr_iso(const Distr *d) { return d->alphaU == d->alphaV; }
+
+static float distr_interp_phong(const Distr *d, V3 v) { /* :538-549 */
+    float st2 = sin_theta2(v);
+    if (distr_iso(d) || st2 <= 0x1p-128f) return d->expU;
+    float inv = 1 / st2;
+    return d->expU * (v.x * v.x * inv) + d->expV * (v.y * v.y * inv);
+}
+
+static float distr_eval(const Distr *d, V3 m) { /* :191-238 */
+    if (m.z <= 0) return 0.0f;
+    float cosTheta2 = m.z * m.z;
+    float beckmannExponent = ((m.x * m.x) / (d->alphaU * d->alphaU) + (m.y * m.y) / (d->alphaV * d->alphaV)) / cosTheta2;
+    float result;
+    if (d->type == MTSGPU_DISTR_BECKMANN) {
+        result = o_fastexp(-beckmannExponent) / (M_PI_F * d->alphaU * d->alphaV * cosTheta2 * cosTheta2);
+    } else if (d->type == MTSGPU_DISTR_GGX) {
+        float root = ((float)1 + beckmannExponent) * cosTheta2;
+        result = (float)1 / (M_PI_F * d->alphaU * d->alphaV * root * root);
+    } else {
+        float exponent = distr_interp_phong(d, m);
+        result = sqrtf((d->expU + 2) * (d->expV + 2)) * INV_TWOPI_F * o_pow(m.z, exponent);
+    }
+    if (result * m.z < 1e-20f) result = 0;
+    return result;
+}
+
+static float distr_project_roughness(const Distr *d, V3 v) { /* :526-536 */
+    float invSinTheta2 = 1 / sin_theta2(v);
+    if (distr_iso(d) || invSinTheta2 <= 0) return d->alphaU;
+    float cosPhi2 = v.x * v.x * invSinTheta2;
+    float sinPhi2 = v.y * v.y * invSinTheta2;
+    return sqrtf(cosPhi2 * d->alphaU * d->alphaU + sinPhi2 * d->alphaV * d->alphaV);
+}
+
+static float distr_smithG1(const Distr *d, V3 v, V3 m) { /* :477-518 */
+    if (vdot(v, m) * v.z <= 0) return 0.0f;
+    float tanTheta = fabsf(tan_theta(v));
+    if (tanTheta == 0.0f) return 1.0f;
+    float alpha = distr_project_roughness(d, v);
+    if (d->type == MTSGPU_DISTR_GGX) {
+        float root = alpha * tanTheta;
+        return 2.0f / (1.0f + m_hypot2((float)1.0f, root));
+    }
+    float a = 1.0f / (alpha * tanTheta);
+    if (a >= 1.6f) return 1.0f;
+    float aSqr = a * a;
+    return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+}
+static inline float distr_G(const Distr *d, V3 wi, V3 wo, V3 m) { return distr_smithG1(d, wi, m) * distr_smithG1(d, wo, m); }
+
+static void distr_sample_first_quadrant(const Distr *d, float u1, float *phi, float *exponent) { /* :679-688 */
+    float c, s;
+    *phi = o_atan(sqrtf((d->expU + 2.0f) / (d->expV + 2.0f)) * o_tan(M_PI_F * u1 * 0.5f));
+    o_sincos(*phi, &s, &c);
+    *exponent = d->expU * c * c + d->expV * s * s;
+}
+
+static V3 distr_sample_all(const Distr *d, float sx, float sy, float *pdf) { /* :287-402 */
+    float cosThetaM = 0.0f, sinPhiM, cosPhiM, alphaSqr;
+    if (d->type == MTSGPU_DISTR_BECKMANN || d->type == MTSGPU_DISTR_GGX) {
+        if (distr_iso(d)) {
+            o_sincos((2.0f * M_PI_F) * sy, &sinPhiM, &cosPhiM);
+            alphaSqr = d->alphaU * d->alphaU;
+        } else {
+            float phiM = o_atan(d->alphaV / d->alphaU * o_tan(M_PI_F + 2 * M_PI_F * sy)) + M_PI_F * floorf(2 * sy + 0.5f);
+            o_sincos(phiM, &sinPhiM, &cosPhiM);
+            float cosSc = cosPhiM / d->alphaU, sinSc = sinPhiM / d->alphaV;
+            alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
+        }
+        if (d->type == MTSGPU_DISTR_BECKMANN) {
+            float tanThetaMSqr = alphaSqr * -o_fastlog(1.0f - sx);
+            cosThetaM = 1.0f / sqrtf(1.0f + tanThetaMSqr);
+            *pdf = (1.0f - sx) / (M_PI_F * d->alphaU * d->alphaV * cosThetaM * cosThetaM * cosThetaM);
+        } else {
+            float tanThetaMSqr = alphaSqr * sx / (1.0f - sx);
+            cosThetaM = 1.0f / sqrtf(1.0f + tanThetaMSqr);
+            float temp = 1 + tanThetaMSqr / alphaSqr;
+            *pdf = INV_PI_F / (d->alphaU * d->alphaV * cosThetaM * cosThetaM * cosThetaM * temp * temp);
+        }
+    } else {
+        float phiM, exponent;
+        if (distr_iso(d)) {
+            phiM = (2.0f * M_PI_F) * sy;
+            exponent = d->expU;
+        } else {
+            if (sy < 0.25f) {
+                distr_sample_first_quadrant(d, 4 * sy, &phiM, &exponent);
+            } else if (sy < 0.5f) {
+                distr_sample_first_quadrant(d, 4 * (0.5f - sy), &phiM, &exponent);
+                phiM = M_PI_F - phiM;
+            } else if (sy < 0.75f) {
+                distr_sample_first_quadrant(d, 4 * (sy - 0.5f), &phiM, &exponent);
+                phiM += M_PI_F;
+            } else {
+                distr_sample_first_quadrant(d, 4 * (1 - sy), &phiM, &exponent);
+                phiM = 2 * M_PI_F - phiM;
+            }
+        }
+        o_sincos(phiM, &sinPhiM, &cosPhiM);
+        cosThetaM = o_pow(sx, 1.0f / (exponent + 2.0f));
+        *pdf = sqrtf((d->expU + 2.0f) * (d->expV + 2.0f)) * INV_TWOPI_F * o_pow(cosThetaM, exponent + 1.0f);
+    }
+    if (*pdf < 1e-20f) *pdf = 0;
+    float sinThetaM = sqrtf(smax((float)0, 1 - cosThetaM * cosThetaM));
+    return v3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+}
+
+static void distr_sample_visible11(const Distr *d, float thetaI, float sx, float sy, float *slx, float *sly) { /* :573-670 */
+    const float SQRT_PI_INV = 1 / sqrtf(M_PI_F);
+    if (d->type == MTSGPU_DISTR_BECKMANN) {
+        if (thetaI < 1e-4f) {
+            float s, c;
+            float r = sqrtf(-o_fastlog(1.0f - sx));
+            o_sincos(2 * M_PI_F * sy, &s, &c);
+            *slx = r * c; *sly = r * s;
+            return;
+        }
+        float tanThetaI = o_tan(thetaI);
+        float cotThetaI = 1 / tanThetaI;
+        float a = -1, c = m_erf(cotThetaI);
+        float sample_x = smax(sx, (float)1e-6f);
+        float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+        float b = c - (1 + c) * o_pow(1 - sample_x, fit);
+        float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * o_exp(-cotThetaI * cotThetaI));
+        int it = 0;
+        while (++it < 10) {
+            if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+            float invErf = m_erfinv(b);
+            float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * o_exp(-invErf * invErf)) - sample_x;
+            float derivative = normalization * (1 - invErf * tanThetaI);
+            if (fabsf(value) < 1e-5f) break;
+            if (value > 0) c = b; else a = b;
+            b -= value / derivative;
+        }
+        *slx = m_erfinv(b);
+        *sly = m_erfinv(2.0f * smax(sy, (float)1e-6f) - 1.0f);
+        return;
+    }
+    /* GGX */
+    if (thetaI < 1e-4f) {
+        float s, c;
+        float r = safe_sqrt(sx / (1 - sx));
+        o_sincos(2 * M_PI_F * sy, &s, &c);
+        *slx = r * c; *sly = r * s;
+        return;
+    }
+    float tanThetaI = o_tan(thetaI);
+    float a = 1 / tanThetaI;
+    float G1 = 2.0f / (1.0f + safe_sqrt(1.0f + 1.0f / (a * a)));
+    float A = 2.0f * sx / G1 - 1.0f;
+    if (fabsf(A) == 1) A -= signumf(A) * EPSILON;
+    float tmp = 1.0f / (A * A - 1.0f);
+    float B = tanThetaI;
+    float D = safe_sqrt(B * B * tmp * tmp - (A * A - B * B) * tmp);
+    float slope_x_1 = B * tmp - D;
+    float slope_x_2 = B * tmp + D;
+    *slx = (A < 0.0f || slope_x_2 > 1.0f / tanThetaI) ? slope_x_1 : slope_x_2;
+    float S;
+    if (sy > 0.5f) { S = 1.0f; sy = 2.0f * (sy - 0.5f); }
+    else { S = -1.0f; sy = 2.0f * (0.5f - sy); }
+    float z = (sy * (sy * (sy * (-(float)0.365728915865723) + (float)0.790235037209296) - (float)0.424965825137544) + (float)0.000152998850436920) /
+              (sy * (sy * (sy * (sy * (float)0.169507819808272 - (float)0.397203533833404) - (float)0.232500544458471) + (float)1) - (float)0.539825872510702);
+    *sly = S * z * sqrtf(1.0f + (*slx) * (*slx));
+}
+
+static V3 distr_sample_visible(const Distr *d, V3 _wi, float sx, float sy) { /* :421-460 */
+    V3 wi = vnormalize(v3(d->alphaU * _wi.x, d->alphaV * _wi.y, _wi.z));
+    float theta = 0, phi = 0;
+    if (wi.z < (float)0.99999) {
+        theta = o_acos(wi.z);
+        phi = o_atan2(wi.y, wi.x);
+    }
+    float sinPhi, cosPhi;
+    o_sincos(phi, &sinPhi, &cosPhi);
+    float slx, sly;
+    distr_sample_visible11(d, theta, sx, sy, &slx, &sly);
+    float nx = cosPhi * slx - sinPhi * sly;
+    float ny = sinPhi * slx + cosPhi * sly;
+    nx *= d->alphaU;
+    ny *= d->alphaV;
+    float normalization = (float)1 / sqrtf(nx * nx + ny * ny + (float)1.0);
+    return v3(-nx * normalization, -ny * normalization, normalization);
+}
+
+static float distr_pdf_visible(const Distr *d, V3 wi, V3 m) { /* :462-466 */
+    if (wi.z == 0) return 0.0f;
+    return distr_smithG1(d, wi, m) * vabsdot(wi, m) * distr_eval(d, m) / fabsf(wi.z);
+}
+static float distr_pdf(const Distr *d, V3 wi, V3 m) { /* :270-276 */
+    if (d->sampleVisible) return distr_pdf_visible(d, wi, m);
+    return distr_eval(d, m) * m.z;
+}
+static V3 distr_sample(const Distr *d, V3 wi, float sx, float sy, float *pdf) { /* :243-253 */
+    if (d->sampleVisible) {
+        V3 m = distr_sample_visible(d, wi, sx, sy);
+        *pdf = distr_pdf_visible(d, wi, m);
+        return m;
+    }
+    return distr_sample_all(d, sx, sy, pdf);
+}
+static void distr_scale_alpha(Distr *d, float v) { /* :181-186 */
+    d->alphaU *= v; d->alphaV *= v;
+    if (d->type == MTSGPU_DISTR_PHONG) {
+        d->expU = smax(2.0f / (d->alphaU * d->alphaU) - 2.0f, 0.0f);
+        d->expV = smax(2.0f / (d->alphaV * d->alphaV) - 2.0f, 0.0f);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Fresnel (libcore/util.cpp:651-771)                                        */
+/* ------------------------------------------------------------------------ */
+static float fresnel_dielectric_ext(float cosThetaI_, float *cosThetaT_, float eta) {
+    if (eta == 1) { *cosThetaT_ = -cosThetaI_; return 0.0f; }
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta,
+          cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) { *cosThetaT_ = 0.0f; return 1.0f; }
+    float cosThetaI = fabsf(cosThetaI_);
+    float cosThetaT = sqrtf(cosThetaTSqr);
+    float Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    float Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    *cosThetaT_ = (cosThetaI_ > 0) ? -cosThetaT : cosThetaT;
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+static V3 s_safe_sqrt(V3 a) { return v3(safe_sqrt(a.x), safe_sqrt(a.y), safe_sqrt(a.z)); }
+static V3 fresnel_conductor_exact(float cosThetaI, V3 eta, V3 k) { /* util.cpp:739-761 */
+    float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
+    V3 temp1 = vsub(vsub(vmulv(eta, eta), vmulv(k, k)), v3(sinThetaI2, sinThetaI2, sinThetaI2));
+    V3 a2pb2 = s_safe_sqrt(vadd(vmulv(temp1, temp1), vmul(vmulv(vmulv(vmulv(k, k), eta), eta), 4)));
+    V3 a = s_safe_sqrt(vmul(vadd(a2pb2, temp1), 0.5f));
+    V3 term1 = vadd(a2pb2, v3(cosThetaI2, cosThetaI2, cosThetaI2));
+    V3 term2 = vmul(a, 2 * cosThetaI);
+    V3 Rs2 = vdivv(vsub(term1, term2), vadd(term1, term2));
+    V3 term3 = vadd(vmul(a2pb2, cosThetaI2), v3(sinThetaI4, sinThetaI4, sinThetaI4));
+    V3 term4 = vmul(term2, sinThetaI2);
+    V3 Rp2 = vdivv(vmulv(Rs2, vsub(term3, term4)), vadd(term3, term4));
+    return vmul(vadd(Rp2, Rs2), 0.5f);
+}
+static inline V3 reflect_v(V3 wi, V3 n) { return vsub(vmul(n, 2 * vdot(wi, n)), wi); } /* util.cpp:763-765 */
+static inline V3 refract_v(V3 wi, V3 n, float eta, float cosThetaT) { /* util.cpp:767-771 */
+    if (cosThetaT < 0) eta = 1 / eta;
+    return vsub(vmul(n, vdot(wi, n) * eta + cosThetaT), vmul(wi, eta));
+}
+
+/* ------------------------------------------------------------------------ */
+/* BSDFs (bsdfs/diffuse.cpp, roughconductor.cpp, roughdielectric.cpp)        */
+/* ------------------------------------------------------------------------ */
+enum { /* BSDF::EBSDFType (include/mitsuba/render/bsdf.h) */
+    E_NULL = 0x00001, E_DIFF_REFL = 0x00002, E_DIFF_TRANS = 0x00004, E_GLOSSY_REFL = 0x00008,
+    E_GLOSSY_TRANS = 0x00010, E_DELTA_REFL = 0x00020, E_DELTA_TRANS = 0x00040,
+    E_FRONT = 0x01000, E_BACK = 0x02000
+};
+#define E_SMOOTH (E_DIFF_REFL | E_DIFF_TRANS | E_GLOSSY_REFL | E_GLOSSY_TRANS)
+#define E_TRANSMISSION (E_DIFF_TRANS | E_GLOSSY_TRANS | E_DELTA_TRANS | E_NULL)
+#define E_DELTA (E_NULL | E_DELTA_REFL | E_DELTA_TRANS)
+
+typedef struct {
+    int type, distr, sampleVisible, flags;
+    float alpha; /* texture average, isotropic */
+    float alphaU, alphaV;
+    V3 refl, specR, specT, eta3, k3;
+    float eta, invEta;
+} Bsdf;
+
+static float tex_scale_for_energy(V3 v, int ensure) { /* bsdf.cpp:88-112 */
+    if (!ensure) return 1.0f;
+    float actualMax = smaxc(v);
+    if (actualMax > 1.0f) return 0.99f * (1.0f / actualMax);
+    return 1.0f;
+}
+
+static int bsdf_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
+    memset(b, 0, sizeof *b);
+    b->type = d->type;
+    if (d->type == MTSGPU_BSDF_DIFFUSE) {
+        V3 r = v3(d->reflectance[0], d->reflectance[1], d->reflectance[2]);
+        float sc = tex_scale_for_energy(r, d->ensure_energy_conservation);
+        if (sc != 1.0f) r = vmul(r, sc);
+        b->refl = r;
+        b->flags = (smaxc(r) > 0) ? (E_DIFF_REFL | E_FRONT) : 0; /* diffuse.cpp:93-101 */
+        return MTSGPU_OK;
+    }
+    if (d->type != MTSGPU_BSDF_ROUGHCONDUCTOR && d->type != MTSGPU_BSDF_ROUGHDIELECTRIC) return MTSGPU_EINVAL;
+    if (d->distribution < 0 || d->distribution > 2) return MTSGPU_EINVAL;
+    b->distr = d->distribution;
+    /* MicrofacetDistribution(props) (microfacet.h:105-150) */
+    float au = smax(d->alpha_u, 1e-4f), av = smax(d->alpha_v, 1e-4f);
+    b->sampleVisible = d->distribution == MTSGPU_DISTR_PHONG ? 0 : d->sample_visible;
+    /* ConstantFloatTexture(alpha)->eval(its).average() (hw/basicshader.h:105) */
+    b->alphaU = savg(v3(au, au, au));
+    b->alphaV = savg(v3(av, av, av));
+    V3 sr = v3(d->specular_reflectance[0], d->specular_reflectance[1], d->specular_reflectance[2]);
+    float sc = tex_scale_for_energy(sr, d->ensure_energy_conservation);
+    if (sc != 1.0f) sr = vmul(sr, sc);
+    b->specR = sr;
+    if (d->type == MTSGPU_BSDF_ROUGHCONDUCTOR) {
+        /* roughconductor.cpp:168-199: m_eta = eta / extEta */
+        float r = 1.0f / d->ext_eta;
+        b->eta3 = vmul(v3(d->eta[0], d->eta[1], d->eta[2]), r);
+        b->k3 = vmul(v3(d->k[0], d->k[1], d->k[2]), r);
+        b->flags = E_GLOSSY_REFL | E_FRONT;
+    } else {
+        if (d->int_ior < 0 || d->ext_ior < 0 || d->int_ior == d->ext_ior) return MTSGPU_EINVAL;
+        b->eta = d->int_ior / d->ext_ior; /* roughdielectric.cpp:198-199 */
+        b->invEta = 1 / b->eta;
+        V3 st = v3(d->specular_transmittance[0], d->specular_transmittance[1], d->specular_transmittance[2]);
+        float sct = tex_scale_for_energy(st, d->ensure_energy_conservation);
+        if (sct != 1.0f) st = vmul(st, sct);
+        b->specT = st;
+        b->flags = E_GLOSSY_REFL | E_GLOSSY_TRANS | E_FRONT | E_BACK;
+    }
+    return MTSGPU_OK;
+}
+
+typedef struct { V3 wi, wo; float eta; int sampledType; } BRec;
+
+static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
+    V3 zero = v3(0, 0, 0);
+    if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:110-117 */
+        /* bRec.typeMask = EAll, so only the cosine tests can reject */
+        if (r->wi.z <= 0 || r->wo.z <= 0) return zero;
+        return vmul(b->refl, INV_PI_F * r->wo.z);
+    }
+    Distr d;
+    if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:257-292 */
+        if (r->wi.z <= 0 || r->wo.z <= 0) return zero;
+        V3 H = vnormalize(vadd(r->wo, r->wi));
+        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        float D = distr_eval(&d, H);
+        if (D == 0) return zero;
+        V3 F = vmulv(fresnel_conductor_exact(vdot(r->wi, H), b->eta3, b->k3), b->specR);
+        float G = distr_G(&d, r->wi, r->wo, H);
+        float model = D * G / (4.0f * r->wi.z);
+        return vmul(F, model);
+    }
+    /* roughdielectric.cpp:270-346 */
+    if (r->wi.z == 0) return zero;
+    int reflect = r->wi.z * r->wo.z > 0;
+    V3 H;
+    if (reflect) {
+        H = vnormalize(vadd(r->wo, r->wi));
+    } else {
+        float eta = r->wi.z > 0 ? b->eta : b->invEta;
+        H = vnormalize(vadd(r->wi, vmul(r->wo, eta)));
+    }
+    H = vmul(H, signumf(H.z));
+    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    float D = distr_eval(&d, H);
+    if (D == 0) return zero;
+    float ct;
+    float F = fresnel_dielectric_ext(vdot(r->wi, H), &ct, b->eta);
+    float G = distr_G(&d, r->wi, r->wo, H);
+    if (reflect) {
+        float value = F * D * G / (4.0f * fabsf(r->wi.z));
+        return vmul(b->specR, value);
+    }
+    float eta = r->wi.z > 0.0f ? b->eta : b->invEta;
+    float sqrtDenom = vdot(r->wi, H) + eta * vdot(r->wo, H);
+    float value = ((1 - F) * D * G * eta * eta * vdot(r->wi, H) * vdot(r->wo, H)) /
+                  (r->wi.z * sqrtDenom * sqrtDenom);
+    float factor = (r->wi.z > 0 ? b->invEta : b->eta); /* mode == ERadiance */
+    return vmul(b->specT, fabsf(value * factor * factor));
+}
+
+static float bsdf_pdf(const Bsdf *b, const BRec *r) {
+    if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:119-126 */
+        if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
+        return cosine_hemisphere_pdf(r->wo);
+    }
+    Distr d;
+    if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:294-319 */
+        if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
+        V3 H = vnormalize(vadd(r->wo, r->wi));
+        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        if (b->sampleVisible)
+            return distr_eval(&d, H) * distr_smithG1(&d, r->wi, H) / (4.0f * r->wi.z);
+        return distr_pdf(&d, r->wi, H) / (4 * vabsdot(r->wo, H));
+    }
+    /* roughdielectric.cpp:348-405 */
+    int reflect = r->wi.z * r->wo.z > 0;
+    V3 H;
+    float dwh_dwo;
+    if (reflect) {
+        H = vnormalize(vadd(r->wo, r->wi));
+        dwh_dwo = 1.0f / (4.0f * vdot(r->wo, H));
+    } else {
+        float eta = r->wi.z > 0 ? b->eta : b->invEta;
+        H = vnormalize(vadd(r->wi, vmul(r->wo, eta)));
+        float sqrtDenom = vdot(r->wi, H) + eta * vdot(r->wo, H);
+        dwh_dwo = (eta * eta * vdot(r->wo, H)) / (sqrtDenom * sqrtDenom);
+    }
+    H = vmul(H, signumf(H.z));
+    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    if (!b->sampleVisible) distr_scale_alpha(&d, 1.2f - 0.2f * sqrtf(fabsf(r->wi.z)));
+    float prob = distr_pdf(&d, vmul(r->wi, signumf(r->wi.z)), H);
+    float ct;
+    float F = fresnel_dielectric_ext(vdot(r->wi, H), &ct, b->eta);
+    prob *= reflect ? F : (1 - F);
+    return fabsf(prob * dwh_dwo);
+}
+
+/* sample(bRec, pdf, sample) of each BSDF; consumes sampler->next1D() for the
+ * roughdielectric lobe choice (roughdielectric.cpp:554) */
+static V3 bsdf_sample(const Bsdf *b, BRec *r, float *pdf, float sx, float sy, Sampler *smp) {
+    V3 zero = v3(0, 0, 0);
+    if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:139-150 */
+        if (r->wi.z <= 0) return zero;
+        r->wo = square_to_cosine_hemisphere(sx, sy);
+        r->eta = 1.0f;
+        r->sampledType = E_DIFF_REFL;
+        *pdf = cosine_hemisphere_pdf(r->wo);
+        return b->refl;
+    }
+    Distr d;
+    if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:357-406 */
+        if (r->wi.z < 0) return zero;
+        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        V3 m = distr_sample(&d, r->wi, sx, sy, pdf);
+        if (*pdf == 0) return zero;
+        r->wo = reflect_v(r->wi, m);
+        r->eta = 1.0f;
+        r->sampledType = E_GLOSSY_REFL;
+        if (r->wo.z <= 0) return zero;
+        V3 F = vmulv(fresnel_conductor_exact(vdot(r->wi, m), b->eta3, b->k3), b->specR);
+        float weight;
+        if (b->sampleVisible) weight = distr_smithG1(&d, r->wo, m);
+        else weight = distr_eval(&d, m) * distr_G(&d, r->wi, r->wo, m) * vdot(r->wi, m) / (*pdf * r->wi.z);
+        *pdf /= 4.0f * vdot(r->wo, m);
+        return vmul(F, weight);
+    }
+    /* roughdielectric.cpp:525-615 */
+    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    Distr sd = d;
+    if (!b->sampleVisible) distr_scale_alpha(&sd, 1.2f - 0.2f * sqrtf(fabsf(r->wi.z)));
+    float microfacetPDF;
+    V3 m = distr_sample(&sd, vmul(r->wi, signumf(r->wi.z)), sx, sy, &microfacetPDF);
+    if (microfacetPDF == 0) return zero;
+    *pdf = microfacetPDF;
+    float cosThetaT;
+    float F = fresnel_dielectric_ext(vdot(r->wi, m), &cosThetaT, b->eta);
+    V3 weight = v3(1.0f, 1.0f, 1.0f);
+    int sampleReflection = 1;
+    if (next1d(smp) > F) { sampleReflection = 0; *pdf *= 1 - F; }
+    else *pdf *= F;
+    float dwh_dwo;
+    if (sampleReflection) {
+        r->wo = reflect_v(r->wi, m);
+        r->eta = 1.0f;
+        r->sampledType = E_GLOSSY_REFL;
+        if (r->wi.z * r->wo.z <= 0) return zero;
+        weight = vmulv(weight, b->specR);
+        dwh_dwo = 1.0f / (4.0f * vdot(r->wo, m));
+    } else {
+        if (cosThetaT == 0) return zero;
+        r->wo = refract_v(r->wi, m, b->eta, cosThetaT);
+        r->eta = cosThetaT < 0 ? b->eta : b->invEta;
+        r->sampledType = E_GLOSSY_TRANS;
+        if (r->wi.z * r->wo.z >= 0) return zero;
+        float factor = cosThetaT < 0 ? b->invEta : b->eta;
+        weight = vmulv(weight, vmul(b->specT, factor * factor));
+        float sqrtDenom = vdot(r->wi, m) + r->eta * vdot(r->wo, m);
+        dwh_dwo = (r->eta * r->eta * vdot(r->wo, m)) / (sqrtDenom * sqrtDenom);
+    }
+    if (b->sampleVisible) weight = vmul(weight, distr_smithG1(&d, r->wo, m));
+    else weight = vmul(weight, fabsf(distr_eval(&d, m) * distr_G(&d, r->wi, r->wo, m) * vdot(r->wi, m) / (microfacetPDF * r->wi.z)));
+    *pdf *= fabsf(dwh_dwo);
+    return weight;
+}
+
+/* ------------------------------------------------------------------------ */
+/* TriAccel (render/triaccel.h:58-160)                                       */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint32_t k; float n_u, n_v, n_d, a_u, a_v, b_nu, b_nv, c_nu, c_nv; } TriAccel;
+
+static int triaccel_load(TriAccel *ta, V3 A, V3 B, V3 C) {
+    static const int waldModulo[4] = {1, 2, 0, 1};
+    V3 b = vsub(C, A), c = vsub(B, A), N = vcross(c, b);
+    ta->k = 0;
+    for (int j = 0; j < 3; j++)
+        if (fabsf(vget(N, j)) > fabsf(vget(N, (int)ta->k))) ta->k = (uint32_t)j;
+    uint32_t u = (uint32_t)waldModulo[ta->k], v = (uint32_t)waldModulo[ta->k + 1];
+    const float n_k = vget(N, (int)ta->k), denom = vget(b, (int)u) * vget(c, (int)v) - vget(b, (int)v) * vget(c, (int)u);
+    if (denom == 0) { ta->k = 3; return 1; }
+    ta->n_u = vget(N, (int)u) / n_k;
+    ta->n_v = vget(N, (int)v) / n_k;
+    ta->n_d = vdot(A, N) / n_k;
+    ta->b_nu = vget(b, (int)u) / denom;
+    ta->b_nv = -vget(b, (int)v) / denom;
+    ta->a_u = vget(A, (int)u);
+    ta->a_v = vget(A, (int)v);
+    ta->c_nu = vget(c, (int)v) / denom;
+    ta->c_nv = -vget(c, (int)u) / denom;
+    return 0;
+}
+
+static inline int triaccel_intersect(const TriAccel *ta, const Ray *ray, float mint, float maxt,
+                                     float *u, float *v, float *t) {
+    float o_u, o_v, o_k, d_u, d_v, d_k;
+    switch (ta->k) {
+        case 0: o_u = ray->o.y; o_v = ray->o.z; o_k = ray->o.x; d_u = ray->d.y; d_v = ray->d.z; d_k = ray->d.x; break;
+        case 1: o_u = ray->o.z; o_v = ray->o.x; o_k = ray->o.y; d_u = ray->d.z; d_v = ray->d.x; d_k = ray->d.y; break;
+        case 2: o_u = ray->o.x; o_v = ray->o.y; o_k = ray->o.z; d_u = ray->d.x; d_v = ray->d.y; d_k = ray->d.z; break;
+        default: return 0;
+    }
+    *t = (ta->n_d - o_u * ta->n_u - o_v * ta->n_v - o_k) / (d_u * ta->n_u + d_v * ta->n_v + d_k);
+    if (*t < mint || *t > maxt) return 0;
+    const float hu = o_u + *t * d_u - ta->a_u;
+    const float hv = o_v + *t * d_v - ta->a_v;
+    *u = hv * ta->b_nu + hu * ta->b_nv;
+    *v = hu * ta->c_nu + hv * ta->c_nv;
+    return *u >= 0 && *v >= 0 && *u + *v <= 1.0f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* scene (configure): meshes, emitters, acceleration                          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    V3 *pos, *nrm;        /* nrm NULL: face normals */
+    float *uv;
+    uint32_t *idx;
+    V3 *dpdu;             /* per-triangle UV tangent (trimesh.cpp:683-739) or NULL */
+    uint32_t nv, nt, primOffset;
+    int bsdf, emitter;
+    float *areaCdf;       /* nt+1 */
+    float invArea;
+} Mesh;
+
+typedef struct { int type; V3 radiance; float weight; int mesh; } Emitter;
+
+typedef struct { float bmin[3], bmax[3]; uint32_t left, right, first, count; } BNode;
+
+typedef struct {
+    Mesh *meshes; uint32_t nmeshes;
+    Bsdf *bsdfs; uint32_t nbsdfs; /* + defaults appended */
+    Emitter *emitters; uint32_t nemitters;
+    float *emCdf; float emNorm;
+    TriAccel *ta; uint32_t *taMesh, *taTri; uint32_t nprims;
+    BNode *nodes; uint32_t nnodes; uint32_t *order;
+    float aabbMin[3], aabbMax[3];
+    Camera cam;
+    int envIndex;
+} Scene;
+
+/* unitAngle (core/util.h:309-314) -- uses float asin */
+static float unit_angle(V3 u, V3 v) {
+    if (vdot(u, v) < 0) return M_PI_F - 2 * asinf(0.5f * vlen(vadd(v, u)));
+    return 2 * asinf(0.5f * vlen(vsub(v, u)));
+}
+
+/* DiscreteDistribution (core/pmf.h:35-169) */
+static float dd_normalize(float *cdf, uint32_t n, float *normalization) {
+    float sum = cdf[n];
+    if (sum > 0) {
+        *normalization = 1.0f / sum;
+        for (uint32_t i = 1; i < n + 1; ++i) cdf[i] *= *normalization;
+        cdf[n] = 1.0f;
+    } else {
+        *normalization = 0.0f;
+    }
+    return sum;
+}
+static uint32_t dd_sample(const float *cdf, uint32_t n, float value) {
+    /* std::lower_bound over cdf[0..n] */
+    uint32_t lo = 0, hi = n + 1;
+    while (lo < hi) { uint32_t mid = (lo + hi) / 2; if (cdf[mid] < value) lo = mid + 1; else hi = mid; }
+    long idx = (long)lo - 1; if (idx < 0) idx = 0;
+    uint32_t index = (uint32_t)idx; if (index > n - 1) index = n - 1;
+    while (cdf[index + 1] - cdf[index] == 0 && index < n - 1) ++index; /* guarded variant of :133-134 */
+    return index;
+}
+static uint32_t dd_sample_reuse(const float *cdf, uint32_t n, float *value, float *pdf) {
+    uint32_t index = dd_sample(cdf, n, *value);
+    if (pdf) *pdf = cdf[index + 1] - cdf[index];
+    *value = (*value - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return index;
+}
+
+static void compute_normals(Mesh *m, int face, int flip, const float *nin) { /* trimesh.cpp:608-681 */
+    if (face) {
+        m->nrm = NULL;
+        if (flip)
+            for (uint32_t i = 0; i < m->nt; ++i) { uint32_t t = m->idx[3 * i]; m->idx[3 * i] = m->idx[3 * i + 1]; m->idx[3 * i + 1] = t; }
+        return;
+    }
+    m->nrm = (V3 *)calloc(m->nv, sizeof(V3));
+    if (nin) {
+        for (uint32_t i = 0; i < m->nv; ++i) {
+            m->nrm[i] = v3(nin[3 * i], nin[3 * i + 1], nin[3 * i + 2]);
+            if (flip) m->nrm[i] = vmul(m->nrm[i], -1);
+        }
+        return;
+    }
+    for (uint32_t i = 0; i < m->nt; i++) {
+        V3 n = v3(0, 0, 0);
+        for (int j = 0; j < 3; ++j) {
+            V3 v0 = m->pos[m->idx[3 * i + j]], v1 = m->pos[m->idx[3 * i + (j + 1) % 3]], v2 = m->pos[m->idx[3 * i + (j + 2) % 3]];
+            V3 sideA = vsub(v1, v0), sideB = vsub(v2, v0);
+            if (j == 0) {
+                n = vcross(sideA, sideB);
+                float length = vlen(n);
+                if (length == 0) break;
+                n = vdiv(n, length);
+            }
+            float angle = unit_angle(vnormalize(sideA), vnormalize(sideB));
+            V3 *dst = &m->nrm[m->idx[3 * i + j]];
+            *dst = vadd(*dst, vmul(n, angle));
+        }
+    }
+    for (uint32_t i = 0; i < m->nv; i++) {
+        V3 n = m->nrm[i];
+        float length = vlen(n);
+        if (flip) length *= -1;
+        if (length != 0) m->nrm[i] = vdiv(n, length);
+        else m->nrm[i] = v3(1, 0, 0);
+    }
+}
+
+static void compute_uv_tangents(Mesh *m) { /* trimesh.cpp:683-739 */
+    if (!m->uv) { m->dpdu = NULL; return; }
+    m->dpdu = (V3 *)calloc(m->nt, sizeof(V3));
+    for (uint32_t i = 0; i < m->nt; i++) {
+        uint32_t i0 = m->idx[3 * i], i1 = m->idx[3 * i + 1], i2 = m->idx[3 * i + 2];
+        V3 v0 = m->pos[i0], v1 = m->pos[i1], v2 = m->pos[i2];
+        float u0 = m->uv[2 * i0], w0 = m->uv[2 * i0 + 1], u1 = m->uv[2 * i1], w1 = m->uv[2 * i1 + 1], u2 = m->uv[2 * i2], w2 = m->uv[2 * i2 + 1];
+        V3 dP1 = vsub(v1, v0), dP2 = vsub(v2, v0);
+        float dUV1x = u1 - u0, dUV1y = w1 - w0, dUV2x = u2 - u0, dUV2y = w2 - w0;
+        V3 n = vcross(dP1, dP2);
+        float length = vlen(n);
+        if (length == 0) continue;
+        float determinant = dUV1x * dUV2y - dUV1y * dUV2x;
+        if (determinant == 0) {
+            V3 b, c;
+            coordinate_system(vdiv(n, length), &b, &c);
+            m->dpdu[i] = b;
+        } else {
+            float invDet = 1.0f / determinant;
+            m->dpdu[i] = vmul(vsub(vmul(dP1, dUV2y), vmul(dP2, dUV1y)), invDet);
+        }
+    }
+}
+
+/* --- oracle BVH (median split; any exact closest-hit structure gives the same
+ * result as the reference kd-tree up to exact-t ties, which both the oracle
+ * and the product break towards the larger primitive index) -------------- */
+typedef struct { float c[3]; float bmin[3], bmax[3]; } PrimBox;
+
+static uint32_t bvh_build(Scene *S, PrimBox *pb, uint32_t *order, uint32_t first, uint32_t count, uint32_t *nnodes) {
+    uint32_t id = (*nnodes)++;
+    BNode *n = &S->nodes[id];
+    float bmin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, bmax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    float cmin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, cmax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (uint32_t i = first; i < first + count; ++i) {
+        PrimBox *p = &pb[order[i]];
+        for (int a = 0; a < 3; ++a) {
+            if (p->bmin[a] < bmin[a]) bmin[a] = p->bmin[a];
+            if (p->bmax[a] > bmax[a]) bmax[a] = p->bmax[a];
+            if (p->c[a] < cmin[a]) cmin[a] = p->c[a];
+            if (p->c[a] > cmax[a]) cmax[a] = p->c[a];
+        }
+    }
+    for (int a = 0; a < 3; ++a) { /* conservative inflation: never loses a hit */
+        float e = (bmax[a] - bmin[a]) * 1e-4f + 1e-6f * (fabsf(bmin[a]) + fabsf(bmax[a])) + 1e-30f;
+        n->bmin[a] = bmin[a] - e; n->bmax[a] = bmax[a] + e;
+    }
+    if (count <= 4) { n->first = first; n->count = count; n->left = n->right = 0; return id; }
+    int axis = 0;
+    float ext = cmax[0] - cmin[0];
+    for (int a = 1; a < 3; ++a) if (cmax[a] - cmin[a] > ext) { ext = cmax[a] - cmin[a]; axis = a; }
+    /* nth_element by centroid on axis (simple sort of the range) */
+    uint32_t mid = first + count / 2;
+    /* insertion-free quickselect */
+    uint32_t lo = first, hi = first + count - 1;
+    while (lo < hi) {
+        float pivot = pb[order[(lo + hi) / 2]].c[axis];
+        uint32_t i = lo, j = hi;
+        while (i <= j) {
+            while (pb[order[i]].c[axis] < pivot) i++;
+            while (pb[order[j]].c[axis] > pivot) { if (j == 0) break; j--; }
+            if (i <= j) { uint32_t t = order[i]; order[i] = order[j]; order[j] = t; i++; if (j == 0) break; j--; }
+        }
+        if (mid <= j) hi = j; else if (mid >= i) lo = i; else break;
+    }
+    n->count = 0;
+    uint32_t l = bvh_build(S, pb, order, first, mid - first, nnodes);
+    uint32_t r = bvh_build(S, pb, order, mid, first + count - mid, nnodes);
+    S->nodes[id].left = l; S->nodes[id].right = r; S->nodes[id].count = 0;
+    return id;
+}
+
+static void scene_free(Scene *S) {
+    for (uint32_t i = 0; i < S->nmeshes; ++i) {
+        Mesh *m = &S->meshes[i];
+        free(m->pos); free(m->nrm); free(m->uv); free(m->idx); free(m->dpdu); free(m->areaCdf);
+    }
+    free(S->meshes); free(S->bsdfs); free(S->emitters); free(S->emCdf);
+    free(S->ta); free(S->taMesh); free(S->taTri); free(S->nodes); free(S->order);
+    memset(S, 0, sizeof *S);
+}
+
+static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
+    memset(S, 0, sizeof *S);
+    S->envIndex = -1;
+    int rc = camera_configure(&D->sensor, &S->cam);
+    if (rc) return rc;
+    S->nbsdfs = D->num_bsdfs;
+    S->bsdfs = (Bsdf *)calloc(D->num_bsdfs + 2, sizeof(Bsdf));
+    for (uint32_t i = 0; i < D->num_bsdfs; ++i)
+        if ((rc = bsdf_configure(&D->bsdfs[i], &S->bsdfs[i]))) return rc;
+    /* Shape::configure default BSDFs (shape.cpp:48-70) */
+    mtsgpu_bsdf_desc dd; memset(&dd, 0, sizeof dd);
+    dd.type = MTSGPU_BSDF_DIFFUSE; dd.ensure_energy_conservation = 1;
+    bsdf_configure(&dd, &S->bsdfs[D->num_bsdfs]);           /* black, emitters */
+    dd.reflectance[0] = dd.reflectance[1] = dd.reflectance[2] = 0.5f;
+    bsdf_configure(&dd, &S->bsdfs[D->num_bsdfs + 1]);       /* 0.5 gray */
+
+    S->nemitters = D->num_emitters;
+    S->emitters = (Emitter *)calloc(D->num_emitters + 1, sizeof(Emitter));
+    for (uint32_t i = 0; i < D->num_emitters; ++i) {
+        const mtsgpu_emitter_desc *e = &D->emitters[i];
+        S->emitters[i].type = e->type;
+        S->emitters[i].radiance = v3(e->radiance[0], e->radiance[1], e->radiance[2]);
+        S->emitters[i].weight = e->sampling_weight;
+        S->emitters[i].mesh = -1;
+        if (e->type != MTSGPU_EMITTER_AREA) return MTSGPU_EINVAL; /* envmap: next row */
+    }
+    if (D->num_emitters == 0) return MTSGPU_EINVAL; /* sunsky fallback is out of scope */
+
+    S->nmeshes = D->num_meshes;
+    S->meshes = (Mesh *)calloc(D->num_meshes, sizeof(Mesh));
+    uint32_t prims = 0;
+    for (uint32_t i = 0; i < D->num_meshes; ++i) {
+        const mtsgpu_mesh_desc *md = &D->meshes[i];
+        Mesh *m = &S->meshes[i];
+        if (md->num_triangles == 0 || !md->positions || !md->indices) return MTSGPU_EINVAL;
+        m->nv = md->num_vertices; m->nt = md->num_triangles; m->primOffset = prims;
+        prims += m->nt;
+        m->pos = (V3 *)malloc(sizeof(V3) * m->nv);
+        for (uint32_t v = 0; v < m->nv; ++v) m->pos[v] = v3(md->positions[3 * v], md->positions[3 * v + 1], md->positions[3 * v + 2]);
+        m->idx = (uint32_t *)malloc(sizeof(uint32_t) * 3 * m->nt);
+        memcpy(m->idx, md->indices, sizeof(uint32_t) * 3 * m->nt);
+        for (uint32_t t = 0; t < 3 * m->nt; ++t) if (m->idx[t] >= m->nv) return MTSGPU_EINVAL;
+        if (md->texcoords) { m->uv = (float *)malloc(sizeof(float) * 2 * m->nv); memcpy(m->uv, md->texcoords, sizeof(float) * 2 * m->nv); }
+        m->emitter = md->emitter;
+        if (md->emitter >= (int)D->num_emitters) return MTSGPU_EINVAL;
+        if (md->bsdf >= 0) { if (md->bsdf >= (int)D->num_bsdfs) return MTSGPU_EINVAL; m->bsdf = md->bsdf; }
+        else m->bsdf = (md->emitter >= 0) ? (int)D->num_bsdfs : (int)D->num_bsdfs + 1;
+        if (md->emitter >= 0) {
+            if (S->emitters[md->emitter].mesh >= 0) return MTSGPU_EINVAL;
+            S->emitters[md->emitter].mesh = (int)i;
+        }
+        compute_normals(m, md->face_normals, md->flip_normals, md->normals);
+        compute_uv_tangents(m);
+        if (md->emitter >= 0) { /* TriMesh::prepareSamplingTable (trimesh.cpp:389-404) */
+            m->areaCdf = (float *)malloc(sizeof(float) * (m->nt + 1));
+            m->areaCdf[0] = 0.0f;
+            for (uint32_t t = 0; t < m->nt; ++t) {
+                V3 p0 = m->pos[m->idx[3 * t]], p1 = m->pos[m->idx[3 * t + 1]], p2 = m->pos[m->idx[3 * t + 2]];
+                float area = 0.5f * vlen(vcross(vsub(p1, p0), vsub(p2, p0))); /* triangle.cpp:60-66 */
+                m->areaCdf[t + 1] = m->areaCdf[t] + area;
+            }
+            float norm;
+            float surfaceArea = dd_normalize(m->areaCdf, m->nt, &norm);
+            m->invArea = 1.0f / surfaceArea;
+        }
+    }
+    for (uint32_t i = 0; i < S->nemitters; ++i)
+        if (S->emitters[i].type == MTSGPU_EMITTER_AREA && S->emitters[i].mesh < 0) return MTSGPU_EINVAL;
+    /* Scene::initialize emitter PDF (scene.cpp:376-381) */
+    S->emCdf = (float *)malloc(sizeof(float) * (S->nemitters + 1));
+    S->emCdf[0] = 0.0f;
+    for (uint32_t i = 0; i < S->nemitters; ++i) S->emCdf[i + 1] = S->emCdf[i] + S->emitters[i].weight;
+    dd_normalize(S->emCdf, S->nemitters, &S->emNorm);
+
+    /* TriAccel precompute (skdtree.cpp:74-109) + scene bounds (gkdtree.h:996-1001,1211-1217) */
+    S->nprims = prims;
+    S->ta = (TriAccel *)malloc(sizeof(TriAccel) * prims);
+    S->taMesh = (uint32_t *)malloc(sizeof(uint32_t) * prims);
+    S->taTri = (uint32_t *)malloc(sizeof(uint32_t) * prims);
+    PrimBox *pb = (PrimBox *)malloc(sizeof(PrimBox) * prims);
+    float amin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, amax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+    for (uint32_t i = 0; i < S->nmeshes; ++i) {
+        Mesh *m = &S->meshes[i];
+        for (uint32_t t = 0; t < m->nt; ++t) {
+            uint32_t p = m->primOffset + t;
+            V3 A = m->pos[m->idx[3 * t]], B = m->pos[m->idx[3 * t + 1]], C = m->pos[m->idx[3 * t + 2]];
+            triaccel_load(&S->ta[p], A, B, C);
+            S->taMesh[p] = i; S->taTri[p] = t;
+            for (int a = 0; a < 3; ++a) {
+                float x0 = vget(A, a), x1 = vget(B, a), x2 = vget(C, a);
+                float lo = x0, hi = x0;
+                if (x1 < lo) lo = x1;
+                if (x1 > hi) hi = x1;
+                if (x2 < lo) lo = x2;
+                if (x2 > hi) hi = x2;
+                pb[p].bmin[a] = lo; pb[p].bmax[a] = hi;
+                pb[p].c[a] = 0.5f * (lo + hi);
+                if (lo < amin[a]) amin[a] = lo;
+                if (hi > amax[a]) amax[a] = hi;
+            }
+        }
+    }
+    const float eps = 1e-3f; /* MTS_KD_AABB_EPSILON */
+    for (int a = 0; a < 3; ++a) {
+        amin[a] -= (amax[a] - amin[a]) * eps + eps;
+        amax[a] += (amax[a] - amin[a]) * eps + eps;
+        S->aabbMin[a] = amin[a]; S->aabbMax[a] = amax[a];
+    }
+    S->order = (uint32_t *)malloc(sizeof(uint32_t) * prims);
+    for (uint32_t i = 0; i < prims; ++i) S->order[i] = i;
+    S->nodes = (BNode *)malloc(sizeof(BNode) * (2 * prims + 1));
+    uint32_t nn = 0;
+    bvh_build(S, pb, S->order, 0, prims, &nn);
+    S->nnodes = nn;
+    free(pb);
+    return MTSGPU_OK;
+}
+
+/* AABB::rayIntersect (core/aabb.h:308-338) on the scene bounds */
+static int aabb_ray(const float *mn, const float *mx, const Ray *ray, float *nearT, float *farT) {
+    *nearT = -INFINITY; *farT = INFINITY;
+    for (int i = 0; i < 3; i++) {
+        const float origin = vget(ray->o, i);
+        const float minVal = mn[i], maxVal = mx[i];
+        if (vget(ray->d, i) == 0) {
+            if (origin < minVal || origin > maxVal) return 0;
+        } else {
+            float t1 = (minVal - origin) * vget(ray->dRcp, i);
+            float t2 = (maxVal - origin) * vget(ray->dRcp, i);
+            if (t1 > t2) { float t = t1; t1 = t2; t2 = t; }
+            *nearT = smax(t1, *nearT);
+            *farT = smin(t2, *farT);
+            if (!(*nearT <= *farT)) return 0;
+        }
+    }
+    return 1;
+}
+
+static inline int node_hit(const BNode *n, const Ray *r, float tmin, float tmax) {
+    float t0 = tmin, t1 = tmax;
+    for (int a = 0; a < 3; ++a) {
+        float o = vget(r->o, a), inv = vget(r->dRcp, a);
+        float ta = (n->bmin[a] - o) * inv, tb = (n->bmax[a] - o) * inv;
+        if (ta != ta || tb != tb) { /* 0*inf: origin on the slab plane */
+            if (o < n->bmin[a] || o > n->bmax[a]) return 0;
+            continue;
+        }
+        if (ta > tb) { float t = ta; ta = tb; tb = t; }
+        if (ta > t0) t0 = ta;
+        if (tb < t1) t1 = tb;
+        if (t0 > t1) return 0;
+    }
+    return 1;
+}
+
+typedef struct { uint64_t rays, shadow, tests, nodes; } Counters;
+
+/* closest hit over [mint, maxt] (the clipped interval ShapeKDTree passes to
+ * rayIntersectHavran, sahkdtree3.h:178-308); ties -> larger prim index */
+static int trace_closest(const Scene *S, const Ray *ray, float mint, float maxt,
+                         uint32_t *prim, float *tu, float *tv, float *tt, Counters *C) {
+    uint32_t stack[128]; int sp = 0;
+    stack[sp++] = 0;
+    int found = 0; uint32_t best = 0; float bt = maxt, bu = 0, bv = 0;
+    while (sp) {
+        const BNode *n = &S->nodes[stack[--sp]];
+        C->nodes++;
+        if (!node_hit(n, ray, mint, bt)) continue;
+        if (n->count) {
+            for (uint32_t i = n->first; i < n->first + n->count; ++i) {
+                uint32_t p = S->order[i];
+                float u, v, t;
+                C->tests++;
+                if (triaccel_intersect(&S->ta[p], ray, mint, bt, &u, &v, &t)) {
+                    if (!found || t < bt || p > best) { found = 1; best = p; bt = t; bu = u; bv = v; }
+                }
+            }
+        } else {
+            stack[sp++] = n->right; stack[sp++] = n->left;
+        }
+    }
+    if (found) { *prim = best; *tu = bu; *tv = bv; *tt = bt; }
+    return found;
+}
+static int trace_any(const Scene *S, const Ray *ray, float mint, float maxt, Counters *C) {
+    uint32_t stack[128]; int sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const BNode *n = &S->nodes[stack[--sp]];
+        C->nodes++;
+        if (!node_hit(n, ray, mint, maxt)) continue;
+        if (n->count) {
+            for (uint32_t i = n->first; i < n->first + n->count; ++i) {
+                float u, v, t;
+                C->tests++;
+                if (triaccel_intersect(&S->ta[S->order[i]], ray, mint, maxt, &u, &v, &t)) return 1;
+            }
+        } else {
+            stack[sp++] = n->right; stack[sp++] = n->left;
+        }
+    }
+    return 0;
+}
+
+typedef struct {
+    int valid;
+    float t;
+    V3 p, geoN, wi;
+    Frame sh;
+    int mesh; uint32_t tri;
+} Its;
+
+/* ShapeKDTree::rayIntersect(ray, its) (skdtree.cpp:112-142) + fillIntersectionRecord<true>
+ * (skdtree.h:343-429) */
+static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *C) {
+    float mint, maxt;
+    its->valid = 0;
+    its->t = INFINITY;
+    C->rays++;
+    if (!aabb_ray(S->aabbMin, S->aabbMax, ray, &mint, &maxt)) return;
+    float rayMinT = ray->mint;
+    if (rayMinT == EPSILON)
+        rayMinT *= smax(smax(smax(fabsf(ray->o.x), fabsf(ray->o.y)), fabsf(ray->o.z)), EPSILON);
+    if (rayMinT > mint) mint = rayMinT;
+    if (ray->maxt < maxt) maxt = ray->maxt;
+    if (!(maxt > mint)) return;
+    uint32_t prim; float u, v, t;
+    if (!trace_closest(S, ray, mint, maxt, &prim, &u, &v, &t, C)) return;
+    const Mesh *m = &S->meshes[S->taMesh[prim]];
+    uint32_t tri = S->taTri[prim];
+    its->valid = 1; its->t = t; its->mesh = (int)S->taMesh[prim]; its->tri = tri;
+    const float bx = 1 - u - v, by = u, bz = v;
+    const uint32_t i0 = m->idx[3 * tri], i1 = m->idx[3 * tri + 1], i2 = m->idx[3 * tri + 2];
+    V3 p0 = m->pos[i0], p1 = m->pos[i1], p2 = m->pos[i2];
+    its->p = vadd(vadd(vmul(p0, bx), vmul(p1, by)), vmul(p2, bz));
+    V3 side1 = vsub(p1, p0), side2 = vsub(p2, p0);
+    V3 faceNormal = vcross(side1, side2);
+    float length = vlen(faceNormal);
+    if (!vzero(faceNormal)) faceNormal = vdiv(faceNormal, length);
+    V3 dpdu = m->dpdu ? m->dpdu[tri] : side1;
+    V3 shN;
+    if (m->nrm) {
+        shN = vnormalize(vadd(vadd(vmul(m->nrm[i0], bx), vmul(m->nrm[i1], by)), vmul(m->nrm[i2], bz)));
+        if (vdot(faceNormal, shN) < 0) faceNormal = vneg(faceNormal);
+    } else {
+        shN = faceNormal;
+    }
+    its->geoN = faceNormal;
+    compute_shading_frame(shN, dpdu, &its->sh);
+    its->wi = to_local(&its->sh, vneg(ray->d));
+}
+
+/* ShapeKDTree::rayIntersect(ray) shadow variant (skdtree.cpp:207-226) */
+static int scene_occluded(const Scene *S, const Ray *ray, Counters *C) {
+    float mint, maxt;
+    C->shadow++;
+    if (!aabb_ray(S->aabbMin, S->aabbMax, ray, &mint, &maxt)) return 0;
+    float rayMinT = ray->mint;
+    if (rayMinT == EPSILON)
+        rayMinT *= smax(smax(fabsf(ray->o.x), fabsf(ray->o.y)), fabsf(ray->o.z));
+    if (rayMinT > mint) mint = rayMinT;
+    if (ray->maxt < maxt) maxt = ray->maxt;
+    if (!(maxt > mint)) return 0;
+    return trace_any(S, ray, mint, maxt, C);
+}
+
+/* ------------------------------------------------------------------------ */
+/* direct emitter sampling                                                   */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    V3 ref, refN, p, n, d;
+    float dist, pdf;
+    int measureSolidAngle;
+    int emitter;
+} DRec;
+
+/* AreaLight::eval (area.cpp:104-109) */
+static V3 its_Le(const Scene *S, const Its *its, V3 d) {
+    const Emitter *e = &S->emitters[S->meshes[its->mesh].emitter];
+    if (vdot(its->sh.n, d) <= 0) return v3(0, 0, 0);
+    return e->radiance;
+}
+
+/* Scene::sampleEmitterDirect (scene.cpp:828-852) -> AreaLight::sampleDirect
+ * (area.cpp:158-173) -> Shape::sampleDirect (shape.cpp:102-115) ->
+ * TriMesh::samplePosition (trimesh.cpp:412-425) -> Triangle::sample (triangle.cpp:24-58) */
+static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, Counters *C) {
+    V3 zero = v3(0, 0, 0);
+    float emPdf;
+    uint32_t index = dd_sample_reuse(S->emCdf, S->nemitters, &sx, &emPdf);
+    const Emitter *e = &S->emitters[index];
+    const Mesh *m = &S->meshes[e->mesh];
+    /* samplePosition */
+    float py = sy;
+    uint32_t tri = dd_sample_reuse(m->areaCdf, m->nt, &py, NULL);
+    V3 p0 = m->pos[m->idx[3 * tri]], p1 = m->pos[m->idx[3 * tri + 1]], p2 = m->pos[m->idx[3 * tri + 2]];
+    float a = safe_sqrt(1.0f - sx);              /* warp::squareToUniformTriangle (warp.cpp:76-79) */
+    float bx = 1 - a, by = a * py;
+    V3 sideA = vsub(p1, p0), sideB = vsub(p2, p0);
+    dRec->p = vadd(vadd(p0, vmul(sideA, bx)), vmul(sideB, by));
+    if (m->nrm) {
+        V3 n0 = m->nrm[m->idx[3 * tri]], n1 = m->nrm[m->idx[3 * tri + 1]], n2 = m->nrm[m->idx[3 * tri + 2]];
+        dRec->n = vnormalize(vadd(vadd(vmul(n0, 1.0f - bx - by), vmul(n1, bx)), vmul(n2, by)));
+    } else {
+        dRec->n = vnormalize(vcross(sideA, sideB));
+    }
+    dRec->pdf = m->invArea;
+    /* Shape::sampleDirect */
+    dRec->d = vsub(dRec->p, dRec->ref);
+    float distSquared = vlen2(dRec->d);
+    dRec->dist = sqrtf(distSquared);
+    dRec->d = vdiv(dRec->d, dRec->dist);
+    float dp = vabsdot(dRec->d, dRec->n);
+    dRec->pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+    dRec->measureSolidAngle = 1;
+    V3 value;
+    if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0 && dRec->pdf != 0) {
+        value = vdiv(e->radiance, dRec->pdf);
+    } else {
+        dRec->pdf = 0.0f;
+        value = zero;
+    }
+    if (dRec->pdf != 0) {
+        Ray sray;
+        sray.o = dRec->ref;
+        ray_set_dir(&sray, dRec->d);
+        sray.mint = EPSILON;
+        sray.maxt = dRec->dist * (1 - SHADOW_EPSILON);
+        sray.hasDiff = 0;
+        if (scene_occluded(S, &sray, C)) return zero;
+        dRec->emitter = (int)index;
+        dRec->pdf *= emPdf;
+        value = vdiv(value, emPdf);
+        return value;
+    }
+    return zero;
+}
+
+/* Scene::pdfEmitterDirect (scene.cpp:949-952) -> AreaLight::pdfDirect (area.cpp:175-181)
+ * -> Shape::pdfDirect (shape.cpp:117-126); pdfEmitterDiscrete (scene.h:848-850) */
+static float pdf_emitter_direct(const Scene *S, const DRec *dRec) {
+    const Emitter *e = &S->emitters[dRec->emitter];
+    float pdf = 0.0f;
+    if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0) {
+        float pdfPos = S->meshes[e->mesh].invArea;
+        pdf = pdfPos * (dRec->dist * dRec->dist) / vabsdot(dRec->d, dRec->n);
+    }
+    return pdf * (e->weight * S->emNorm);
+}
+
+static inline float mi_weight(float pdfA, float pdfB) { /* path.cpp:296-300 */
+    pdfA *= pdfA; pdfB *= pdfB;
+    return pdfA / (pdfA + pdfB);
+}
+
+/* ------------------------------------------------------------------------ */
+/* MIPathTracer::Li (integrators/path/path.cpp:119-294)                      */
+/* ------------------------------------------------------------------------ */
+typedef struct { int maxDepth, rrDepth, strict, hide, hasAlpha; } PathParams;
+
+static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *alpha, int *depthOut, Counters *C) {
+    Its its;
+    V3 L = v3(0, 0, 0);
+    int scattered = 0;
+    int emitted = 1; /* RadianceQueryRecord::EEmittedRadiance, cleared after the first bounce */
+    int depth = 1;
+    scene_intersect(S, &ray, &its, C);       /* rRec.rayIntersect(ray) (records.inl:117-144) */
+    *alpha = P->hasAlpha ? (its.valid ? 1.0f : 0.0f) : 1.0f;
+    ray.mint = EPSILON;
+    V3 throughput = v3(1.0f, 1.0f, 1.0f);
+    float eta = 1.0f;
+    while (depth <= P->maxDepth || P->maxDepth < 0) {
+        if (!its.valid) {
+            /* no environment emitter in this row: evalEnvironment = 0 */
+            break;
+        }
+        const Bsdf *bsdf = &S->bsdfs[S->meshes[its.mesh].bsdf];
+        int isEmitter = S->meshes[its.mesh].emitter >= 0;
+        if (isEmitter && emitted && (!P->hide || scattered))
+            L = vadd(L, vmulv(throughput, its_Le(S, &its, vneg(ray.d))));
+        if ((depth >= P->maxDepth && P->maxDepth > 0) ||
+            (P->strict && vdot(ray.d, its.geoN) * its.wi.z >= 0))
+            break;
+
+        DRec dRec;
+        memset(&dRec, 0, sizeof dRec);
+        dRec.ref = its.p;
+        dRec.refN = (bsdf->flags & (E_TRANSMISSION | E_BACK)) == 0 ? its.sh.n : v3(0, 0, 0);
+        if (bsdf->flags & E_SMOOTH) {
+            float nx, ny;
+            next2d(smp, &nx, &ny);
+            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C);
+            if (!vzero(value)) {
+                BRec bRec;
+                bRec.wi = its.wi;
+                bRec.wo = to_local(&its.sh, dRec.d);
+                V3 bsdfVal = bsdf_eval(bsdf, &bRec);
+                if (!vzero(bsdfVal) && (!P->strict || vdot(its.geoN, dRec.d) * bRec.wo.z > 0)) {
+                    float bsdfPdf = dRec.measureSolidAngle ? bsdf_pdf(bsdf, &bRec) : 0;
+                    float weight = mi_weight(dRec.pdf, bsdfPdf);
+                    L = vadd(L, vmul(vmulv(vmulv(throughput, value), bsdfVal), weight));
+                }
+            }
+        }
+
+        float bsdfPdf;
+        BRec bRec;
+        bRec.wi = its.wi; bRec.eta = 1.0f; bRec.sampledType = 0;
+        float bx, by;
+        next2d(smp, &bx, &by);
+        V3 bsdfWeight = bsdf_sample(bsdf, &bRec, &bsdfPdf, bx, by, smp);
+        if (vzero(bsdfWeight)) break;
+        scattered |= bRec.sampledType != E_NULL;
+        const V3 wo = to_world(&its.sh, bRec.wo);
+        float woDotGeoN = vdot(its.geoN, wo);
+        if (P->strict && woDotGeoN * bRec.wo.z <= 0) break;
+
+        int hitEmitter = 0;
+        V3 value = v3(0, 0, 0);
+        Ray nray;
+        nray.o = its.p; ray_set_dir(&nray, wo); nray.mint = EPSILON; nray.maxt = INFINITY; nray.hasDiff = 0;
+        ray = nray;
+        scene_intersect(S, &ray, &its, C);
+        if (its.valid) {
+            if (S->meshes[its.mesh].emitter >= 0) {
+                value = its_Le(S, &its, vneg(ray.d));
+                /* DirectSamplingRecord::setQuery (records.inl:168-176) */
+                dRec.p = its.p; dRec.n = its.sh.n; dRec.measureSolidAngle = 1;
+                dRec.emitter = S->meshes[its.mesh].emitter; dRec.d = ray.d; dRec.dist = its.t;
+                hitEmitter = 1;
+            }
+        } else {
+            break; /* no environment emitter */
+        }
+        throughput = vmulv(throughput, bsdfWeight);
+        eta *= bRec.eta;
+        if (hitEmitter) {
+            float lumPdf = !(bRec.sampledType & E_DELTA) ? pdf_emitter_direct(S, &dRec) : 0;
+            L = vadd(L, vmul(vmulv(throughput, value), mi_weight(bsdfPdf, lumPdf)));
+        }
+        if (!its.valid) break;
+        emitted = 0;
+        if (depth++ >= P->rrDepth) {
+            float q = smin(smaxc(throughput) * eta * eta, (float)0.95f);
+            if (next1d(smp) >= q) break;
+            throughput = vdiv(throughput, q);
+        }
+        if (smp->err) break;
+    }
+    *depthOut = depth;
+    return L;
+}
+
+/* ------------------------------------------------------------------------ */
+/* film: ImageBlock::put (render/imageblock.h:124-204) + rfilter LUT          */
+/* (libcore/rfilter.cpp:37-55, rfilters/box.cpp, rfilters/gaussian.cpp)       */
+/* ------------------------------------------------------------------------ */
+typedef struct { float radius, scale; float values[FILTER_RES + 1]; int border; } Filter;
+
+static int filter_configure(int type, float param, Filter *f) {
+    float stddev = 0;
+    if (type == MTSGPU_RFILTER_BOX) f->radius = param + 1e-5f;
+    else if (type == MTSGPU_RFILTER_GAUSSIAN) { stddev = param; f->radius = 4 * stddev; }
+    else return MTSGPU_EINVAL;
+    if (!(f->radius > 0)) return MTSGPU_EINVAL;
+    float sum = 0.0f;
+    for (int i = 0; i < FILTER_RES; ++i) {
+        float x = (f->radius * i) / FILTER_RES, value;
+        if (type == MTSGPU_RFILTER_BOX) value = fabsf(x) <= f->radius ? 1.0f : 0.0f;
+        else {
+            float alpha = -1.0f / (2.0f * stddev * stddev);
+            value = smax((float)0.0f, o_fastexp(alpha * x * x) - o_fastexp(alpha * f->radius * f->radius));
+        }
+        f->values[i] = value;
+        sum += value;
+    }
+    f->values[FILTER_RES] = 0.0f;
+    f->scale = FILTER_RES / f->radius;
+    f->border = (int)ceilf(f->radius - 0.5f);
+    sum *= 2 * f->radius / FILTER_RES;
+    float normalization = 1.0f / sum;
+    for (int i = 0; i < FILTER_RES; ++i) f->values[i] *= normalization;
+    return MTSGPU_OK;
+}
+static inline float filter_eval_disc(const Filter *f, float x) {
+    int i = (int)fabsf(x * f->scale);
+    if (FILTER_RES < i) i = FILTER_RES;
+    return f->values[i];
+}
+
+/* splat into the 32x32 block that renders pixel (px,py); own-pixel weight goes
+ * to `own`, every other touched pixel to `spill` (film layout, border b) */
+static int film_put(const Filter *f, int W, int H, int px, int py, float sx, float sy,
+                    const float *val5, float *own, float *spill, int fw, int fh) {
+    for (int i = 0; i < 5; ++i)
+        if (!isfinite(val5[i]) || val5[i] < 0) return 0;
+    const int b = f->border;
+    const int bx = (px / BLOCK_SIZE) * BLOCK_SIZE, by = (py / BLOCK_SIZE) * BLOCK_SIZE;
+    /* the block bitmap is allocated at blockSize + 2b even for partial blocks
+       (renderproc.cpp:68-86 only resets the logical size) */
+    const int bw = BLOCK_SIZE + 2 * b, bh = BLOCK_SIZE + 2 * b;
+    (void)W; (void)H;
+    const float posx = sx - 0.5f - (float)(bx - b), posy = sy - 0.5f - (float)(by - b);
+    int minx = (int)ceilf(posx - f->radius), miny = (int)ceilf(posy - f->radius);
+    int maxx = (int)floorf(posx + f->radius), maxy = (int)floorf(posy + f->radius);
+    if (minx < 0) minx = 0;
+    if (miny < 0) miny = 0;
+    if (maxx > bw - 1) maxx = bw - 1;
+    if (maxy > bh - 1) maxy = bh - 1;
+    float wx[64], wy[64];
+    for (int x = minx, i = 0; x <= maxx; ++x) wx[i++] = filter_eval_disc(f, x - posx);
+    for (int y = miny, i = 0; y <= maxy; ++y) wy[i++] = filter_eval_disc(f, y - posy);
+    for (int y = miny, yr = 0; y <= maxy; ++y, ++yr) {
+        for (int x = minx, xr = 0; x <= maxx; ++x, ++xr) {
+            const float weight = wx[xr] * wy[yr];
+            int gx = x + bx, gy = y + by; /* film coordinates (border included) */
+            if (gx >= fw || gy >= fh) continue; /* Bitmap::accumulate clips to the film */
+            float *dst = (gx == px + b && gy == py + b) ? own : spill;
+            dst += ((size_t)gy * fw + gx) * 5;
+            for (int k = 0; k < 5; ++k) dst[k] += weight * val5[k];
+        }
+    }
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* SamplingIntegrator::renderBlock (librender/integrator.cpp:140-188)        */
+/* ------------------------------------------------------------------------ */
+int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
+                  float *film, float *samples, mtsgpu_stats *stats, int libm_mode, int threads) {
+    if (!g_sobol_ready) return MTSGPU_ESTATE;
+    if (!scene || !P || !film) return MTSGPU_EINVAL;
+    if (P->spp == 0 || P->rr_depth <= 0 || (P->max_depth <= 0 && P->max_depth != -1)) return MTSGPU_EINVAL;
+    g_cr = libm_mode;
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    if (rc) { scene_free(&S); return rc; }
+    Filter F;
+    if ((rc = filter_configure(P->rfilter, P->rfilter_param, &F))) { scene_free(&S); return rc; }
+    const int W = (int)scene->sensor.film_width, H = (int)scene->sensor.film_height;
+    if (P->x0 + P->width > (uint32_t)W || P->y0 + P->height > (uint32_t)H) { scene_free(&S); return MTSGPU_EINVAL; }
+    const int b = F.border, fw = W + 2 * b, fh = H + 2 * b;
+    const size_t filmFloats = (size_t)fw * fh * 5;
+    float *spill = (float *)calloc(filmFloats, sizeof(float));
+    memset(film, 0, filmFloats * sizeof(float));
+    PathParams PP = {P->max_depth, P->rr_depth, P->strict_normals, P->hide_emitters, P->has_alpha};
+    const uint32_t rb = P->row_block ? P->row_block : 1, rs = P->row_stride ? P->row_stride : 1;
+    Counters tot = {0, 0, 0, 0};
+    uint64_t pathLen = 0, nsamples = 0;
+    int err = 0;
+    const float diffScale = 1.0f / sqrtf((float)P->spp); (void)diffScale;
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : pathLen, nsamples) reduction(| : err)
+#endif
+    for (long pi = 0; pi < (long)P->width * P->height; ++pi) {
+        const int lx = (int)(pi % P->width), ly = (int)(pi / P->width);
+        const int px = (int)P->x0 + lx, py = (int)P->y0 + ly;
+        if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
+        Sampler smp;
+        sampler_init(&smp, P->scramble, (uint32_t)W, (uint32_t)H);
+        sampler_generate(&smp, px, py);
+        Counters C = {0, 0, 0, 0};
+        for (uint32_t j = 0; j < P->spp; ++j) {
+            float ux, uy;
+            next2d(&smp, &ux, &uy);
+            const float sx = (float)px + ux, sy = (float)py + uy;
+            Ray ray;
+            camera_sample_ray(&S.cam, sx, sy, &ray);
+            float alpha; int depth;
+            V3 L = Li(&S, &PP, ray, &smp, &alpha, &depth, &C);
+            if (smp.err) err = 1;
+            pathLen += (uint64_t)depth; nsamples++;
+            float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};
+#ifdef _OPENMP
+            if (threads != 1) {
+                /* spill pixels are shared between threads */
+#pragma omp critical(oracle_film)
+                film_put(&F, W, H, px, py, sx, sy, val5, film, spill, fw, fh);
+            } else
+#endif
+            film_put(&F, W, H, px, py, sx, sy, val5, film, spill, fw, fh);
+            if (samples) {
+                float *rec = samples + ((size_t)pi * P->spp + j) * MTSGPU_SAMPLE_RECORD_FLOATS;
+                rec[0] = L.x; rec[1] = L.y; rec[2] = L.z; rec[3] = alpha;
+                rec[4] = sx; rec[5] = sy; rec[6] = (float)depth; rec[7] = smp.err ? 1.0f : 0.0f;
+            }
+            sampler_set_index(&smp, smp.sampleIndex + 1);
+        }
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        tot.rays += C.rays;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        tot.shadow += C.shadow;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        tot.tests += C.tests;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        tot.nodes += C.nodes;
+    }
+    for (size_t i = 0; i < filmFloats; ++i) film[i] += spill[i];
+    free(spill);
+    if (stats) {
+        memset(stats, 0, sizeof *stats);
+        stats->samples = nsamples; stats->rays = tot.rays; stats->shadow_rays = tot.shadow;
+        stats->path_length_sum = pathLen; stats->node_visits = tot.nodes; stats->tri_tests = tot.tests;
+    }
+    scene_free(&S);
+    return err ? MTSGPU_EDIM : MTSGPU_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+/* unit-level probes                                                          */
+/* ------------------------------------------------------------------------ */
+int oracle_triaccel_load(const float *A, const float *B, const float *C, float *out10) {
+    TriAccel ta;
+    int r = triaccel_load(&ta, v3(A[0], A[1], A[2]), v3(B[0], B[1], B[2]), v3(C[0], C[1], C[2]));
+    uint32_t k = ta.k; memcpy(&out10[0], &k, 4);
+    out10[1] = ta.n_u; out10[2] = ta.n_v; out10[3] = ta.n_d; out10[4] = ta.a_u; out10[5] = ta.a_v;
+    out10[6] = ta.b_nu; out10[7] = ta.b_nv; out10[8] = ta.c_nu; out10[9] = ta.c_nv;
+    return r;
+}
+int oracle_triaccel_intersect(const float *t10, const float *o, const float *d, float mint, float maxt, float *uvt) {
+    TriAccel ta; memcpy(&ta.k, &t10[0], 4);
+    ta.n_u = t10[1]; ta.n_v = t10[2]; ta.n_d = t10[3]; ta.a_u = t10[4]; ta.a_v = t10[5];
+    ta.b_nu = t10[6]; ta.b_nv = t10[7]; ta.c_nu = t10[8]; ta.c_nv = t10[9];
+    Ray r; r.o = v3(o[0], o[1], o[2]); ray_set_dir(&r, v3(d[0], d[1], d[2]));
+    return triaccel_intersect(&ta, &r, mint, maxt, &uvt[0], &uvt[1], &uvt[2]);
+}
+int oracle_camera(const mtsgpu_sensor_desc *s, float *m16, float *dxdy6) {
+    Camera c;
+    int rc = camera_configure(s, &c);
+    if (rc) return rc;
+    for (int i = 0; i < 4; ++i) for (int j = 0; j < 4; ++j) m16[i * 4 + j] = c.sampleToCamera.m[i][j];
+    dxdy6[0] = c.dx.x; dxdy6[1] = c.dx.y; dxdy6[2] = c.dx.z;
+    dxdy6[3] = c.dy.x; dxdy6[4] = c.dy.y; dxdy6[5] = c.dy.z;
+    return MTSGPU_OK;
+}
+
+/* one BSDF::sample(bRec, pdf, sample) with a replayable 1D sample u3[2]
+ * (the FakeSampler of test_chisquare.cpp:58-88) */
+int oracle_bsdf_sample(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *u3,
+                       float *wo3, float *weight3, float *pdf, float *eta, int libm_mode) {
+    g_cr = libm_mode;
+    Bsdf b;
+    int rc = bsdf_configure(bd, &b);
+    if (rc) return rc;
+    /* replay: a one-dimension Sobol index that returns u3[2] is not available,
+     * so next1D is served from a tiny stub sampler */
+    Sampler s; memset(&s, 0, sizeof s);
+    BRec r; r.wi = v3(wi3[0], wi3[1], wi3[2]); r.eta = 1.0f; r.sampledType = 0;
+    V3 w;
+    if (b.type == MTSGPU_BSDF_ROUGHDIELECTRIC) {
+        /* emulate next1D() = u3[2] by sampling dimension 0 of index 0 -> 0.0 is
+         * not general; instead evaluate the lobe choice explicitly */
+        Distr d; distr_init(&d, b.distr, b.alphaU, b.alphaV, b.sampleVisible);
+        (void)d;
+        /* run the shared code with a sampler whose next1D returns u3[2]:
+         * use a Sobol index 0 with scramble = u3[2] bits */
+        uint32_t bits = (uint32_t)((double)u3[2] * 4294967296.0);
+        s.scramble = bits; s.sobolIndex = 0; s.sampleIndex = 0; s.dim = 6; s.logRes = 0;
+        w = bsdf_sample(&b, &r, pdf, u3[0], u3[1], &s);
+    } else {
+        w = bsdf_sample(&b, &r, pdf, u3[0], u3[1], &s);
+    }
+    wo3[0] = r.wo.x; wo3[1] = r.wo.y; wo3[2] = r.wo.z;
+    weight3[0] = w.x; weight3[1] = w.y; weight3[2] = w.z;
+    *eta = r.eta;
+    return (int)r.sampledType;
+}
+int oracle_bsdf_eval(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *wo3,
+                     float *value3, float *pdf, int libm_mode) {
+    g_cr = libm_mode;
+    Bsdf b;
+    int rc = bsdf_configure(bd, &b);
+    if (rc) return rc;
+    BRec r; r.wi = v3(wi3[0], wi3[1], wi3[2]); r.wo = v3(wo3[0], wo3[1], wo3[2]); r.eta = 1; r.sampledType = 0;
+    V3 v = bsdf_eval(&b, &r);
+    value3[0] = v.x; value3[1] = v.y; value3[2] = v.z;
+    *pdf = bsdf_pdf(&b, &r);
+    return MTSGPU_OK;
+}

@@ -1,0 +1,46 @@
+/*
+ * mts_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of Mitsuba 0.6's `path` integrator hot path, used as the
+ * parity checker for the HIP product (libmtsgpu.so) and as the timed CPU
+ * baseline ("port") in bench.py.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product never does.
+ *
+ * Parity pinning: see oracle/mts_oracle.c header and DESIGN.md section 3.
+ */
+#ifndef MTS_ORACLE_H
+#define MTS_ORACLE_H
+
+#include "../include/mtsgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* libm mode: 0 = glibc float functions exactly as the reference calls them;
+ * 1 = correctly-rounded-by-double evaluation (the product's device libm). */
+int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *params,
+                  float *film, float *samples, mtsgpu_stats *stats,
+                  int libm_mode, int threads);
+
+/* Unit-level entry points (tests/) */
+int oracle_sobol_init(const char *joe_kuo_path);
+float oracle_sobol_sample(uint64_t index, uint32_t dim, uint32_t scramble);
+uint64_t oracle_sobol_lookup(uint32_t m, uint32_t frame, uint32_t px, uint32_t py, uint64_t scramble);
+uint32_t oracle_sobol_matrix(uint32_t dim, uint32_t col);
+/* TriAccel load + test (triaccel.h:58-160); out = {k,n_u,n_v,n_d,a_u,a_v,b_nu,b_nv,c_nu,c_nv} */
+int oracle_triaccel_load(const float *A, const float *B, const float *C, float *out10);
+int oracle_triaccel_intersect(const float *ta10, const float *o, const float *d,
+                              float mint, float maxt, float *uvt);
+/* Camera: returns sampleToCamera (16) and near-plane differentials dx,dy (3+3) */
+int oracle_camera(const mtsgpu_sensor_desc *s, float *sample_to_camera16, float *dxdy6);
+/* Microfacet / BSDF probes for consistency tests: see mts_oracle.c */
+int oracle_bsdf_sample(const mtsgpu_bsdf_desc *b, const float *wi3, const float *u3,
+                       float *wo3, float *weight3, float *pdf, float *eta, int libm_mode);
+int oracle_bsdf_eval(const mtsgpu_bsdf_desc *b, const float *wi3, const float *wo3,
+                     float *value3, float *pdf, int libm_mode);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,64 @@
+"""GPU parity: libmtsgpu.so (HIP, gfx950) vs the CPU oracle on identical Sobol
+sample sequences.
+
+Bar: per-sample Li (RGB), alpha, sample position and path
+depth bit-identical to the oracle run with correctly-rounded transcendentals
+(libm_mode=1, the device's libm); the film bit-identical except pixels that
+received spill splats (|u| within 1e-5 of a pixel edge), which match to 1e-6
+relative (float atomics change the summation order).
+"""
+import numpy as np
+import pytest
+
+from mitsuba_amd import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def _compare(film_g, smp_g, film_o, smp_o):
+    assert smp_g.shape == smp_o.shape
+    same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
+    bad = np.nonzero(~same)[0]
+    assert same.all(), 'per-sample mismatch at %d records, first: %s vs %s' % (
+        bad.size, smp_g[bad[:3]].tolist(), smp_o[bad[:3]].tolist())
+    np.testing.assert_allclose(film_g, film_o, rtol=1e-6, atol=1e-7)
+    frac = np.mean(_bits(film_g) == _bits(film_o))
+    assert frac > 0.999, frac
+
+
+def test_cornell_small_bitexact(gpu_ctx, oracle):
+    sc, it = scenes.build('C1', width=64, height=48, spp=8)
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['samples'] == st_o['samples'] == 64 * 48 * 8
+    assert st_g['rays'] == st_o['rays']
+    assert st_g['shadow_rays'] == st_o['shadow_rays']
+    assert st_g['path_length_sum'] == st_o['path_length_sum']
+
+
+def test_cornell_window_and_gaussian(gpu_ctx, oracle):
+    sc, it = scenes.build('C1', width=96, height=80, spp=4)
+    it.rfilter = 'gaussian'
+    gpu_ctx.upload(sc)
+    win = (17, 9, 40, 33)
+    film_g, smp_g, _ = gpu_ctx.render(it, window=win, samples=True)
+    film_o, smp_o, _ = oracle.render(sc, it, window=win, samples=True, libm_mode=1)
+    assert np.all(_bits(smp_g) == _bits(smp_o))
+    np.testing.assert_allclose(film_g, film_o, rtol=2e-6, atol=1e-6)
+
+
+def test_row_interleave_sums_to_full(gpu_ctx):
+    sc, it = scenes.build('C1', width=64, height=64, spp=4)
+    gpu_ctx.upload(sc)
+    full, _, _ = gpu_ctx.render(it)
+    parts = [gpu_ctx.render(it, row=(8, 4, k))[0] for k in range(4)]
+    acc = np.zeros_like(full)
+    for p in parts:
+        acc += p
+    np.testing.assert_allclose(acc, full, rtol=1e-6, atol=1e-7)
