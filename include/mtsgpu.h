@@ -161,6 +161,9 @@ typedef struct {
     uint64_t path_length_sum;       /* sum of rRec.depth at exit (path.cpp:290)    */
     uint64_t node_visits;           /* BVH nodes visited (stats builds)            */
     uint64_t tri_tests;             /* TriAccel tests (stats builds)               */
+    uint64_t hits;                  /* intersection records filled (stats builds)  */
+    uint64_t nee_samples;           /* emitter samples drawn (stats builds)        */
+    uint64_t sobol_reads;           /* direction-number words read, approx. (stats) */
     double kernel_ms;               /* device time of the render launches          */
 } mtsgpu_stats;
 

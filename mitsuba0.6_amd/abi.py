@@ -73,7 +73,8 @@ FLAG_TRAVERSAL_STATS = 1
 class Stats(C.Structure):
     _fields_ = [('samples', C.c_uint64), ('rays', C.c_uint64), ('shadow_rays', C.c_uint64),
                 ('path_length_sum', C.c_uint64), ('node_visits', C.c_uint64),
-                ('tri_tests', C.c_uint64), ('kernel_ms', C.c_double)]
+                ('tri_tests', C.c_uint64), ('hits', C.c_uint64), ('nee_samples', C.c_uint64),
+                ('sobol_reads', C.c_uint64), ('kernel_ms', C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

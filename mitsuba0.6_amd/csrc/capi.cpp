@@ -246,7 +246,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
     unsigned long long *cnt = (unsigned long long *)ctx->counters.p;
     L.counters = cnt;
-    L.task_counter = (uint32_t *)(cnt + 8);
+    L.task_counter = (uint32_t *)(cnt + 15);
 
     int bpc = 0;
     mtsg_path_kernel_occupancy(&bpc);
@@ -276,6 +276,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         stats->path_length_sum = hc[3];
         stats->node_visits = stats_mode ? hc[4] : 0;
         stats->tri_tests = stats_mode ? hc[5] : 0;
+        stats->hits = stats_mode ? hc[7] : 0;
+        stats->nee_samples = stats_mode ? hc[9] : 0;
+        stats->sobol_reads = stats_mode ? hc[10] : 0;
         stats->kernel_ms = ms;
     }
     if (hc[6]) return fail(ctx, MTSGPU_EDIM, "Lookup dimension exceeds the direction number table size! You may have to "

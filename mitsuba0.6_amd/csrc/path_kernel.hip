@@ -392,6 +392,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
     const uint32_t lane = threadIdx.x & 63;
 
     unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
+    unsigned long long cHits = 0, cNee = 0, cSobol = 0;
 
     int state = ST_NEWSAMPLE;
     bool haveTask = false;
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
         if (state == ST_PRIMARY) {
             // rRec.rayIntersect (records.inl:117-144)
             if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+            if (STATS && hit) cHits++;
             P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
             P.rayD = rd;
             vertex = true;
@@ -505,6 +507,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
         } else if (state == ST_EXT) {
             // after scene->rayIntersect(ray, its) (path.cpp:226-286)
             if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+            if (STATS && hit) cHits++;
             if (!P.its.valid) {
                 endPath = true;   // no environment emitter: break before the throughput update
             } else {
@@ -569,6 +572,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
                         next2d(L, smp, px, py, ex, ey);
                         float emPdf;
                         const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
+                        if (STATS) cNee++;
                         const MtsgEmitter &e = S.emitters[ei];
                         // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
                         float py2 = ey;
@@ -672,6 +676,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
             }
             cLen += (unsigned long long)P.depth;
             cSamples++;
+            if (STATS) cSobol += (unsigned long long)__popcll(smp.sobolIndex) * smp.dim;
             if (smp.err) cErr++;
             ++j;
             state = ST_NEWSAMPLE;
@@ -691,6 +696,9 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
     if (STATS) {
         atomicAdd(L.counters + 4, cNodes);
         atomicAdd(L.counters + 5, cTests);
+        atomicAdd(L.counters + 7, cHits);
+        atomicAdd(L.counters + 9, cNee);
+        atomicAdd(L.counters + 10, cSobol);
     }
     if (cErr) atomicAdd(L.counters + 6, cErr);
 }

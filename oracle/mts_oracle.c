@@ -1792,9 +1792,20 @@ static int film_put(const Filter *f, int W, int H, int px, int py, float sx, flo
             const float weight = wx[xr] * wy[yr];
             int gx = x + bx, gy = y + by; /* film coordinates (border included) */
             if (gx >= fw || gy >= fh) continue; /* Bitmap::accumulate clips to the film */
-            float *dst = (gx == px + b && gy == py + b) ? own : spill;
-            dst += ((size_t)gy * fw + gx) * 5;
-            for (int k = 0; k < 5; ++k) dst[k] += weight * val5[k];
+            const int isOwn = gx == px + b && gy == py + b;
+            float *dst = (isOwn ? own : spill) + ((size_t)gy * fw + gx) * 5;
+            if (isOwn) {
+                for (int k = 0; k < 5; ++k) dst[k] += weight * val5[k];
+            } else {
+                /* pixels of other tasks: shared between OpenMP threads */
+                for (int k = 0; k < 5; ++k) {
+                    const float add = weight * val5[k];
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+                    dst[k] += add;
+                }
+            }
         }
     }
     return 1;
@@ -1849,13 +1860,6 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
             if (smp.err) err = 1;
             pathLen += (uint64_t)depth; nsamples++;
             float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};
-#ifdef _OPENMP
-            if (threads != 1) {
-                /* spill pixels are shared between threads */
-#pragma omp critical(oracle_film)
-                film_put(&F, W, H, px, py, sx, sy, val5, film, spill, fw, fh);
-            } else
-#endif
             film_put(&F, W, H, px, py, sx, sy, val5, film, spill, fw, fh);
             if (samples) {
                 float *rec = samples + ((size_t)pi * P->spp + j) * MTSGPU_SAMPLE_RECORD_FLOATS;
