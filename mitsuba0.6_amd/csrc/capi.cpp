@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,9 +21,10 @@
 #include "scene_build.h"
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
+hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
-int mtsg_path_kernel_occupancy(int *blocksPerCU);
+int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
 
 namespace {
 
@@ -57,7 +59,7 @@ struct mtsgpu_ctx {
     HostScene host;
     MtsgDeviceScene dscene;
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
-    DevBuf film_own, film_spill, samples, counters;
+    DevBuf film_own, film_spill, samples, counters, contrib;
 };
 
 namespace {
@@ -70,6 +72,24 @@ int fail(mtsgpu_ctx *ctx, int code, const std::string &msg) {
 int hip_fail(mtsgpu_ctx *ctx, hipError_t e, const char *what) {
     return fail(ctx, e == hipErrorOutOfMemory ? MTSGPU_ENOMEM : MTSGPU_EHIP,
                 std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Sobol direction numbers as 4-bit XOR tables: [dim][c][v] = XOR of columns
+// 4c..4c+3 of the dimension selected by the bits of v (sobolseq.h:43-57)
+const std::vector<uint32_t> &sobol_nibble_tables() {
+    static std::vector<uint32_t> T;
+    if (!T.empty()) return T;
+    const std::vector<uint32_t> &M = mtsg_sobol_matrices();
+    T.assign((size_t)MTSG_SOBOL_DIMS * MTSG_NIBBLES * 16, 0u);
+    for (int d = 0; d < MTSG_SOBOL_DIMS; ++d)
+        for (int c = 0; c < MTSG_NIBBLES; ++c)
+            for (int v = 0; v < 16; ++v) {
+                uint32_t r = 0;
+                for (int b = 0; b < 4; ++b)
+                    if ((v >> b) & 1) r ^= M[(size_t)d * MTSG_SOBOL_SIZE + 4 * c + b];
+                T[((size_t)d * MTSG_NIBBLES + c) * 16 + v] = r;
+            }
+    return T;
 }
 
 template <class T>
@@ -137,7 +157,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         (e = upload(ctx->positions, H.positions, s)) != hipSuccess || (e = upload(ctx->normals, H.normals, s)) != hipSuccess ||
         (e = upload(ctx->shapes, H.shapes, s)) != hipSuccess || (e = upload(ctx->bsdfs, H.bsdfs, s)) != hipSuccess ||
         (e = upload(ctx->emitters, H.emitters, s)) != hipSuccess || (e = upload(ctx->area_cdf, H.area_cdf, s)) != hipSuccess ||
-        (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, mtsg_sobol_matrices(), s)) != hipSuccess)
+        (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, sobol_nibble_tables(), s)) != hipSuccess)
         return hip_fail(ctx, e, "scene upload");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "scene upload sync");
     MtsgDeviceScene &D = ctx->dscene;
@@ -153,7 +173,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     D.emitters = (const MtsgEmitter *)ctx->emitters.p;
     D.area_cdf = (const float *)ctx->area_cdf.p;
     D.em_cdf = (const float *)ctx->em_cdf.p;
-    D.sobol = (const uint32_t *)ctx->sobol.p;
+    D.sobol = nullptr;
     D.num_emitters = (uint32_t)H.emitters.size();
     D.num_prims = (uint32_t)H.tris.size();
     D.em_norm = H.em_norm;
@@ -217,19 +237,32 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.row_block = P->row_block ? P->row_block : 1;
     L.row_stride = P->row_stride ? P->row_stride : 1;
     L.row_phase = P->row_phase % L.row_stride;
-    // active rows of the window under the interleave
-    uint32_t active = 0;
-    for (uint32_t y = 0; y < P->height; ++y)
-        if ((y / L.row_block) % L.row_stride == L.row_phase) ++active;
-    // tasks enumerate rows compacted over the interleave; map r -> y in the kernel
+    // work decomposition: compact rows (interleave) x columns in 8x8 tiles
     const uint32_t rowsCompact = ((P->height + L.row_block - 1) / L.row_block + L.row_stride - 1) / L.row_stride * L.row_block;
-    const uint32_t tilesX = (P->width + 7) / 8, tilesY = (rowsCompact + 7) / 8;
-    L.num_tasks = tilesX * tilesY * 64;
-    (void)active;
-
+    L.tiles_x = (P->width + 7) / 8;
+    const uint32_t tilesY = (rowsCompact + 7) / 8;
+    L.num_pixels = L.tiles_x * tilesY * 64;
+    // Sobol index width: frame << 2m | 2m bits (sobolseq.h:93-125); 52 columns per dimension
+    uint32_t sppBits = 0;
+    while ((1ull << sppBits) < (uint64_t)P->spp) ++sppBits;
+    const uint32_t indexBits = (m > 1 ? 2 * m : 0) + sppBits;
+    if (indexBits > 52) return fail(ctx, MTSGPU_EINVAL, "sample index exceeds the 52-bit Sobol direction numbers");
+    L.nibbles = indexBits <= 32 ? 8 : MTSG_NIBBLES;
+    L.lds_dims = 32;
+    L.sobol_nib = (const uint32_t *)ctx->sobol.p;
+    L.stack_depth = H.bvh_depth + 2;
+    L.num_nodes = (uint32_t)H.nodes.size();
+    // small scenes: stage the whole BVH + TriAccel array in LDS (<= 32 KiB)
+    const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri);
+    L.scene_lds = (sceneBytes <= (32u << 10) && !std::getenv("MTSGPU_NO_SCENE_LDS")) ? 1u : 0u;
+    // own-pixel splat buffer [5][chunk][pixels]; spp processed in chunks that fit the budget
+    size_t budget = (size_t)8 << 30;
+    if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);
+    const size_t perSample = (size_t)L.num_pixels * 5 * 4;
+    const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));
     const size_t filmFloats = (size_t)L.fw * L.fh * 5;
     if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||
-        (e = ctx->counters.ensure(16 * 8)) != hipSuccess)
+        (e = ctx->counters.ensure(16 * 8)) != hipSuccess || (e = ctx->contrib.ensure(perSample * chunk)) != hipSuccess)
         return hip_fail(ctx, e, "film allocation");
     float *own = film_dev ? film_dev : (float *)ctx->film_own.p;
     const size_t nsamp = samples_host ? (size_t)P->width * P->height * P->spp * MTSGPU_SAMPLE_RECORD_FLOATS : 0;
@@ -244,20 +277,25 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.film_own = own;
     L.film_spill = (float *)ctx->film_spill.p;
     L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
+    L.contrib = (float *)ctx->contrib.p;
     unsigned long long *cnt = (unsigned long long *)ctx->counters.p;
     L.counters = cnt;
-    L.task_counter = (uint32_t *)(cnt + 15);
 
     int bpc = 0;
-    mtsg_path_kernel_occupancy(&bpc);
+    mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
-    int grid = ctx->num_cus * bpc;
-    const uint64_t lanesNeeded = (uint64_t)L.num_tasks;
-    const int maxGrid = (int)std::max<uint64_t>(1, (lanesNeeded + 255) / 256);
-    grid = std::min(grid, maxGrid);
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
     if ((e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
-    if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
+    for (uint32_t j0 = 0; j0 < P->spp; j0 += chunk) {
+        if (P->cancel && *P->cancel) break;
+        L.j0 = j0;
+        L.chunk_spp = std::min(chunk, P->spp - j0);
+        L.num_items = (uint64_t)L.chunk_spp * L.num_pixels;
+        const uint64_t blocksNeeded = (L.num_items + 255) / 256;
+        const int grid = (int)std::min<uint64_t>((uint64_t)ctx->num_cus * bpc, std::max<uint64_t>(1, blocksNeeded));
+        if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
+        if ((e = mtsg_launch_reduce(L, stream)) != hipSuccess) return hip_fail(ctx, e, "reduce launch");
+    }
     if ((e = hipEventRecord(ctx->ev1, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
     if ((e = mtsg_launch_finalize(own, L.film_spill, filmFloats, stream)) != hipSuccess) return hip_fail(ctx, e, "finalize launch");
     unsigned long long hc[16];
@@ -305,7 +343,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
-                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters};
+                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib};
     for (DevBuf *b : bufs) b->release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

@@ -121,10 +121,25 @@ struct MtsgLaunch {
     int32_t film_w, film_h, fw, fh;   // image size and film size incl. borders
     uint32_t x0, y0, width, height;
     uint32_t row_block, row_stride, row_phase;
-    uint32_t num_tasks;               // pixels in the window after row interleave
-    float *film_own;                  // fw*fh*5: own-pixel sums (written once per pixel)
+    // work decomposition: items = (sample j in [j0, j0 + chunk_spp)) x (compact pixel p in [0, num_pixels))
+    uint32_t tiles_x;                 // 8x8 pixel tiles across the window
+    uint32_t num_pixels;              // compact pixels incl. padding of partial tiles
+    uint32_t j0, chunk_spp;
+    uint64_t num_items;
+    // Sobol direction numbers as 4-bit lookup tables: nib[dim][c][v] = XOR of the
+    // columns 4c..4c+3 selected by v (same product as sobolseq.h:43-57)
+    const uint32_t *sobol_nib;        // MTSG_SOBOL_DIMS * MTSG_NIBBLES * 16 words
+    uint32_t lds_dims;                // dims [0, lds_dims) staged in LDS
+    uint32_t nibbles;                 // 8 (index < 2^32) or MTSG_NIBBLES
+    uint32_t stack_depth;             // LDS traversal stack entries per lane
+    uint32_t num_nodes;               // BVH2 inner nodes
+    uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
+    float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
+    float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)
     float *samples;                   // optional per-sample records
-    uint32_t *task_counter;           // global work queue head
-    unsigned long long *counters;     // [0] samples [1] rays [2] shadow [3] pathlen [4] nodes [5] tests [6] dim errors
+    unsigned long long *counters;     // [0] samples [1] rays [2] shadow [3] pathlen [4] nodes [5] tests
+                                      // [6] dim errors [7] hits [9] nee [10] sobol words
 };
+
+#define MTSG_NIBBLES 13

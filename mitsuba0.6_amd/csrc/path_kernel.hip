@@ -4,36 +4,72 @@
 // (src/integrators/path/path.cpp:119-294), as one persistent HIP kernel.
 //
 // Execution model:
-//  * one lane = one pixel task at a time (all `spp` samples of that pixel, in
-//    sample order, so the pixel's own film sum is accumulated in registers in
-//    exactly the reference's order);
-//  * a lane whose path ends starts the next sample immediately (path
-//    regeneration), and a lane whose pixel is done pulls the next pixel from a
-//    global queue with one wave-aggregated atomic;
+//  * work items are (sample j, pixel p) pairs, j-major, pixels in 8x8 tiles;
+//    lane g of the persistent grid takes items g, g + lanes, g + 2 lanes, ...
+//    (static striding: no queue, no tail of long per-pixel tasks);
+//  * a lane whose path ends starts its next item immediately (regeneration);
 //  * each loop iteration traces exactly one ray per active lane (primary,
-//    shadow or extension) through a shared BVH2 traversal, then advances that
+//    shadow or extension) through one shared BVH2 traversal, then advances that
 //    lane's path state machine to its next ray;
-//  * traversal stacks live in LDS, lane-strided (conflict-free).
+//  * the own-pixel splat of every sample is stored to HBM ([5][spp][pixels])
+//    and a second kernel sums each pixel in sample order -- the reference's
+//    ImageBlock accumulation order, bit for bit; splats into other pixels (box
+//    filter edges, gaussian) go to a spill film with float atomics;
+//  * LDS holds the Sobol direction numbers of the first dimensions as 4-bit
+//    lookup tables (8 independent reads per 32-bit sample instead of up to 32
+//    dependent ones) and the lane-strided traversal stacks.
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "dbsdf.h"
 #include "layout.h"
 
 #define BLOCK 256
-#define STACK 32
 
 // ---------------------------------------------------------------------------
 // Sobol sampler (samplers/sobol.cpp:147-258, sobolseq.h:43-130)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float sobol_sample(const uint32_t *__restrict__ M, uint64_t index, uint32_t dim,
-                                             uint32_t scramble) {
-    uint32_t result = scramble;
-    const uint32_t *row = M + dim * MTSG_SOBOL_SIZE;
-    while (index) {                      // XOR over the set bits of index (order-free)
-        uint32_t b = (uint32_t)__builtin_ctzll(index);
-        result ^= row[b];
-        index &= index - 1;
+// sobol::sampleSingle (sobolseq.h:43-57): XOR of the direction-number columns
+// selected by the bits of `index`, evaluated 4 bits at a time through
+// precomputed XOR tables (exactly the same XOR, so the same result)
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;     // LDS
+typedef __attribute__((address_space(1))) const uint32_t glb_u32;     // global
+typedef __attribute__((address_space(3))) const MtsgNode lds_node;
+typedef __attribute__((address_space(1))) const MtsgNode glb_node;
+typedef __attribute__((address_space(3))) const MtsgTri lds_tri;
+typedef __attribute__((address_space(1))) const MtsgTri glb_tri;
+typedef float vf4 __attribute__((ext_vector_type(4)));
+typedef int vi4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const vf4 lds_f4;
+typedef __attribute__((address_space(1))) const vf4 glb_f4;
+typedef __attribute__((address_space(3))) const vi4 lds_i4;
+typedef __attribute__((address_space(1))) const vi4 glb_i4;
+
+template <int NIB, typename T>
+__device__ __forceinline__ uint32_t sobol_bits(T *tab, uint64_t index) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < NIB; ++c) r ^= tab[c * 16 + (uint32_t)((index >> (4 * c)) & 15u)];
+    return r;
+}
+
+struct SobolCtx {
+    lds_u32 *lds;             // [lds_dims][nibbles][16]
+    glb_u32 *glob;            // [1024][MTSG_NIBBLES][16]
+    uint32_t lds_dims, nibbles, scramble;
+};
+
+__device__ __forceinline__ float sobol_sample(const SobolCtx &C, uint64_t index, uint32_t dim) {
+    uint32_t bits;
+    if (dim < C.lds_dims) {
+        lds_u32 *t = C.lds + dim * C.nibbles * 16;
+        bits = (C.nibbles == 8) ? sobol_bits<8>(t, index) : sobol_bits<MTSG_NIBBLES>(t, index);
+    } else {
+        glb_u32 *t = C.glob + (size_t)dim * MTSG_NIBBLES * 16;
+        bits = (C.nibbles == 8) ? sobol_bits<8>(t, index) : sobol_bits<MTSG_NIBBLES>(t, index);
     }
+    const uint32_t result = C.scramble ^ bits;
     float v = (float)result * (1.0f / 4294967296.0f);
     return smin(v, D_ONE_MINUS_EPS);
 }
@@ -82,10 +118,12 @@ struct Hit {
 // ---------------------------------------------------------------------------
 // BVH2 traversal
 // ---------------------------------------------------------------------------
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool traverse(const MtsgDeviceScene &S, f3 o, f3 d, float mint, float maxt,
+template <bool ANY, bool STATS, typename NodeT, typename TriT>
+__device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          int *__restrict__ stk, uint32_t &bestSlot, float &bu, float &bv,
                                          float &bt, unsigned long long &nodes, unsigned long long &tests) {
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     // reciprocal direction for the (conservative) node tests; exact zeros use
     // +-1e30 so that 0 * inf never produces NaN (TriAccel uses the exact ray)
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
@@ -101,11 +139,11 @@ __device__ __forceinline__ bool traverse(const MtsgDeviceScene &S, f3 o, f3 d, f
     while (true) {
         if (node >= 0) {
             if (STATS) nodes++;
-            const MtsgNode *n = S.nodes + node;
-            const float4 a = *reinterpret_cast<const float4 *>(&n->c0lox);
-            const float4 b = *reinterpret_cast<const float4 *>(&n->c1lox);
-            const float4 c = *reinterpret_cast<const float4 *>(&n->c0loz);
-            const int4 e = *reinterpret_cast<const int4 *>(&n->c0);
+            NodeT *n = nodesArr + node;
+            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
+            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
+            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
+            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
             // child 0
             float t0x = (a.x - o.x) * ix, t1x = (a.y - o.x) * ix;
             float t0y = (a.z - o.y) * iy, t1y = (a.w - o.y) * iy;
@@ -138,10 +176,10 @@ __device__ __forceinline__ bool traverse(const MtsgDeviceScene &S, f3 o, f3 d, f
             const uint32_t first = ref >> 4, count = ref & 15u;
             for (uint32_t i = first; i < first + count; ++i) {
                 if (STATS) tests++;
-                const MtsgTri *tr = S.tris + i;
-                const float4 q0 = *reinterpret_cast<const float4 *>(&tr->k);
-                const float4 q1 = *reinterpret_cast<const float4 *>(&tr->a_u);
-                const float4 q2 = *reinterpret_cast<const float4 *>(&tr->c_nu);
+                TriT *tr = trisArr + i;
+                const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
+                const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
+                const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
                 const uint32_t k = __float_as_uint(q0.x);
                 // TriAccel::rayIntersect (triaccel.h:92-160)
                 float o_u, o_v, o_k, d_u, d_v, d_k;
@@ -325,31 +363,28 @@ struct PathVars {
     int depth;
     bool scattered, emitted;
     float alpha;
-    // vertex
-    Hit its;
-    f3 rayD;          // direction of the ray that produced `its`
-    // pending NEE / BSDF sample
-    f3 neeC;          // throughput*value*bsdfVal*weight, committed if unoccluded
+    Hit its;          // current vertex
+    f3 neeC;          // throughput*value*bsdfVal*weight, committed if the shadow ray is unoccluded
     f3 refN;          // DirectSamplingRecord::refN of the current vertex
     f3 bsdfWeight;
     float bsdfPdf, bsdfEta;
     int sampledType;
 };
 
-__device__ __forceinline__ float next1d(const MtsgLaunch &L, SamplerState &s) {
-    if (s.dim >= MTSG_SOBOL_DIMS) { s.err = true; return 0.0f; }        // sobol.cpp:219-229
-    return sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
+__device__ __forceinline__ float next1d(const SobolCtx &C, SamplerState &s) {   // sobol.cpp:219-229
+    if (s.dim >= MTSG_SOBOL_DIMS) { s.err = true; return 0.0f; }
+    return sobol_sample(C, s.sobolIndex, s.dim++);
 }
-__device__ __forceinline__ void next2d(const MtsgLaunch &L, SamplerState &s, int px, int py, float &u,
-                                       float &v) {                                 // sobol.cpp:231-250
-    if (s.dim + 1 >= 5 && s.dim < 5) s.dim = 5;
+__device__ __forceinline__ void next2d(const SobolCtx &C, float resolution, SamplerState &s, int px, int py,
+                                       float &u, float &v) {                       // sobol.cpp:231-250
+    if (s.dim + 1 >= 5 && s.dim < 5) s.dim = 5;   // skip the (empty) array dimensions [5,5)
     if (s.dim + 1 >= MTSG_SOBOL_DIMS) { s.err = true; u = v = 0.0f; return; }
     if (s.dim == 0 && s.sobolIndex != (uint64_t)s.sampleIndex) {
-        u = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble) * L.resolution - (float)px;
-        v = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble) * L.resolution - (float)py;
+        u = sobol_sample(C, s.sobolIndex, s.dim++) * resolution - (float)px;
+        v = sobol_sample(C, s.sobolIndex, s.dim++) * resolution - (float)py;
     } else {
-        u = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
-        v = sobol_sample(L.scene.sobol, s.sobolIndex, s.dim++, L.scramble);
+        u = sobol_sample(C, s.sobolIndex, s.dim++);
+        v = sobol_sample(C, s.sobolIndex, s.dim++);
     }
 }
 
@@ -368,88 +403,87 @@ __device__ __forceinline__ f3 area_Le(const MtsgDeviceScene &S, const Hit &h, f3
     return ld3(e.radiance);
 }
 
-// decode task -> pixel (tile-major 8x8 over the window's active rows)
-__device__ __forceinline__ bool task_pixel(const MtsgLaunch &L, uint32_t task, int &px, int &py) {
-    const uint32_t tilesX = (L.width + 7) / 8;
-    const uint32_t tile = task >> 6, in = task & 63;
-    const uint32_t lx = (tile % tilesX) * 8 + (in & 7);
-    const uint32_t r = (tile / tilesX) * 8 + (in >> 3);
+// compact pixel index (8x8 tiles over the window's active rows) -> image pixel
+__device__ __forceinline__ bool pixel_of(const MtsgLaunch &L, uint32_t p, int &px, int &py) {
+    const uint32_t tile = p >> 6, in = p & 63;
+    const uint32_t lx = (tile % L.tiles_x) * 8 + (in & 7);
+    const uint32_t r = (tile / L.tiles_x) * 8 + (in >> 3);
     if (lx >= L.width) return false;
-    const uint32_t rb = L.row_block, rs = L.row_stride;
-    const uint32_t blk = r / rb, off = r % rb;
-    const uint32_t ly = (blk * rs + L.row_phase) * rb + off;
+    const uint32_t blk = r / L.row_block, off = r % L.row_block;
+    const uint32_t ly = (blk * L.row_stride + L.row_phase) * L.row_block + off;
     if (ly >= L.height) return false;
     px = (int)(L.x0 + lx);
     py = (int)(L.y0 + ly);
     return true;
 }
 
-template <bool SAMPLES, bool STATS>
-__global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
-    __shared__ int stack_mem[STACK * BLOCK];
-    int *stk = stack_mem + threadIdx.x;
+#ifndef MTSG_WAVES_PER_EU
+#define MTSG_WAVES_PER_EU 3
+#endif
+
+template <bool SAMPLES, bool STATS, bool SCENE_LDS>
+__global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaunch L) {
+    extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
-    const uint32_t lane = threadIdx.x & 63;
+    // LDS: [Sobol nibble tables][BVH nodes + TriAccel (small scenes)][traversal stacks]
+    const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
+    for (uint32_t i = threadIdx.x; i < tabWords; i += BLOCK) {
+        const uint32_t d = i / (L.nibbles * 16), r = i % (L.nibbles * 16);
+        lds[i] = L.sobol_nib[(size_t)d * MTSG_NIBBLES * 16 + r];
+    }
+    uint32_t sceneWords = 0;
+    if (SCENE_LDS) {
+        const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
+        const uint32_t *gn = reinterpret_cast<const uint32_t *>(S.nodes);
+        const uint32_t *gt = reinterpret_cast<const uint32_t *>(S.tris);
+        for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[tabWords + i] = gn[i];
+        for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[tabWords + nodeWords + i] = gt[i];
+        sceneWords = nodeWords + triWords;
+    }
+    __syncthreads();
+    lds_node *ldsNodes = (lds_node *)(lds + tabWords);
+    lds_tri *ldsTris = (lds_tri *)(lds + tabWords + L.num_nodes * 16);
+    SobolCtx SC;
+    SC.lds = (lds_u32 *)lds;
+    SC.glob = (glb_u32 *)L.sobol_nib;
+    SC.lds_dims = L.lds_dims;
+    SC.nibbles = L.nibbles;
+    SC.scramble = L.scramble;
+    int *stk = reinterpret_cast<int *>(lds + tabWords + sceneWords) + threadIdx.x;
 
     unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
     unsigned long long cHits = 0, cNee = 0, cSobol = 0;
 
+    const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
+    uint64_t item = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
     int state = ST_NEWSAMPLE;
-    bool haveTask = false;
     int px = 0, py = 0;
-    uint32_t j = 0;
-    float own[5] = {0, 0, 0, 0, 0};
+    uint32_t j = 0, pix = 0;
     SamplerState smp;
     smp.sobolIndex = 0; smp.sampleIndex = 0; smp.dim = 0; smp.err = false;
     PathVars P;
     float sx = 0, sy = 0;
-    // current ray
-    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);
+    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);    // the ray traced in this iteration
     float rmint = 0, rmaxt = 0;
-    uint32_t sampleSlot = 0;
 
     while (true) {
-        // ---- A: start samples / fetch tasks --------------------------------
-        if (state == ST_NEWSAMPLE) {
-            if (haveTask && j >= L.spp) {
-                float *dst = L.film_own + ((size_t)(py + L.filter.border) * L.fw + (px + L.filter.border)) * 5;
-#pragma unroll
-                for (int k = 0; k < 5; ++k) dst[k] = own[k];
-                haveTask = false;
-            }
-        }
-        // wave-aggregated task fetch
-        while (true) {
-            const bool need = (state == ST_NEWSAMPLE) && !haveTask;
-            const unsigned long long mask = __ballot(need);
-            if (mask == 0) break;
-            uint32_t base = 0;
-            const int leader = __ffsll((long long)mask) - 1;
-            if ((int)lane == leader) base = atomicAdd(L.task_counter, (uint32_t)__popcll(mask));
-            base = __shfl(base, leader);
-            if (need) {
-                const uint32_t rank = (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-                const uint32_t task = base + rank;
-                if (task >= L.num_tasks) {
-                    state = ST_DONE;
-                } else if (task_pixel(L, task, px, py)) {
-                    haveTask = true;
-                    j = 0;
-                    sampleSlot = 0;
-#pragma unroll
-                    for (int k = 0; k < 5; ++k) own[k] = 0.0f;
-                }
-            }
-        }
-        if (state == ST_NEWSAMPLE) {
-            // SamplingIntegrator::renderBlock inner loop body (integrator.cpp:165-186)
+        // ---- A: start the next sample (renderBlock loop body, integrator.cpp:165-186)
+        while (state == ST_NEWSAMPLE) {
+            if (item >= L.num_items) { state = ST_DONE; break; }
+            const uint64_t it = item;
+            item += lanes;
+            const uint32_t jj = (uint32_t)(it / L.num_pixels);
+            pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
+            if (!pixel_of(L, pix, px, py)) continue;
+            j = L.j0 + jj;
+            // sampler->generate(offset) + setSampleIndex(j) (sobol.cpp:187-217)
             smp.dim = 0;
             smp.sampleIndex = j;
             smp.err = false;
             if (L.lut.m > 1) smp.sobolIndex = sobol_lookup(L.lut, j, (uint32_t)px, (uint32_t)py, L.scramble64);
             else smp.sobolIndex = j;
             float u, v;
-            next2d(L, smp, px, py, u, v);
+            next2d(SC, L.resolution, smp, px, py, u, v);
             sx = (float)px + u;
             sy = (float)py + v;
             // PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298)
@@ -479,31 +513,43 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
         bool hit = false;
         uint32_t slot = 0;
         float hu = 0, hv = 0, ht = 0;
-        if (state == ST_PRIMARY || state == ST_EXT || state == ST_SHADOW) {
+        if (state != ST_DONE) {
             const bool shadow = state == ST_SHADOW;
             if (shadow) cShadow++; else cRays++;
             float mint, maxt;
-            if (ray_interval(S, ro, rd, rmint, rmaxt, shadow, mint, maxt)) {
-                if (shadow)
-                    hit = traverse<true, STATS>(S, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
-                else
-                    hit = traverse<false, STATS>(S, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+            // a shadow ray whose estimate is zero cannot change Li: skip its traversal
+            const bool needed = !shadow || !is_zero(P.neeC);
+            if (needed && ray_interval(S, ro, rd, rmint, rmaxt, shadow, mint, maxt)) {
+                if (SCENE_LDS) {
+                    if (shadow)
+                        hit = traverse<true, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    else
+                        hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                } else {
+                    glb_node *gn = (glb_node *)S.nodes;
+                    glb_tri *gt = (glb_tri *)S.tris;
+                    if (shadow)
+                        hit = traverse<true, STATS>(gn, gt, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    else
+                        hit = traverse<false, STATS>(gn, gt, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                }
             }
         }
 
         // ---- C: advance the path state machine ------------------------------
-        bool vertex = false;      // run the top-of-loop body of Li() for P.its
+        bool vertex = false;      // run the loop head of Li() for P.its
         bool endPath = false;
+        bool doBsdf = false;      // sample the BSDF at P.its
         if (state == ST_PRIMARY) {
             // rRec.rayIntersect (records.inl:117-144)
             if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
             if (STATS && hit) cHits++;
             P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
-            P.rayD = rd;
             vertex = true;
         } else if (state == ST_SHADOW) {
+            // Scene::sampleEmitterDirect's visibility test (scene.cpp:838-842)
             if (!hit) P.L = add(P.L, P.neeC);
-            state = ST_EXT;   // continue with the BSDF sample below
+            doBsdf = true;
         } else if (state == ST_EXT) {
             // after scene->rayIntersect(ray, its) (path.cpp:226-286)
             if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
@@ -511,46 +557,39 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
             if (!P.its.valid) {
                 endPath = true;   // no environment emitter: break before the throughput update
             } else {
-                bool hitEmitter = false;
-                f3 value = mk(0, 0, 0);
                 const MtsgShape &sh = S.shapes[P.its.shape];
-                f3 dn = mk(0, 0, 0);
-                int em = -1;
-                if (sh.emitter >= 0) {
-                    value = area_Le(S, P.its, neg(rd));
-                    dn = P.its.sh.n;
-                    em = sh.emitter;
-                    hitEmitter = true;
-                }
                 P.thr = mulv(P.thr, P.bsdfWeight);
                 P.eta *= P.bsdfEta;
-                if (hitEmitter) {
+                if (sh.emitter >= 0) {
+                    const f3 value = area_Le(S, P.its, neg(rd));
                     float lumPdf = 0;
                     if (!(P.sampledType & MTSG_F_DELTA)) {
-                        // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126
-                        const MtsgEmitter &e = S.emitters[em];
+                        // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
+                        // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
+                        const MtsgEmitter &e = S.emitters[sh.emitter];
+                        const f3 dn = P.its.sh.n;
                         float pdf = 0.0f;
                         if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0)
                             pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
                         lumPdf = pdf * (e.weight * S.em_norm);
                     }
-                    float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                    const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
                     P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
                 }
                 P.emitted = false;
                 if (P.depth++ >= L.rr_depth) {
                     const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
-                    if (next1d(L, smp) >= q) endPath = true;
+                    if (next1d(SC, smp) >= q) endPath = true;
                     else P.thr = divs(P.thr, q);
                 }
                 if (smp.err) endPath = true;
-                if (!endPath) { P.rayD = rd; vertex = true; }
+                if (!endPath) vertex = true;
             }
         }
 
-        bool needBsdf = false;
         if (vertex) {
-            // loop head of Li() (path.cpp:135-200)
+            // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
+            const f3 inDir = rd;
             if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
                 endPath = true;
             } else if (!P.its.valid) {
@@ -559,17 +598,17 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
                 const MtsgShape &sh = S.shapes[P.its.shape];
                 const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
                 if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
-                    P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(P.rayD))));
+                    P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(inDir))));
                 if ((P.depth >= L.max_depth && L.max_depth > 0) ||
-                    (L.strict_normals && dot(P.rayD, P.its.geoN) * P.its.wi.z >= 0)) {
+                    (L.strict_normals && dot(inDir, P.its.geoN) * P.its.wi.z >= 0)) {
                     endPath = true;
                 } else {
                     P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
-                    needBsdf = true;
+                    doBsdf = true;
                     if (bsdf.flags & MTSG_F_SMOOTH) {
                         // Scene::sampleEmitterDirect (scene.cpp:828-852)
                         float ex, ey;
-                        next2d(L, smp, px, py, ex, ey);
+                        next2d(SC, L.resolution, smp, px, py, ex, ey);
                         float emPdf;
                         const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
                         if (STATS) cNee++;
@@ -606,8 +645,7 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
                         if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
                         else pdf = 0.0f;
                         if (pdf != 0) {
-                            // the shadow ray's verdict is applied after the trace; everything
-                            // else of the NEE estimate is visibility-independent (path.cpp:176-199)
+                            // everything of the NEE estimate but the visibility (path.cpp:176-199)
                             const float dpdf = pdf * emPdf;
                             value = divs(value, emPdf);
                             f3 c = mk(0, 0, 0);
@@ -622,27 +660,27 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
                                 }
                             }
                             P.neeC = c;
+                            // Ray(dRec.ref, dRec.d, Epsilon, dRec.dist*(1-ShadowEpsilon)) (scene.cpp:839-840)
                             ro = P.its.p;
                             rd = dd;
                             rmint = D_EPSILON;
                             rmaxt = dist * (1 - D_SHADOW_EPSILON);
                             state = ST_SHADOW;
-                            needBsdf = false;   // BSDF sampling resumes after the shadow trace
+                            doBsdf = false;   // BSDF sampling resumes after the shadow trace
                         }
                     }
                 }
             }
         }
-        // BSDF sampling (path.cpp:206-226): after a shadow ray, or at a vertex
-        // that issued none
-        const bool doBsdf = !endPath && ((state == ST_EXT && !vertex) || (vertex && needBsdf));
-        if (doBsdf) {
+
+        if (doBsdf && !endPath) {
+            // BSDF sampling (path.cpp:206-226)
             state = ST_EXT;
             const MtsgBsdf &bsdf = S.bsdfs[S.shapes[P.its.shape].bsdf];
             float bx, by;
-            next2d(L, smp, px, py, bx, by);
+            next2d(SC, L.resolution, smp, px, py, bx, by);
             float u1d = 0.0f;
-            if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(L, smp);   // roughdielectric.cpp:554
+            if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
             const BSample bs = bsdf_sample(bsdf, P.its.wi, bx, by, u1d);
             if (is_zero(bs.weight) || smp.err) {
                 endPath = true;
@@ -665,9 +703,14 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
         }
 
         if (endPath) {
-            // block->put(samplePos, spec, alpha); sampler->advance() (integrator.cpp:184-186)
+            // block->put(samplePos, spec, alpha) (integrator.cpp:184): own-pixel splat -> contrib
             const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
+            float own[5] = {0, 0, 0, 0, 0};
             film_splat(L, px, py, sx, sy, val, own);
+            const size_t plane = (size_t)L.chunk_spp * L.num_pixels;
+            float *c = L.contrib + (size_t)(j - L.j0) * L.num_pixels + pix;
+#pragma unroll
+            for (int k = 0; k < 5; ++k) c[k * plane] = own[k];
             if (SAMPLES) {
                 const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
                 float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
@@ -676,19 +719,11 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
             }
             cLen += (unsigned long long)P.depth;
             cSamples++;
-            if (STATS) cSobol += (unsigned long long)__popcll(smp.sobolIndex) * smp.dim;
+            if (STATS) cSobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
             if (smp.err) cErr++;
-            ++j;
             state = ST_NEWSAMPLE;
         }
     }
-    // flush a task finished in the last iteration
-    if (haveTask && j >= L.spp) {
-        float *dst = L.film_own + ((size_t)(py + L.filter.border) * L.fw + (px + L.filter.border)) * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) dst[k] = own[k];
-    }
-    (void)sampleSlot;
     atomicAdd(L.counters + 0, cSamples);
     atomicAdd(L.counters + 1, cRays);
     atomicAdd(L.counters + 2, cShadow);
@@ -701,6 +736,27 @@ __global__ __launch_bounds__(BLOCK) void path_kernel(MtsgLaunch L) {
         atomicAdd(L.counters + 10, cSobol);
     }
     if (cErr) atomicAdd(L.counters + 6, cErr);
+}
+
+// per-pixel ordered sum of the own-pixel splats: film_own[p] (+)= c[0] + c[1] + ...
+// in sample order -- the reference's `*dest++ += weight * value[k]` sequence
+__global__ void film_reduce(MtsgLaunch L) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= L.num_pixels) return;
+    int px, py;
+    if (!pixel_of(L, p, px, py)) return;
+    float *dst = L.film_own + ((size_t)(py + L.filter.border) * L.fw + (px + L.filter.border)) * 5;
+    float acc[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) acc[k] = dst[k];
+    const size_t plane = (size_t)L.chunk_spp * L.num_pixels;
+    const float *c = L.contrib + p;
+    for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) acc[k] += c[k * plane + (size_t)jj * L.num_pixels];
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dst[k] = acc[k];
 }
 
 __global__ void film_finalize(float *__restrict__ own, const float *__restrict__ spill, size_t n) {
@@ -727,11 +783,30 @@ __global__ void arith_probe(const float *a, const float *b, float *out, int n) {
 // ---------------------------------------------------------------------------
 // host-side launchers (called by capi.cpp)
 // ---------------------------------------------------------------------------
+size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
+    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
+    return ((size_t)L.lds_dims * L.nibbles * 16 + scene + (size_t)L.stack_depth * BLOCK) * 4;
+}
+
+template <bool SCENE_LDS>
+static void launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
+    const size_t lds = mtsg_path_lds_bytes(L);
+    if (samples && stats) hipLaunchKernelGGL((path_kernel<true, true, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else if (samples) hipLaunchKernelGGL((path_kernel<true, false, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else if (stats) hipLaunchKernelGGL((path_kernel<false, true, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else hipLaunchKernelGGL((path_kernel<false, false, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
+}
+
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
-    if (samples && stats) hipLaunchKernelGGL((path_kernel<true, true>), dim3(grid), dim3(BLOCK), 0, stream, L);
-    else if (samples) hipLaunchKernelGGL((path_kernel<true, false>), dim3(grid), dim3(BLOCK), 0, stream, L);
-    else if (stats) hipLaunchKernelGGL((path_kernel<false, true>), dim3(grid), dim3(BLOCK), 0, stream, L);
-    else hipLaunchKernelGGL((path_kernel<false, false>), dim3(grid), dim3(BLOCK), 0, stream, L);
+    if (L.scene_lds) launch_path<true>(L, grid, samples, stats, stream);
+    else launch_path<false>(L, grid, samples, stats, stream);
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream) {
+    const int threads = 256;
+    const int blocks = (int)((L.num_pixels + threads - 1) / threads);
+    hipLaunchKernelGGL(film_reduce, dim3(blocks), dim3(threads), 0, stream, L);
     return hipGetLastError();
 }
 
@@ -747,6 +822,10 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
     return hipGetLastError();
 }
 
-int mtsg_path_kernel_occupancy(int *blocksPerCU) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false>, BLOCK, 0);
+int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
+    if (L.scene_lds)
+        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, true>, BLOCK,
+                                                                 mtsg_path_lds_bytes(L));
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, false>, BLOCK,
+                                                             mtsg_path_lds_bytes(L));
 }

@@ -62,8 +62,8 @@ def load_library(path=None):
 class Context:
     """One libmtsgpu context (one HIP device)."""
 
-    def __init__(self, device=-1):
-        self.L = load_library()
+    def __init__(self, device=-1, lib_path=None):
+        self.L = load_library(lib_path)
         h = C.c_void_p()
         rc = self.L.mtsgpu_create(device, C.byref(h))
         if rc != 0:
