@@ -159,8 +159,10 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
             const bool h0 = n0 <= f0, h1 = n1 <= f1;
             if (h0 && h1) {
                 int nearC = e.x, farC = e.y;
-                if (n1 < n0) { nearC = e.y; farC = e.x; }
-                stk[sp * BLOCK] = farC;
+                float farT = n1;
+                if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
+                stk[sp * (2 * BLOCK)] = farC;
+                stk[sp * (2 * BLOCK) + BLOCK] = __float_as_int(farT);
                 ++sp;
                 node = nearC;
                 continue;
@@ -206,9 +208,14 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 }
             }
         }
-        if (sp == 0) break;
-        --sp;
-        node = stk[sp * BLOCK];
+        // pop, skipping subtrees that start beyond the closest hit found so far
+        bool popped = false;
+        while (sp > 0) {
+            --sp;
+            const float tEntry = __int_as_float(stk[sp * (2 * BLOCK) + BLOCK]);
+            if (ANY || tEntry <= bt) { node = stk[sp * (2 * BLOCK)]; popped = true; break; }
+        }
+        if (!popped) break;
     }
     return found;
 }
@@ -421,55 +428,93 @@ __device__ __forceinline__ bool pixel_of(const MtsgLaunch &L, uint32_t p, int &p
 #define MTSG_WAVES_PER_EU 3
 #endif
 
+// sobol::look_up (sobolseq.h:93-125) as the GF(2) solve it encodes; the XOR of
+// the second dimension's (top m bits of) columns over the index bits comes from
+// 4-bit tables in LDS (ycolTab[c][v]), the m x m inverse from the kernel args
+template <typename T>
+__device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *ycolTab, uint32_t nibbles,
+                                                     uint32_t frame, uint32_t px, uint32_t py, uint64_t scramble) {
+    const uint32_t m = Lu.m;
+    const uint32_t s = (uint32_t)((scramble & 0xFFFFFFFFull) >> (32 - m));
+    const uint32_t mask = (1u << m) - 1u;
+    const uint32_t sx = (px ^ s) & mask, sy = (py ^ s) & mask;
+    const uint32_t jlo = __builtin_bitreverse32(sx) >> (32 - m);
+    const uint64_t index = ((uint64_t)frame << (2 * m)) | jlo;
+    const uint32_t K = (nibbles == 8) ? sobol_bits<8>(ycolTab, index) : sobol_bits<MTSG_NIBBLES>(ycolTab, index);
+    const uint32_t rhs = (sy ^ K) & mask;
+    uint32_t jhi = 0;
+    for (uint32_t t = 0; t < m; ++t) jhi |= (uint32_t)(__builtin_popcount(Lu.inv[t] & rhs) & 1) << t;
+    return index | ((uint64_t)jhi << m);
+}
+
+// One loop iteration = one bounce of Li() for every lane: trace the lane's
+// pending shadow ray (NEE of the previous vertex) and its closest-hit ray
+// (camera or BSDF-sampled), then shade the new vertex: add the NEE estimate if
+// unoccluded, the MIS-weighted emission of the hit, Russian roulette, then at
+// the new vertex draw the NEE sample and the BSDF sample, which produce the
+// next iteration's two rays.  Sampler dimensions are consumed in the
+// reference's order (NEE 2D, BSDF 2D [+1D], RR 1D), and radiance is
+// accumulated in the reference's order (NEE term before the BSDF-hit term).
 template <bool SAMPLES, bool STATS, bool SCENE_LDS>
 __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaunch L) {
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
-    // LDS: [Sobol nibble tables][BVH nodes + TriAccel (small scenes)][traversal stacks]
+    // LDS: [Sobol nibble tables][look_up column tables][BVH + TriAccel (small scenes)][stacks]
     const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
     for (uint32_t i = threadIdx.x; i < tabWords; i += BLOCK) {
         const uint32_t d = i / (L.nibbles * 16), r = i % (L.nibbles * 16);
         lds[i] = L.sobol_nib[(size_t)d * MTSG_NIBBLES * 16 + r];
     }
+    for (uint32_t i = threadIdx.x; i < 16 * 16; i += BLOCK) {
+        const uint32_t c = i >> 4, v = i & 15;
+        uint32_t r = 0;
+        for (int b = 0; b < 4; ++b)
+            if ((v >> b) & 1) r ^= L.lut.ycol[4 * c + b];
+        lds[tabWords + i] = r;
+    }
+    const uint32_t base2 = tabWords + 16 * 16;
     uint32_t sceneWords = 0;
     if (SCENE_LDS) {
         const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
         const uint32_t *gn = reinterpret_cast<const uint32_t *>(S.nodes);
         const uint32_t *gt = reinterpret_cast<const uint32_t *>(S.tris);
-        for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[tabWords + i] = gn[i];
-        for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[tabWords + nodeWords + i] = gt[i];
+        for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[base2 + i] = gn[i];
+        for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[base2 + nodeWords + i] = gt[i];
         sceneWords = nodeWords + triWords;
     }
     __syncthreads();
-    lds_node *ldsNodes = (lds_node *)(lds + tabWords);
-    lds_tri *ldsTris = (lds_tri *)(lds + tabWords + L.num_nodes * 16);
+    lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
+    lds_node *ldsNodes = (lds_node *)(lds + base2);
+    lds_tri *ldsTris = (lds_tri *)(lds + base2 + L.num_nodes * 16);
     SobolCtx SC;
     SC.lds = (lds_u32 *)lds;
     SC.glob = (glb_u32 *)L.sobol_nib;
     SC.lds_dims = L.lds_dims;
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
-    int *stk = reinterpret_cast<int *>(lds + tabWords + sceneWords) + threadIdx.x;
+    int *stk = reinterpret_cast<int *>(lds + base2 + sceneWords) + threadIdx.x;
 
     unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
     unsigned long long cHits = 0, cNee = 0, cSobol = 0;
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
     uint64_t item = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-    int state = ST_NEWSAMPLE;
+    bool active = false, done = false;
     int px = 0, py = 0;
     uint32_t j = 0, pix = 0;
     SamplerState smp;
     smp.sobolIndex = 0; smp.sampleIndex = 0; smp.dim = 0; smp.err = false;
     PathVars P;
     float sx = 0, sy = 0;
-    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1);    // the ray traced in this iteration
-    float rmint = 0, rmaxt = 0;
+    // rays of this iteration: closest (camera / extension) and shadow (NEE)
+    bool haveRay = false, primary = false, haveShadow = false;
+    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), sd = mk(0, 0, 1);
+    float rmint = 0, rmaxt = 0, smaxt = 0;
 
     while (true) {
         // ---- A: start the next sample (renderBlock loop body, integrator.cpp:165-186)
-        while (state == ST_NEWSAMPLE) {
-            if (item >= L.num_items) { state = ST_DONE; break; }
+        while (!active && !done) {
+            if (item >= L.num_items) { done = true; break; }
             const uint64_t it = item;
             item += lanes;
             const uint32_t jj = (uint32_t)(it / L.num_pixels);
@@ -480,8 +525,10 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             smp.dim = 0;
             smp.sampleIndex = j;
             smp.err = false;
-            if (L.lut.m > 1) smp.sobolIndex = sobol_lookup(L.lut, j, (uint32_t)px, (uint32_t)py, L.scramble64);
-            else smp.sobolIndex = j;
+            if (L.lut.m > 1)
+                smp.sobolIndex = sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py, L.scramble64);
+            else
+                smp.sobolIndex = j;
             float u, v;
             next2d(SC, L.resolution, smp, px, py, u, v);
             sx = (float)px + u;
@@ -505,199 +552,193 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             P.depth = 1;
             P.scattered = false;
             P.emitted = true;
-            state = ST_PRIMARY;
+            haveRay = true;
+            primary = true;
+            haveShadow = false;
+            active = true;
         }
-        if (__all(state == ST_DONE)) break;
+        if (__all(done)) break;
 
-        // ---- B: trace one ray per active lane ------------------------------
+        // ---- B: trace the shadow ray, then the closest-hit ray ---------------
+        bool occluded = false;
+        if (active && haveShadow) {
+            cShadow++;
+            float mint, maxt;
+            // a shadow ray whose estimate is zero cannot change Li: skip its traversal
+            if (!is_zero(P.neeC) && ray_interval(S, P.its.p, sd, D_EPSILON, smaxt, true, mint, maxt)) {
+                uint32_t sl; float a0, a1, a2;
+                if (SCENE_LDS)
+                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+                else
+                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+            }
+        }
         bool hit = false;
         uint32_t slot = 0;
         float hu = 0, hv = 0, ht = 0;
-        if (state != ST_DONE) {
-            const bool shadow = state == ST_SHADOW;
-            if (shadow) cShadow++; else cRays++;
+        if (active && haveRay) {
+            cRays++;
             float mint, maxt;
-            // a shadow ray whose estimate is zero cannot change Li: skip its traversal
-            const bool needed = !shadow || !is_zero(P.neeC);
-            if (needed && ray_interval(S, ro, rd, rmint, rmaxt, shadow, mint, maxt)) {
-                if (SCENE_LDS) {
-                    if (shadow)
-                        hit = traverse<true, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
-                    else
-                        hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
-                } else {
-                    glb_node *gn = (glb_node *)S.nodes;
-                    glb_tri *gt = (glb_tri *)S.tris;
-                    if (shadow)
-                        hit = traverse<true, STATS>(gn, gt, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
-                    else
-                        hit = traverse<false, STATS>(gn, gt, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
-                }
+            if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
+                if (SCENE_LDS)
+                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                else
+                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
             }
         }
 
-        // ---- C: advance the path state machine ------------------------------
-        bool vertex = false;      // run the loop head of Li() for P.its
+        // ---- C: shade -------------------------------------------------------
         bool endPath = false;
-        bool doBsdf = false;      // sample the BSDF at P.its
-        if (state == ST_PRIMARY) {
-            // rRec.rayIntersect (records.inl:117-144)
-            if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
-            if (STATS && hit) cHits++;
-            P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
-            vertex = true;
-        } else if (state == ST_SHADOW) {
-            // Scene::sampleEmitterDirect's visibility test (scene.cpp:838-842)
-            if (!hit) P.L = add(P.L, P.neeC);
-            doBsdf = true;
-        } else if (state == ST_EXT) {
-            // after scene->rayIntersect(ray, its) (path.cpp:226-286)
-            if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
-            if (STATS && hit) cHits++;
-            if (!P.its.valid) {
-                endPath = true;   // no environment emitter: break before the throughput update
+        if (active) {
+            // NEE of the previous vertex (scene.cpp:838-842, path.cpp:176-199)
+            if (haveShadow && !occluded) P.L = add(P.L, P.neeC);
+            haveShadow = false;
+            bool vertex = false;
+            if (!haveRay) {
+                endPath = true;   // the BSDF sample at the previous vertex failed
             } else {
-                const MtsgShape &sh = S.shapes[P.its.shape];
-                P.thr = mulv(P.thr, P.bsdfWeight);
-                P.eta *= P.bsdfEta;
-                if (sh.emitter >= 0) {
-                    const f3 value = area_Le(S, P.its, neg(rd));
-                    float lumPdf = 0;
-                    if (!(P.sampledType & MTSG_F_DELTA)) {
-                        // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
-                        // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
-                        const MtsgEmitter &e = S.emitters[sh.emitter];
-                        const f3 dn = P.its.sh.n;
-                        float pdf = 0.0f;
-                        if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0)
-                            pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
-                        lumPdf = pdf * (e.weight * S.em_norm);
-                    }
-                    const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
-                    P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
-                }
-                P.emitted = false;
-                if (P.depth++ >= L.rr_depth) {
-                    const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
-                    if (next1d(SC, smp) >= q) endPath = true;
-                    else P.thr = divs(P.thr, q);
-                }
-                if (smp.err) endPath = true;
-                if (!endPath) vertex = true;
-            }
-        }
-
-        if (vertex) {
-            // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
-            const f3 inDir = rd;
-            if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
-                endPath = true;
-            } else if (!P.its.valid) {
-                endPath = true;   // primary miss, no environment emitter
-            } else {
-                const MtsgShape &sh = S.shapes[P.its.shape];
-                const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
-                if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
-                    P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(inDir))));
-                if ((P.depth >= L.max_depth && L.max_depth > 0) ||
-                    (L.strict_normals && dot(inDir, P.its.geoN) * P.its.wi.z >= 0)) {
-                    endPath = true;
+                // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
+                if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+                if (STATS && hit) cHits++;
+                if (primary) {
+                    P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
+                    vertex = true;
+                } else if (!P.its.valid) {
+                    endPath = true;   // no environment emitter: break before the throughput update
                 } else {
-                    P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
-                    doBsdf = true;
-                    if (bsdf.flags & MTSG_F_SMOOTH) {
-                        // Scene::sampleEmitterDirect (scene.cpp:828-852)
-                        float ex, ey;
-                        next2d(SC, L.resolution, smp, px, py, ex, ey);
-                        float emPdf;
-                        const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
-                        if (STATS) cNee++;
-                        const MtsgEmitter &e = S.emitters[ei];
-                        // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
-                        float py2 = ey;
-                        const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
-                        const uint32_t prim = e.tri_first + lt;
-                        const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
-                        const float a = safe_sqrt(1.0f - ex);
-                        const float bx = 1 - a, by = a * py2;
-                        const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
-                                 p2 = ld3(S.positions + 3 * (size_t)pv.z);
-                        const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
-                        const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
-                        f3 ln;
-                        if (S.shapes[e.shape].has_normals) {
-                            const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
-                                     n2 = ld3(S.normals + 3 * (size_t)pv.z);
-                            ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
-                        } else {
-                            ln = normalize(cross(sideA, sideB));
+                    const MtsgShape &sh = S.shapes[P.its.shape];
+                    P.thr = mulv(P.thr, P.bsdfWeight);
+                    P.eta *= P.bsdfEta;
+                    if (sh.emitter >= 0) {
+                        const f3 value = area_Le(S, P.its, neg(rd));
+                        float lumPdf = 0;
+                        if (!(P.sampledType & MTSG_F_DELTA)) {
+                            // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
+                            // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
+                            const MtsgEmitter &e = S.emitters[sh.emitter];
+                            const f3 dn = P.its.sh.n;
+                            float pdf = 0.0f;
+                            if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0)
+                                pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
+                            lumPdf = pdf * (e.weight * S.em_norm);
                         }
-                        float pdf = e.inv_area;
-                        // Shape::sampleDirect (shape.cpp:102-115)
-                        f3 dd = sub(lp, P.its.p);
-                        const float distSquared = len2(dd);
-                        const float dist = dsqrt(distSquared);
-                        dd = divs(dd, dist);
-                        const float dp = absdot(dd, ln);
-                        pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
-                        // AreaLight::sampleDirect (area.cpp:158-173)
-                        f3 value = mk(0, 0, 0);
-                        if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
-                        else pdf = 0.0f;
-                        if (pdf != 0) {
-                            // everything of the NEE estimate but the visibility (path.cpp:176-199)
-                            const float dpdf = pdf * emPdf;
-                            value = divs(value, emPdf);
-                            f3 c = mk(0, 0, 0);
-                            if (!is_zero(value)) {
-                                const f3 wo = to_local(P.its.sh, dd);
-                                const f3 bsdfVal = bsdf_eval(bsdf, P.its.wi, wo);
-                                if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                    const float bsdfPdf = bsdf_pdf(bsdf, P.its.wi, wo);
-                                    const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
-                                    const float weight = pa / (pa + pb);
-                                    c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
-                                }
+                        const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                        P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
+                    }
+                    P.emitted = false;
+                    if (P.depth++ >= L.rr_depth) {
+                        const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
+                        if (next1d(SC, smp) >= q) endPath = true;
+                        else P.thr = divs(P.thr, q);
+                    }
+                    if (smp.err) endPath = true;
+                    vertex = !endPath;
+                }
+            }
+            haveRay = false;
+            primary = false;
+
+            if (vertex) {
+                // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
+                if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
+                    endPath = true;
+                } else if (!P.its.valid) {
+                    endPath = true;   // camera ray missed, no environment emitter
+                } else {
+                    const MtsgShape &sh = S.shapes[P.its.shape];
+                    const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
+                    if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
+                        P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
+                    if ((P.depth >= L.max_depth && L.max_depth > 0) ||
+                        (L.strict_normals && dot(rd, P.its.geoN) * P.its.wi.z >= 0)) {
+                        endPath = true;
+                    } else {
+                        P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
+                        if (bsdf.flags & MTSG_F_SMOOTH) {
+                            // Scene::sampleEmitterDirect (scene.cpp:828-852)
+                            float ex, ey;
+                            next2d(SC, L.resolution, smp, px, py, ex, ey);
+                            float emPdf;
+                            const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
+                            if (STATS) cNee++;
+                            const MtsgEmitter &e = S.emitters[ei];
+                            // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
+                            float py2 = ey;
+                            const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
+                            const uint32_t prim = e.tri_first + lt;
+                            const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
+                            const float a = safe_sqrt(1.0f - ex);
+                            const float bx = 1 - a, by = a * py2;
+                            const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
+                                     p2 = ld3(S.positions + 3 * (size_t)pv.z);
+                            const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
+                            const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
+                            f3 ln;
+                            if (S.shapes[e.shape].has_normals) {
+                                const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
+                                         n2 = ld3(S.normals + 3 * (size_t)pv.z);
+                                ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
+                            } else {
+                                ln = normalize(cross(sideA, sideB));
                             }
-                            P.neeC = c;
-                            // Ray(dRec.ref, dRec.d, Epsilon, dRec.dist*(1-ShadowEpsilon)) (scene.cpp:839-840)
-                            ro = P.its.p;
-                            rd = dd;
-                            rmint = D_EPSILON;
-                            rmaxt = dist * (1 - D_SHADOW_EPSILON);
-                            state = ST_SHADOW;
-                            doBsdf = false;   // BSDF sampling resumes after the shadow trace
+                            float pdf = e.inv_area;
+                            // Shape::sampleDirect (shape.cpp:102-115)
+                            f3 dd = sub(lp, P.its.p);
+                            const float distSquared = len2(dd);
+                            const float dist = dsqrt(distSquared);
+                            dd = divs(dd, dist);
+                            const float dp = absdot(dd, ln);
+                            pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+                            // AreaLight::sampleDirect (area.cpp:158-173)
+                            f3 value = mk(0, 0, 0);
+                            if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+                            else pdf = 0.0f;
+                            if (pdf != 0) {
+                                // the NEE estimate but for visibility (path.cpp:176-199)
+                                const float dpdf = pdf * emPdf;
+                                value = divs(value, emPdf);
+                                f3 c = mk(0, 0, 0);
+                                if (!is_zero(value)) {
+                                    const f3 wo = to_local(P.its.sh, dd);
+                                    const f3 bsdfVal = bsdf_eval(bsdf, P.its.wi, wo);
+                                    if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
+                                        const float bsdfPdf = bsdf_pdf(bsdf, P.its.wi, wo);
+                                        const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
+                                        const float weight = pa / (pa + pb);
+                                        c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
+                                    }
+                                }
+                                // Ray(dRec.ref, dRec.d, Epsilon, dRec.dist*(1-ShadowEpsilon)) (scene.cpp:839-840)
+                                P.neeC = c;
+                                sd = dd;
+                                smaxt = dist * (1 - D_SHADOW_EPSILON);
+                                haveShadow = true;
+                            }
                         }
+                        // BSDF sampling (path.cpp:206-226)
+                        float bx2, by2;
+                        next2d(SC, L.resolution, smp, px, py, bx2, by2);
+                        float u1d = 0.0f;
+                        if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
+                        const BSample bs = bsdf_sample(bsdf, P.its.wi, bx2, by2, u1d);
+                        if (!is_zero(bs.weight) && !smp.err) {
+                            P.scattered |= bs.sampledType != MTSG_F_NULL;
+                            const f3 wo = to_world(P.its.sh, bs.wo);
+                            if (!L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
+                                P.bsdfWeight = bs.weight;
+                                P.bsdfPdf = bs.pdf;
+                                P.bsdfEta = bs.eta;
+                                P.sampledType = bs.sampledType;
+                                ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
+                                rd = wo;
+                                rmint = D_EPSILON;
+                                rmaxt = INFINITY;
+                                haveRay = true;
+                            }
+                        }
+                        // no next ray: the path ends once the pending shadow ray is resolved
+                        if (!haveRay && !haveShadow) endPath = true;
                     }
-                }
-            }
-        }
-
-        if (doBsdf && !endPath) {
-            // BSDF sampling (path.cpp:206-226)
-            state = ST_EXT;
-            const MtsgBsdf &bsdf = S.bsdfs[S.shapes[P.its.shape].bsdf];
-            float bx, by;
-            next2d(SC, L.resolution, smp, px, py, bx, by);
-            float u1d = 0.0f;
-            if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
-            const BSample bs = bsdf_sample(bsdf, P.its.wi, bx, by, u1d);
-            if (is_zero(bs.weight) || smp.err) {
-                endPath = true;
-            } else {
-                P.scattered |= bs.sampledType != MTSG_F_NULL;
-                const f3 wo = to_world(P.its.sh, bs.wo);
-                if (L.strict_normals && dot(P.its.geoN, wo) * bs.wo.z <= 0) {
-                    endPath = true;
-                } else {
-                    P.bsdfWeight = bs.weight;
-                    P.bsdfPdf = bs.pdf;
-                    P.bsdfEta = bs.eta;
-                    P.sampledType = bs.sampledType;
-                    ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
-                    rd = wo;
-                    rmint = D_EPSILON;
-                    rmaxt = INFINITY;
                 }
             }
         }
@@ -721,7 +762,8 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             cSamples++;
             if (STATS) cSobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
             if (smp.err) cErr++;
-            state = ST_NEWSAMPLE;
+            active = false;
+            haveRay = haveShadow = false;
         }
     }
     atomicAdd(L.counters + 0, cSamples);
@@ -785,7 +827,7 @@ __global__ void arith_probe(const float *a, const float *b, float *out, int n) {
 // ---------------------------------------------------------------------------
 size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
     const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
-    return ((size_t)L.lds_dims * L.nibbles * 16 + scene + (size_t)L.stack_depth * BLOCK) * 4;
+    return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + (size_t)L.stack_depth * 2 * BLOCK) * 4;
 }
 
 template <bool SCENE_LDS>
