@@ -258,7 +258,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // own-pixel splat buffer [5][chunk][pixels]; spp processed in chunks that fit the budget
     size_t budget = (size_t)8 << 30;
     if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);
-    const size_t perSample = (size_t)L.num_pixels * 5 * 4;
+    const size_t perSample = (size_t)L.num_pixels * 4 * 4;   // float4 per sample
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));
     const size_t filmFloats = (size_t)L.fw * L.fh * 5;
     if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||

@@ -10,6 +10,12 @@
 #include "layout.h"
 
 enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
+
+#ifdef MTSG_BSDF_INLINE
+#define BSDF_CALL __device__ __forceinline__
+#else
+#define BSDF_CALL __device__ __noinline__
+#endif
 enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2 };
 
 __device__ __forceinline__ float tan_theta(f3 v) {           // frame.h:117-122
@@ -342,7 +348,7 @@ __device__ __forceinline__ f3 refract_v(f3 wi, f3 n, float eta, float cosThetaT)
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 
 // ---- BSDF::eval / pdf / sample --------------------------------------------
-__device__ __noinline__ f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
+BSDF_CALL f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
     const f3 zero = mk(0, 0, 0);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
         if (wi.z <= 0 || wo.z <= 0) return zero;
@@ -386,7 +392,7 @@ __device__ __noinline__ f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
     return mul(ld3(b.spec_t), fabsf(value * factor * factor));
 }
 
-__device__ __noinline__ float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
+BSDF_CALL float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
@@ -425,7 +431,7 @@ __device__ __noinline__ float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
 // the caller, which draws it from the sampler only for that BSDF.
 struct BSample { f3 wo; f3 weight; float pdf; float eta; int sampledType; };
 
-__device__ __noinline__ BSample bsdf_sample(const MtsgBsdf &b, f3 wi, float sx, float sy, float u1d) {
+BSDF_CALL BSample bsdf_sample(const MtsgBsdf &b, f3 wi, float sx, float sy, float u1d) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150

@@ -130,7 +130,6 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
     const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
     const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
-    (void)ox; (void)oy; (void)oz;
     bool found = false;
     uint32_t bestPrim = 0;
     bt = maxt;
@@ -144,18 +143,18 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
             const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
             const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
             const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
-            // child 0
-            float t0x = (a.x - o.x) * ix, t1x = (a.y - o.x) * ix;
-            float t0y = (a.z - o.y) * iy, t1y = (a.w - o.y) * iy;
-            float t0z = (c.x - o.z) * iz, t1z = (c.y - o.z) * iz;
-            float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
-            float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
-            // child 1
-            float u0x = (b.x - o.x) * ix, u1x = (b.y - o.x) * ix;
-            float u0y = (b.z - o.y) * iy, u1y = (b.w - o.y) * iy;
-            float u0z = (c.z - o.z) * iz, u1z = (c.w - o.z) * iz;
-            float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
-            float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
+            // slab tests; node boxes are conservatively inflated on the host, so the
+            // fused (o*inv precomputed) form needs no bit-exactness
+            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
+            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
+            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
+            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
+            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
+            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
+            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
+            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
             const bool h0 = n0 <= f0, h1 = n1 <= f1;
             if (h0 && h1) {
                 int nearC = e.x, farC = e.y;
@@ -327,11 +326,11 @@ __device__ __forceinline__ float filter_disc(const MtsgFilter &F, float x) {
     return F.values[i];
 }
 
-__device__ __forceinline__ void film_splat(const MtsgLaunch &L, int px, int py, float sx, float sy,
-                                           const float *val, float *own) {
+__device__ __forceinline__ bool film_splat(const MtsgLaunch &L, int px, int py, float sx, float sy,
+                                           const float *val, float &ownW) {
 #pragma unroll
     for (int i = 0; i < 5; ++i)
-        if (!isfinite(val[i]) || val[i] < 0) return;
+        if (!isfinite(val[i]) || val[i] < 0) return false;
     const MtsgFilter &F = L.filter;
     const int b = F.border;
     const int bx = (px / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE, by = (py / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE;
@@ -350,8 +349,7 @@ __device__ __forceinline__ void film_splat(const MtsgLaunch &L, int px, int py, 
             const int gx = x + bx, gy = y + by;
             if (gx >= L.fw || gy >= L.fh) continue;
             if (gx == px + b && gy == py + b) {
-#pragma unroll
-                for (int k = 0; k < 5; ++k) own[k] += weight * val[k];
+                ownW = weight;
             } else {
                 float *dst = L.film_spill + ((size_t)gy * L.fw + gx) * 5;
 #pragma unroll
@@ -359,6 +357,7 @@ __device__ __forceinline__ void film_splat(const MtsgLaunch &L, int px, int py, 
             }
         }
     }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -484,8 +483,9 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
     }
     __syncthreads();
     lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
-    lds_node *ldsNodes = (lds_node *)(lds + base2);
-    lds_tri *ldsTris = (lds_tri *)(lds + base2 + L.num_nodes * 16);
+    // base2 and the node array size are multiples of 4 words: 16-byte aligned (ds_read_b128)
+    lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
+    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
     SobolCtx SC;
     SC.lds = (lds_u32 *)lds;
     SC.glob = (glb_u32 *)L.sobol_nib;
@@ -565,7 +565,11 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             cShadow++;
             float mint, maxt;
             // a shadow ray whose estimate is zero cannot change Li: skip its traversal
+#ifdef MTSG_ABL_NO_SHADOW
+            if (false) {
+#else
             if (!is_zero(P.neeC) && ray_interval(S, P.its.p, sd, D_EPSILON, smaxt, true, mint, maxt)) {
+#endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS)
                     occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
@@ -744,14 +748,16 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
         }
 
         if (endPath) {
-            // block->put(samplePos, spec, alpha) (integrator.cpp:184): own-pixel splat -> contrib
+            // block->put(samplePos, spec, alpha) (integrator.cpp:184): the own-pixel
+            // splat is stored as {L.rgb, w} (alpha in {0,1} in the sign bit of w) and
+            // film_reduce re-forms weight * value[k] -- the same products
             const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
-            float own[5] = {0, 0, 0, 0, 0};
-            film_splat(L, px, py, sx, sy, val, own);
-            const size_t plane = (size_t)L.chunk_spp * L.num_pixels;
-            float *c = L.contrib + (size_t)(j - L.j0) * L.num_pixels + pix;
-#pragma unroll
-            for (int k = 0; k < 5; ++k) c[k * plane] = own[k];
+            float ownW = 0.0f;
+            const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
+            float4 rec4;
+            if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha == 0.0f ? -ownW : ownW);
+            else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
             if (SAMPLES) {
                 const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
                 float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
@@ -791,11 +797,16 @@ __global__ void film_reduce(MtsgLaunch L) {
     float acc[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) acc[k] = dst[k];
-    const size_t plane = (size_t)L.chunk_spp * L.num_pixels;
-    const float *c = L.contrib + p;
+    const float4 *c = reinterpret_cast<const float4 *>(L.contrib) + p;
     for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) acc[k] += c[k * plane + (size_t)jj * L.num_pixels];
+        const float4 r = c[(size_t)jj * L.num_pixels];
+        const float w = fabsf(r.w);
+        const float alpha = signbit(r.w) ? 0.0f : 1.0f;
+        acc[0] += w * r.x;
+        acc[1] += w * r.y;
+        acc[2] += w * r.z;
+        acc[3] += w * alpha;
+        acc[4] += w * 1.0f;
     }
 #pragma unroll
     for (int k = 0; k < 5; ++k) dst[k] = acc[k];

@@ -41,7 +41,7 @@ class BSDF:
     specularTransmittance: tuple = (1.0, 1.0, 1.0)
     eta: tuple = (0.0, 0.0, 0.0)       # roughconductor RGB eta (see conductors.py)
     k: tuple = (1.0, 1.0, 1.0)
-    material: Optional[str] = 'Cu'
+    material: Optional[str] = None
     extEta: object = 'air'
     intIOR: object = 'bk7'
     extIOR: object = 'air'
@@ -72,8 +72,9 @@ class BSDF:
             if self.material is not None and self.material.lower() == 'none':
                 eta, k = (0.0, 0.0, 0.0), (1.0, 1.0, 1.0)
             elif self.material is not None:
-                from .conductors import conductor_rgb
-                eta, k = conductor_rgb(self.material)
+                raise NotImplementedError(
+                    "roughconductor 'material' lookup (data/ior/*.spd -> RGB) is host-side and not "
+                    "implemented; pass explicit RGB 'eta'/'k' with material=None")
             else:
                 eta, k = self.eta, self.k
             d.eta[:] = eta

@@ -48,21 +48,48 @@ def _quads_mesh(quads, inward=True, center=_CENTER):
     return (np.asarray(pos, np.float64) * S).astype(np.float32), np.asarray(idx, np.uint32)
 
 
-def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1):
+# RGB complex IOR of copper (linear sRGB primaries; used as explicit 'eta'/'k'
+# properties -- the reference's named-material .spd -> RGB conversion is a
+# host-side step outside the hot path)
+CU_ETA = (0.200438, 0.924033, 1.10221)
+CU_K = (3.91295, 2.45285, 2.14219)
+
+
+def rough_materials():
+    """BSDF set exercising every rough-BSDF code path of the kernel."""
+    return [
+        BSDF('roughconductor', distribution='ggx', alpha=0.2, material=None, eta=CU_ETA, k=CU_K),
+        BSDF('roughdielectric', distribution='beckmann', alpha=0.15, intIOR=1.5, extIOR='air'),
+        BSDF('roughconductor', distribution='beckmann', alpha=0.35, material=None, eta=CU_ETA, k=CU_K),
+        BSDF('roughdielectric', distribution='ggx', alpha=0.3, intIOR='bk7', extIOR='air'),
+        BSDF('roughconductor', distribution='phong', alpha=0.25, material=None, eta=CU_ETA, k=CU_K),
+        BSDF('roughconductor', distribution='ggx', alpha=0.1, sampleVisible=False, material='none'),
+        BSDF('roughdielectric', distribution='ggx', alpha=0.2, sampleVisible=False, intIOR=1.33),
+    ]
+
+
+def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, materials='diffuse'):
     """Config C1 (512x512, 64 spp) / C2 (1280x720, 512 spp): diffuse Cornell box
-    with a rectangular area light."""
+    with a rectangular area light.  materials='rough' swaps the
+    blocks and floor for rough conductors/dielectrics (parity coverage)."""
     white = BSDF('diffuse', reflectance=(0.725, 0.71, 0.68))
     red = BSDF('diffuse', reflectance=(0.63, 0.065, 0.05))
     green = BSDF('diffuse', reflectance=(0.14, 0.45, 0.091))
     bsdfs = [white, red, green]
     meshes = []
     # room surfaces: vertex normals left to TriMesh::computeNormals (trimesh.cpp:608-681)
-    for quad, b in ((_FLOOR, 0), (_CEIL, 0), (_BACK, 0), (_GREEN, 2), (_RED, 1)):
+    floor_b, short_b, tall_b = 0, 0, 0
+    if materials == 'rough':
+        rough = rough_materials()
+        base = len(bsdfs)
+        bsdfs += rough
+        floor_b, short_b, tall_b = base + 2, base + 0, base + 1
+    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, 0), (_GREEN, 2), (_RED, 1)):
         p, i = _quads_mesh([quad], inward=True)
         meshes.append(Mesh(p, i, bsdf=b))
-    for quads in (_SHORT, _TALL):
+    for quads, b in ((_SHORT, short_b), (_TALL, tall_b)):
         p, i = _quads_mesh(quads, inward=False, center=np.mean(np.asarray(quads, np.float64).reshape(-1, 3), 0))
-        meshes.append(Mesh(p, i, bsdf=0, faceNormals=True))
+        meshes.append(Mesh(p, i, bsdf=b, faceNormals=True))
     p, i = _quads_mesh([_LIGHT], inward=True)
     meshes.append(Mesh(p, i, bsdf=-1, emitter=0, faceNormals=True))
     emitters = [Emitter('area', radiance=(17.0, 12.0, 4.0))]
