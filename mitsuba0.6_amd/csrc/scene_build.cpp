@@ -500,6 +500,16 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         if (m.emitter >= (int)D->num_emitters) { err = "emitter index out of range"; return MTSGPU_EINVAL; }
         if (m.bsdf >= (int)nb) { err = "bsdf index out of range"; return MTSGPU_EINVAL; }
         sh.bsdf = m.bsdf >= 0 ? m.bsdf : (m.emitter >= 0 ? (int)nb : (int)nb + 1);
+        {   // EAnisotropic (roughconductor.cpp:229-231) without texcoords: computeUVTangents error (trimesh.cpp:685-691)
+            const mtsgpu_bsdf_desc *ub = m.bsdf >= 0 ? &D->bsdfs[m.bsdf] : nullptr;
+            if (!m.texcoords && ub && ub->type != MTSGPU_BSDF_DIFFUSE &&
+                fmax_std(ub->alpha_u, 1e-4f) != fmax_std(ub->alpha_v, 1e-4f)) {
+                err = "computeUVTangents(): texture coordinates are required to generate tangent vectors. If you "
+                      "want to render with an anisotropic material, please make sure that all associated shapes "
+                      "have valid texture coordinates.";
+                return MTSGPU_EINVAL;
+            }
+        }
         // TriMesh::computeNormals (trimesh.cpp:608-681)
         bool hasNormals = false;
         if (m.face_normals) {

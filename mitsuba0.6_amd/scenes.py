@@ -31,9 +31,10 @@ _TALL = [[(423, 330, 247), (265, 330, 296), (314, 330, 456), (472, 330, 406)],
 _CENTER = np.array([278.0, 274.4, 279.6])
 
 
-def _quads_mesh(quads, inward=True, center=_CENTER):
+def _quads_mesh(quads, inward=True, center=_CENTER, uv=False):
     """Triangulate quads (0,1,2),(0,2,3); orient each so its normal faces `center`
-    (inside of the room) or away from it (outside of a block)."""
+    (inside of the room) or away from it (outside of a block).  uv=True also
+    returns per-vertex texcoords (0,0),(1,0),(1,1),(0,1) per quad."""
     pos, idx = [], []
     for q in quads:
         q = np.asarray(q, np.float64)
@@ -45,7 +46,10 @@ def _quads_mesh(quads, inward=True, center=_CENTER):
         base = len(pos)
         pos.extend(q)
         idx += [(base, base + 1, base + 2), (base, base + 2, base + 3)]
-    return (np.asarray(pos, np.float64) * S).astype(np.float32), np.asarray(idx, np.uint32)
+    p, i = (np.asarray(pos, np.float64) * S).astype(np.float32), np.asarray(idx, np.uint32)
+    if uv:
+        return p, i, np.tile(np.array([[0, 0], [1, 0], [1, 1], [0, 1]], np.float32), (len(quads), 1))
+    return p, i
 
 
 # RGB complex IOR of copper (linear sRGB primaries; used as explicit 'eta'/'k'
@@ -65,6 +69,9 @@ def rough_materials():
         BSDF('roughconductor', distribution='phong', alpha=0.25, material=None, eta=CU_ETA, k=CU_K),
         BSDF('roughconductor', distribution='ggx', alpha=0.1, sampleVisible=False, material='none'),
         BSDF('roughdielectric', distribution='ggx', alpha=0.2, sampleVisible=False, intIOR=1.33),
+        BSDF('roughconductor', distribution='ggx', alphaU=0.05, alphaV=0.4, material=None, eta=CU_ETA, k=CU_K),
+        BSDF('roughdielectric', distribution='beckmann', alphaU=0.3, alphaV=0.08, intIOR=1.5),
+        BSDF('roughconductor', distribution='phong', alphaU=0.1, alphaV=0.3, material=None, eta=CU_ETA, k=CU_K),
     ]
 
 
@@ -83,13 +90,14 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
         rough = rough_materials()
         base = len(bsdfs)
         bsdfs += rough
-        floor_b, short_b, tall_b = base + 2, base + 0, base + 1
+        floor_b, short_b, tall_b = base + 7, base + 0, base + 1
+    uv = materials == 'rough'    # UV tangents on every rough surface (anisotropic ones require them)
     for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, 0), (_GREEN, 2), (_RED, 1)):
-        p, i = _quads_mesh([quad], inward=True)
-        meshes.append(Mesh(p, i, bsdf=b))
+        m = _quads_mesh([quad], inward=True, uv=uv)
+        meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b))
     for quads, b in ((_SHORT, short_b), (_TALL, tall_b)):
-        p, i = _quads_mesh(quads, inward=False, center=np.mean(np.asarray(quads, np.float64).reshape(-1, 3), 0))
-        meshes.append(Mesh(p, i, bsdf=b, faceNormals=True))
+        m = _quads_mesh(quads, inward=False, center=np.mean(np.asarray(quads, np.float64).reshape(-1, 3), 0), uv=uv)
+        meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b, faceNormals=True))
     p, i = _quads_mesh([_LIGHT], inward=True)
     meshes.append(Mesh(p, i, bsdf=-1, emitter=0, faceNormals=True))
     emitters = [Emitter('area', radiance=(17.0, 12.0, 4.0))]
