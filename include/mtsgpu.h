@@ -86,6 +86,9 @@ typedef struct {
     uint32_t env_width, env_height;
     float env_scale;                /* 'scale'                                     */
     float env_to_world[16];         /* row-major 4x4 'toWorld'                     */
+    float env_to_world_inv[16];     /* its inverse as the reference's Transform    */
+                                    /* carries it (transform.cpp); all zero: the   */
+                                    /* library inverts env_to_world (Gauss-Jordan) */
 } mtsgpu_emitter_desc;
 
 typedef struct {
@@ -190,6 +193,13 @@ int mtsgpu_render_device(mtsgpu_ctx *ctx, const mtsgpu_render_params *params,
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */
 int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *out, int n);
 int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4);
+/* Host-only (no device needed): configure `scene` and return its environment
+ * emitter's tables -- params[64] = {levels, w0, h0, normalization, pixel_x,
+ * pixel_y, scale, center xyz, radius, total texels, .., lw[l] at 16+l, lh[l] at
+ * 34+l}; texels: 4 halves per texel (RGB + pad), all levels (capacity in
+ * halves); rows h0+1, cols h0*(w0+1), weights h0 floats (any may be NULL). */
+int mtsgpu_debug_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
+                            float *rows, float *cols, float *weights);
 /* Last error message of this context (or of the last failed create). */
 const char *mtsgpu_last_error(mtsgpu_ctx *ctx);
 void mtsgpu_destroy(mtsgpu_ctx *ctx);

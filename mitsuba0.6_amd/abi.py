@@ -34,7 +34,7 @@ class BsdfDesc(C.Structure):
 class EmitterDesc(C.Structure):
     _fields_ = [('type', C.c_int32), ('radiance', _f3), ('sampling_weight', C.c_float),
                 ('env_rgb', C.POINTER(C.c_float)), ('env_width', C.c_uint32), ('env_height', C.c_uint32),
-                ('env_scale', C.c_float), ('env_to_world', _f16)]
+                ('env_scale', C.c_float), ('env_to_world', _f16), ('env_to_world_inv', _f16)]
 
 
 class MeshDesc(C.Structure):

@@ -59,6 +59,7 @@ struct mtsgpu_ctx {
     HostScene host;
     MtsgDeviceScene dscene;
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
+    DevBuf env, env_texels, env_rows, env_cols, env_weights;
     DevBuf film_own, film_spill, samples, counters, contrib;
 };
 
@@ -159,6 +160,20 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         (e = upload(ctx->emitters, H.emitters, s)) != hipSuccess || (e = upload(ctx->area_cdf, H.area_cdf, s)) != hipSuccess ||
         (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, sobol_nibble_tables(), s)) != hipSuccess)
         return hip_fail(ctx, e, "scene upload");
+    const MtsgEnv *denv = nullptr;
+    if (H.env.emitter >= 0) {
+        if ((e = upload(ctx->env_texels, H.env_texels, s)) != hipSuccess || (e = upload(ctx->env_rows, H.env_cdf_rows, s)) != hipSuccess ||
+            (e = upload(ctx->env_cols, H.env_cdf_cols, s)) != hipSuccess || (e = upload(ctx->env_weights, H.env_row_weights, s)) != hipSuccess)
+            return hip_fail(ctx, e, "envmap upload");
+        H.env.texels = (const uint16_t *)ctx->env_texels.p;
+        H.env.cdf_rows = (const float *)ctx->env_rows.p;
+        H.env.cdf_cols = (const float *)ctx->env_cols.p;
+        H.env.row_weights = (const float *)ctx->env_weights.p;
+        if ((e = ctx->env.ensure(sizeof(MtsgEnv))) != hipSuccess ||
+            (e = hipMemcpyAsync(ctx->env.p, &H.env, sizeof(MtsgEnv), hipMemcpyHostToDevice, s)) != hipSuccess)
+            return hip_fail(ctx, e, "envmap upload");
+        denv = (const MtsgEnv *)ctx->env.p;
+    }
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "scene upload sync");
     MtsgDeviceScene &D = ctx->dscene;
     std::memset(&D, 0, sizeof D);
@@ -177,6 +192,8 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     D.num_emitters = (uint32_t)H.emitters.size();
     D.num_prims = (uint32_t)H.tris.size();
     D.em_norm = H.em_norm;
+    D.env = denv;
+    D.env_emitter = H.env.emitter;
     for (int a = 0; a < 3; ++a) { D.aabb_min[a] = H.aabb_min[a]; D.aabb_max[a] = H.aabb_max[a]; }
     D.cam = H.cam;
     ctx->have_scene = true;
@@ -218,6 +235,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     uint32_t m = 0;
     while ((1u << m) < r) ++m;
     L.resolution = (float)r;
+    L.diff_scale = 1.0f / std::sqrt((float)P->spp);   // integrator.cpp:144-145
     mtsg_sobol_lookup_table(m, L.lut);
     uint64_t scr = P->scramble;
     if (scr) scr = mtsg_sample_tea((uint32_t)scr, (uint32_t)(scr >> 32), 4);   // sobol.cpp:93-101
@@ -375,6 +393,33 @@ int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4) {
     info4[1] = (uint32_t)ctx->host.tris.size();
     info4[2] = ctx->host.bvh_depth;
     info4[3] = (uint32_t)ctx->num_cus;
+    return MTSGPU_OK;
+}
+
+// diagnostics: host-side environment tables (tests/test_host_configure.py)
+int mtsgpu_debug_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
+                            float *rows, float *cols, float *weights) {
+    HostScene H;
+    std::string err;
+    const int rc = mtsg_configure_scene(scene, H, err);
+    if (rc) { g_create_error = err; return rc; }
+    const MtsgEnv &E = H.env;
+    if (E.emitter < 0) { g_create_error = "scene has no environment emitter"; return MTSGPU_EINVAL; }
+    if (params) {
+        std::memset(params, 0, 64 * sizeof(float));
+        params[0] = (float)E.levels; params[1] = (float)E.w0; params[2] = (float)E.h0;
+        params[3] = E.normalization; params[4] = E.pixel_x; params[5] = E.pixel_y; params[6] = E.scale;
+        params[7] = E.center[0]; params[8] = E.center[1]; params[9] = E.center[2]; params[10] = E.radius;
+        params[11] = (float)(H.env_texels.size() / 4);
+        for (int l = 0; l < E.levels && l < MTSG_ENV_MAX_LEVELS; ++l) { params[16 + l] = (float)E.lw[l]; params[34 + l] = (float)E.lh[l]; }
+    }
+    if (texels) {
+        if (texel_cap < H.env_texels.size()) return MTSGPU_EINVAL;
+        std::memcpy(texels, H.env_texels.data(), H.env_texels.size() * sizeof(uint16_t));
+    }
+    if (rows) std::memcpy(rows, H.env_cdf_rows.data(), H.env_cdf_rows.size() * sizeof(float));
+    if (cols) std::memcpy(cols, H.env_cdf_cols.data(), H.env_cdf_cols.size() * sizeof(float));
+    if (weights) std::memcpy(weights, H.env_row_weights.data(), H.env_row_weights.size() * sizeof(float));
     return MTSGPU_OK;
 }
 

@@ -58,6 +58,8 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
     float pad;
 };
 
+enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
+
 struct MtsgShape {
     int32_t bsdf, emitter, has_normals, pad;
 };
@@ -83,6 +85,33 @@ struct MtsgFilter {
     float values[MTSG_FILTER_RES + 1];
 };
 
+// Environment emitter (emitters/envmap.cpp): the reference's TMIPMap<Spectrum,
+// SpectrumHalf> pyramid (render/mipmap.h) with every level stored as RGB halves
+// (+1 pad half: one 8-byte load per texel), levels concatenated; the
+// marginal/conditional luminance CDFs of configure() (envmap.cpp:261-321).
+#define MTSG_ENV_MAX_LEVELS 18      // sides < 65536 (envmap.cpp:160-162)
+#define MTSG_EWA_LUT 64             // MTS_MIPMAP_LUT_SIZE (mipmap.h:37)
+struct MtsgEnv {
+    int32_t emitter;                // index into the emitter list
+    int32_t levels;
+    int32_t w0, h0;
+    float normalization;            // m_normalization
+    float pixel_x, pixel_y;         // m_pixelSize
+    float scale;                    // m_scale
+    float center[3], radius;        // m_sceneBSphere
+    float to_world[9], to_local[9]; // vector part of toWorld and of its inverse
+    float inv_ln2;                  // math::log2 (math.cpp:103-106)
+    float max_aniso;                // 10 (envmap.cpp:142)
+    int32_t lw[MTSG_ENV_MAX_LEVELS], lh[MTSG_ENV_MAX_LEVELS];
+    uint32_t loff[MTSG_ENV_MAX_LEVELS];
+    float ratio_x[MTSG_ENV_MAX_LEVELS], ratio_y[MTSG_ENV_MAX_LEVELS];
+    float lut[MTSG_EWA_LUT];
+    const uint16_t *texels;         // 4 halves per texel
+    const float *cdf_rows;          // h0 + 1
+    const float *cdf_cols;          // h0 * (w0 + 1)
+    const float *row_weights;       // h0
+};
+
 struct MtsgDeviceScene {
     const MtsgNode *nodes;
     const MtsgTri *tris;
@@ -96,8 +125,10 @@ struct MtsgDeviceScene {
     const float *area_cdf;
     const float *em_cdf;        // num_emitters + 1
     const uint32_t *sobol;      // MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE
+    const MtsgEnv *env;         // device copy, or null without an environment emitter
     uint32_t num_emitters, num_prims;
-    float em_norm, pad;
+    float em_norm;
+    int32_t env_emitter;        // index of the environment emitter, -1: none
     float aabb_min[3], aabb_max[3];
     MtsgCamera cam;
 };
@@ -114,6 +145,7 @@ struct MtsgLaunch {
     MtsgFilter filter;
     MtsgLookup lut;
     float resolution;           // sobol m_resolution
+    float diff_scale;           // 1/sqrt(sampleCount): ray differential scale (integrator.cpp:144-145)
     uint32_t scramble;          // sobol m_scramble (after TEA), low 32 bits used by sampleSingle
     uint64_t scramble64;
     uint32_t spp;

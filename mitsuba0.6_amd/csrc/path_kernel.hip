@@ -23,6 +23,7 @@
 #include <type_traits>
 
 #include "dbsdf.h"
+#include "denv.h"
 #include "layout.h"
 
 #define BLOCK 256
@@ -608,7 +609,23 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                     P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
                     vertex = true;
                 } else if (!P.its.valid) {
-                    endPath = true;   // no environment emitter: break before the throughput update
+                    // missed: the environment emitter, if any (path.cpp:233-247)
+                    if (S.env_emitter >= 0 && !(L.hide_emitters && !P.scattered)) {
+                        glb_env *E = (glb_env *)S.env;
+                        const f3 value = env_eval(E, rd);
+                        float nT, fT;
+                        // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
+                        if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
+                            P.thr = mulv(P.thr, P.bsdfWeight);
+                            P.eta *= P.bsdfEta;
+                            float lumPdf = 0;
+                            if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
+                                lumPdf = env_pdf_direction(E, rd) * (S.emitters[S.env_emitter].weight * S.em_norm);
+                            const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                            P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
+                        }
+                    }
+                    endPath = true;   // !its.isValid(): break after the environment term
                 } else {
                     const MtsgShape &sh = S.shapes[P.its.shape];
                     P.thr = mulv(P.thr, P.bsdfWeight);
@@ -647,7 +664,22 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                 if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
                     endPath = true;
                 } else if (!P.its.valid) {
-                    endPath = true;   // camera ray missed, no environment emitter
+                    // camera ray missed: scene->evalEnvironment(ray) with the sensor's ray
+                    // differentials (path.cpp:136-142, perspective.cpp:271-298, integrator.cpp:181)
+                    if (S.env_emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered)) {
+                        const MtsgCamera &cam = S.cam;
+                        const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+                        const f3 rxl = normalize(add(nearP, ld3(cam.dx))), ryl = normalize(add(nearP, ld3(cam.dy)));
+                        const float *W = cam.to_world;
+                        f3 rxd = mk(W[0] * rxl.x + W[1] * rxl.y + W[2] * rxl.z, W[4] * rxl.x + W[5] * rxl.y + W[6] * rxl.z,
+                                    W[8] * rxl.x + W[9] * rxl.y + W[10] * rxl.z);
+                        f3 ryd = mk(W[0] * ryl.x + W[1] * ryl.y + W[2] * ryl.z, W[4] * ryl.x + W[5] * ryl.y + W[6] * ryl.z,
+                                    W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
+                        rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
+                        ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
+                        P.L = add(P.L, mulv(P.thr, env_eval_diff((glb_env *)S.env, rd, rxd, ryd)));
+                    }
+                    endPath = true;
                 } else {
                     const MtsgShape &sh = S.shapes[P.its.shape];
                     const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
@@ -666,6 +698,11 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                             const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
                             if (STATS) cNee++;
                             const MtsgEmitter &e = S.emitters[ei];
+                            f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
+                            float pdf = 0.0f, dist = 0.0f;
+                            if (e.type == MTSG_EMITTER_ENVMAP) {
+                                value = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey, dd, dist, pdf);
+                            } else {
                             // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
                             float py2 = ey;
                             const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
@@ -685,18 +722,18 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                             } else {
                                 ln = normalize(cross(sideA, sideB));
                             }
-                            float pdf = e.inv_area;
+                            pdf = e.inv_area;
                             // Shape::sampleDirect (shape.cpp:102-115)
-                            f3 dd = sub(lp, P.its.p);
+                            dd = sub(lp, P.its.p);
                             const float distSquared = len2(dd);
-                            const float dist = dsqrt(distSquared);
+                            dist = dsqrt(distSquared);
                             dd = divs(dd, dist);
                             const float dp = absdot(dd, ln);
                             pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
                             // AreaLight::sampleDirect (area.cpp:158-173)
-                            f3 value = mk(0, 0, 0);
                             if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
                             else pdf = 0.0f;
+                            }
                             if (pdf != 0) {
                                 // the NEE estimate but for visibility (path.cpp:176-199)
                                 const float dpdf = pdf * emPdf;

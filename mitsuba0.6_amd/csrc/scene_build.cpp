@@ -349,6 +349,252 @@ struct Builder {
     }
 };
 
+// ---- environment emitter (emitters/envmap.cpp, render/mipmap.h) ------------
+// half::half(float) (core/half.h:434-488, libcore/half.cpp:78-200): round to
+// nearest even, overflow to infinity, NaN payload kept
+uint16_t float_to_half(float f) {
+    uint32_t i;
+    std::memcpy(&i, &f, 4);
+    const uint32_t s = (i >> 16) & 0x8000u;
+    int e = (int)((i >> 23) & 0xff) - (127 - 15);
+    uint32_t m = i & 0x7fffffu;
+    if (e <= 0) {
+        if (e < -10) return (uint16_t)s;
+        m |= 0x800000u;
+        const int t = 14 - e;
+        const uint32_t a = (1u << (t - 1)) - 1u, b = (m >> t) & 1u;
+        m = (m + a + b) >> t;
+        return (uint16_t)(s | m);
+    }
+    if (e == 0xff - (127 - 15)) {
+        if (m == 0) return (uint16_t)(s | 0x7c00u);
+        m >>= 13;
+        return (uint16_t)(s | 0x7c00u | m | (m == 0));
+    }
+    m = m + 0xfffu + ((m >> 13) & 1u);
+    if (m & 0x800000u) { m = 0; e += 1; }
+    if (e > 30) return (uint16_t)(s | 0x7c00u);
+    return (uint16_t)(s | ((uint32_t)e << 10) | (m >> 13));
+}
+float half_to_float(uint16_t h) {
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16;
+    uint32_t e = (h >> 10) & 0x1f, m = h & 0x3ffu, bits;
+    if (e == 0) {
+        if (m == 0) bits = s;
+        else {
+            e = 127 - 15 + 1;
+            while (!(m & 0x400u)) { m <<= 1; --e; }
+            bits = s | (e << 23) | ((m & 0x3ffu) << 13);
+        }
+    } else if (e == 31) {
+        bits = s | 0x7f800000u | (m << 13);
+    } else {
+        bits = s | ((e + 127 - 15) << 23) | (m << 13);
+    }
+    float f;
+    std::memcpy(&f, &bits, 4);
+    return f;
+}
+inline float luminance(const float *c) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; }
+
+// LanczosSincFilter::eval with lobes = 2 (rfilters/lanczos.cpp:43-55)
+float lanczos2(float x) {
+    x = std::fabs(x);
+    if (x < 1e-4f) return 1.0f;
+    if (x > 2.0f) return 0.0f;
+    const float x1 = kPi * x;   // M_PI is M_PI_FLT in the SINGLE_PRECISION build (constants.h:80-83)
+    const float x2 = x1 / 2.0f;
+    return (std::sin(x1) * std::sin(x2)) / (x1 * x2);
+}
+
+// Resampler<float> in resampling mode (core/rfilter.h:107-198) +
+// resampleAndClamp(min 0, max inf) (rfilter.h:232-280); repeat or clamp boundary
+struct Resampler1D {
+    int src, dst, taps;
+    bool repeat;
+    std::vector<int> start;
+    std::vector<float> w;
+    Resampler1D(int sourceRes, int targetRes, bool rep) : src(sourceRes), dst(targetRes), repeat(rep) {
+        float filterRadius = 2.0f, scale = 1.0f, invScale = 1.0f;
+        if (targetRes < sourceRes) {
+            scale = (float)sourceRes / (float)targetRes;
+            invScale = 1 / scale;
+            filterRadius *= scale;
+        }
+        taps = (int)std::ceil(filterRadius * 2);
+        start.resize(targetRes);
+        w.resize((size_t)taps * targetRes);
+        for (int i = 0; i < targetRes; i++) {
+            const float center = ((float)i + 0.5f) / (float)targetRes * (float)sourceRes;
+            start[i] = (int)std::floor(center - filterRadius + 0.5f);
+            float sum = 0;
+            for (int j = 0; j < taps; j++) {
+                const float pos = (float)(start[i] + j) + 0.5f - center;
+                const float weight = lanczos2(pos * invScale);
+                w[(size_t)i * taps + j] = weight;
+                sum += weight;
+            }
+            const float normalization = 1.0f / sum;
+            for (int j = 0; j < taps; j++) w[(size_t)i * taps + j] = w[(size_t)i * taps + j] * normalization;
+        }
+    }
+    // source/target: `channels` interleaved floats per sample, sample stride in samples
+    void run(const float *source, size_t sstride, float *target, size_t tstride, int channels) const {
+        for (int i = 0; i < dst; ++i) {
+            for (int ch = 0; ch < channels; ++ch) {
+                float result = 0;
+                for (int j = 0; j < taps; ++j) {
+                    int pos = start[i] + j;
+                    if (pos < 0 || pos >= src) {
+                        if (repeat) { pos %= src; if (pos < 0) pos += src; }
+                        else pos = std::min(std::max(pos, 0), src - 1);
+                    }
+                    result += source[sstride * channels * (size_t)pos + ch] * w[(size_t)i * taps + j];
+                }
+                const float lo = (0.0f < result) ? result : 0.0f;              // std::max(min, result)
+                target[tstride * channels * (size_t)i + ch] = (lo < INFINITY) ? lo : INFINITY;
+            }
+        }
+    }
+};
+
+// Bitmap::resample with the MIP map's lanczos-2 filter, ERepeat (u) / EClamp (v)
+// (libcore/bitmap.cpp:2230-2329): an x pass then a y pass, each only if the size changes
+std::vector<float> resample_level(const std::vector<float> &src, int w, int h, int nw, int nh) {
+    std::vector<float> cur = src;
+    if (w != nw) {
+        Resampler1D r(w, nw, true);
+        std::vector<float> tmp((size_t)nw * h * 3);
+        for (int y = 0; y < h; ++y) r.run(cur.data() + (size_t)y * w * 3, 1, tmp.data() + (size_t)y * nw * 3, 1, 3);
+        cur.swap(tmp);
+    }
+    if (h != nh) {
+        Resampler1D r(h, nh, false);
+        std::vector<float> tmp((size_t)nw * nh * 3);
+        for (int x = 0; x < nw; ++x) r.run(cur.data() + (size_t)x * 3, nw, tmp.data() + (size_t)x * 3, nw, 3);
+        cur.swap(tmp);
+    }
+    return cur;
+}
+
+// EnvironmentMap ctor (envmap.cpp:105-185: TMIPMap with EEWA, anisotropy 10,
+// mipmap.h:155-301) and configure() (envmap.cpp:261-321)
+int build_envmap(const mtsgpu_emitter_desc &e, int index, HostScene &S, std::string &err) {
+    const int W = (int)e.env_width, H = (int)e.env_height;
+    if (!e.env_rgb || W <= 0 || H <= 0) { err = "envmap: missing image data"; return MTSGPU_EINVAL; }
+    if (std::max(W, H) > 0xFFFF) {
+        err = "Environment maps images must be smaller than 65536  pixels in width and height";
+        return MTSGPU_EINVAL;
+    }
+    MtsgEnv &E = S.env;
+    std::memset(&E, 0, sizeof E);
+    E.emitter = index;
+    E.w0 = W; E.h0 = H;
+    E.scale = e.env_scale;
+    E.max_aniso = 10.0f;
+    E.inv_ln2 = 1.0f / std::log(2.0f);
+    // level 0: BlockedArray::init (barray.h:103-126) -> clampNegative if min < 0 (mipmap.h:226-236)
+    std::vector<float> cur(e.env_rgb, e.env_rgb + (size_t)W * H * 3);
+    bool negative = false;
+    for (float x : cur) negative |= x < 0;
+    if (negative)
+        for (float &x : cur) x = (0.0f < x) ? x : 0.0f;
+    S.env_texels.clear();
+    auto quantize = [&](const std::vector<float> &lv, int w, int h, int level) {
+        E.lw[level] = w; E.lh[level] = h;
+        E.loff[level] = (uint32_t)(S.env_texels.size() / 4);
+        E.ratio_x[level] = (float)w / (float)W;
+        E.ratio_y[level] = (float)h / (float)H;
+        for (size_t t = 0; t < (size_t)w * h; ++t) {
+            S.env_texels.push_back(float_to_half(lv[3 * t]));
+            S.env_texels.push_back(float_to_half(lv[3 * t + 1]));
+            S.env_texels.push_back(float_to_half(lv[3 * t + 2]));
+            S.env_texels.push_back(0);
+        }
+    };
+    quantize(cur, W, H, 0);
+    int levels = 1, w = W, h = H;
+    while (w > 1 || h > 1) {   // mipmap.h:241-263
+        const int nw = std::max(1, (w + 1) / 2), nh = std::max(1, (h + 1) / 2);
+        cur = resample_level(cur, w, h, nw, nh);
+        if (levels >= MTSG_ENV_MAX_LEVELS) { err = "envmap: too many MIP levels"; return MTSGPU_EINVAL; }
+        quantize(cur, nw, nh, levels);
+        ++levels;
+        w = nw; h = nh;
+    }
+    E.levels = levels;
+    for (int i = 0; i < MTSG_EWA_LUT; ++i) {   // mipmap.h:296-301
+        const float r2 = (float)i / (float)(MTSG_EWA_LUT - 1);
+        E.lut[i] = (float)std::exp((double)(-2.0f * r2)) - (float)std::exp((double)-2.0f);
+    }
+    // sampling CDFs over sin(theta)-weighted luminance of level 0
+    S.env_cdf_cols.assign((size_t)(W + 1) * H, 0.0f);
+    S.env_cdf_rows.assign((size_t)H + 1, 0.0f);
+    S.env_row_weights.assign((size_t)H, 0.0f);
+    size_t colPos = 0, rowPos = 0;
+    float rowSum = 0.0f;
+    S.env_cdf_rows[rowPos++] = 0;
+    for (int y = 0; y < H; ++y) {
+        float colSum = 0;
+        S.env_cdf_cols[colPos++] = 0;
+        for (int x = 0; x < W; ++x) {
+            const uint16_t *t = &S.env_texels[((size_t)y * W + x) * 4];
+            const float c[3] = {half_to_float(t[0]), half_to_float(t[1]), half_to_float(t[2])};
+            colSum += luminance(c);
+            S.env_cdf_cols[colPos++] = colSum;
+        }
+        const float normalization = 1.0f / colSum;
+        for (int x = 1; x < W; ++x) S.env_cdf_cols[colPos - x - 1] *= normalization;
+        S.env_cdf_cols[colPos - 1] = 1.0f;
+        const float weight = std::sin(((float)y + 0.5f) * kPi / (float)H);
+        S.env_row_weights[y] = weight;
+        rowSum += colSum * weight;
+        S.env_cdf_rows[rowPos++] = rowSum;
+    }
+    const float normalization = 1.0f / rowSum;
+    for (int y = 1; y < H; ++y) S.env_cdf_rows[rowPos - y - 1] *= normalization;
+    S.env_cdf_rows[rowPos - 1] = 1.0f;
+    if (rowSum == 0) { err = "The environment map is completely black -- this is not allowed."; return MTSGPU_EINVAL; }
+    if (!std::isfinite(rowSum)) {
+        err = "The environment map contains an invalid floating point value (nan/inf) -- giving up.";
+        return MTSGPU_EINVAL;
+    }
+    E.normalization = 1.0f / (rowSum * (2 * kPi / (float)W) * (kPi / (float)H));
+    E.pixel_x = 2 * kPi / (float)W;
+    E.pixel_y = kPi / (float)H;
+    // toWorld and the inverse the reference's Transform carries
+    M4 T, Ti;
+    bool haveInv = false;
+    for (int i = 0; i < 16; ++i) {
+        T.m[i / 4][i % 4] = e.env_to_world[i];
+        Ti.m[i / 4][i % 4] = e.env_to_world_inv[i];
+        haveInv |= e.env_to_world_inv[i] != 0.0f;
+    }
+    if (!haveInv && !invert(T, Ti)) { err = "envmap: singular 'toWorld'"; return MTSGPU_EINVAL; }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) { E.to_world[3 * r + c] = T.m[r][c]; E.to_local[3 * r + c] = Ti.m[r][c]; }
+    return MTSGPU_OK;
+}
+
+// EnvironmentMap::createShape (envmap.cpp:331-345) as called by
+// Scene::initializeBidirectional (scene.cpp:385-413): bounding sphere of the
+// kd-tree bounds grown by the sensor position, radius x1.5
+void envmap_bsphere(HostScene &S, const mtsgpu_sensor_desc &sensor) {
+    M4 C;
+    for (int i = 0; i < 16; ++i) C.m[i / 4][i % 4] = sensor.to_world[i];
+    const V cp = xf_point(C, v(0.0f, 0.0f, 0.0f));   // AnimatedTransform::getTranslationBounds (track.cpp:79-83)
+    float mn[3], mx[3];
+    const float p[3] = {cp.x, cp.y, cp.z};
+    for (int a = 0; a < 3; ++a) {
+        mn[a] = fmin_std(S.aabb_min[a], p[a]);
+        mx[a] = fmax_std(S.aabb_max[a], p[a]);
+    }
+    const V center = v((mx[0] + mn[0]) * 0.5f, (mx[1] + mn[1]) * 0.5f, (mx[2] + mn[2]) * 0.5f);
+    const float radius = length(center - v(mx[0], mx[1], mx[2]));
+    S.env.center[0] = center.x; S.env.center[1] = center.y; S.env.center[2] = center.z;
+    S.env.radius = fmax_std(1e-4f, radius * 1.5f);
+}
+
 }  // namespace
 
 // ---- Sobol ------------------------------------------------------------------
@@ -444,6 +690,8 @@ int mtsg_configure_filter(int32_t type, float param, MtsgFilter &f, std::string 
 int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &err) {
     if (!D) { err = "null scene"; return MTSGPU_EINVAL; }
     S = HostScene();
+    std::memset(&S.env, 0, sizeof S.env);
+    S.env.emitter = -1;
     int rc = configure_camera(D->sensor, S.cam, err);
     if (rc) return rc;
     S.film_w = D->sensor.film_width;
@@ -469,7 +717,16 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         o.shape = -1;
         o.weight = e.sampling_weight;
         for (int k = 0; k < 3; ++k) o.radiance[k] = e.radiance[k];
-        if (e.type != MTSGPU_EMITTER_AREA) { err = "only area emitters are supported in this build"; return MTSGPU_EINVAL; }
+        if (e.type == MTSGPU_EMITTER_ENVMAP) {
+            if (S.env.emitter >= 0) {   // scene.cpp:510-513
+                err = "Only one environment emitter can be specified per scene.";
+                return MTSGPU_EINVAL;
+            }
+            if ((rc = build_envmap(e, (int)i, S, err))) return rc;
+        } else if (e.type != MTSGPU_EMITTER_AREA) {
+            err = "unsupported emitter type";
+            return MTSGPU_EINVAL;
+        }
     }
     // meshes
     uint32_t prims = 0, verts = 0;
@@ -669,6 +926,7 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         amax[a] += (amax[a] - amin[a]) * eps + eps;
         S.aabb_min[a] = amin[a]; S.aabb_max[a] = amax[a];
     }
+    if (S.env.emitter >= 0) envmap_bsphere(S, D->sensor);
     // BVH
     Builder B(bp, S.nodes);
     B.order.resize(prims);

@@ -24,6 +24,10 @@ struct HostScene {
     MtsgCamera cam;
     uint32_t film_w = 0, film_h = 0;
     uint32_t bvh_depth = 0;
+    // environment emitter (env.emitter < 0: none); pointers in `env` are set at upload
+    MtsgEnv env;
+    std::vector<uint16_t> env_texels;
+    std::vector<float> env_cdf_rows, env_cdf_cols, env_row_weights;
 };
 
 // Returns MTSGPU_OK or an error code; `err` receives the message.

@@ -87,16 +87,30 @@ class BSDF:
 
 @dataclass
 class Emitter:
+    """`area` (src/emitters/area.cpp) or `envmap` (src/emitters/envmap.cpp).
+
+    envmap: `bitmap` is the decoded lat-long image, (H, W, 3) linear RGB float32
+    (what Bitmap(EAuto, stream) yields for an RGB EXR/PFM/HDR file), `scale` and
+    `toWorld` (a transform.Transform) as in the XML."""
     type: str = 'area'
     radiance: tuple = (1.0, 1.0, 1.0)
     samplingWeight: float = 1.0
+    bitmap: Optional[np.ndarray] = None
+    scale: float = 1.0
+    toWorld: object = None
 
     def to_desc(self):
         d = abi.EmitterDesc()
         d.type = {'area': abi.EMITTER_AREA, 'envmap': abi.EMITTER_ENVMAP}[self.type]
         d.radiance[:] = self.radiance
         d.sampling_weight = self.samplingWeight
-        d.env_scale = 1.0
+        d.env_scale = self.scale
+        if self.toWorld is not None:
+            d.env_to_world[:] = [float(x) for x in np.asarray(self.toWorld.m, np.float32).reshape(-1)]
+            d.env_to_world_inv[:] = [float(x) for x in np.asarray(self.toWorld.inv, np.float32).reshape(-1)]
+        else:
+            d.env_to_world[:] = [float(x) for x in np.eye(4, dtype=np.float32).reshape(-1)]
+            d.env_to_world_inv[:] = [float(x) for x in np.eye(4, dtype=np.float32).reshape(-1)]
         return d
 
 
@@ -181,8 +195,10 @@ class Scene:
         ed = (abi.EmitterDesc * max(1, len(self.emitters)))()
         for i, e in enumerate(self.emitters):
             ed[i] = e.to_desc()
-            if getattr(e, 'env_rgb', None) is not None:
-                img = np.ascontiguousarray(e.env_rgb, np.float32)
+            if e.type == 'envmap':
+                if e.bitmap is None:
+                    raise ValueError('envmap emitter needs a bitmap')
+                img = np.ascontiguousarray(e.bitmap, np.float32)
                 keep.append(img)
                 ed[i].env_rgb = abi.fptr(img)
                 ed[i].env_height, ed[i].env_width = img.shape[0], img.shape[1]

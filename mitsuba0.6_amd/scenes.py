@@ -7,6 +7,7 @@ scene a user would write: per-shape meshes with BSDFs and area emitters.
 import numpy as np
 
 from .scene import BSDF, Emitter, Mesh, PathIntegrator, Scene, Sensor, look_at
+from .transform import Transform
 
 S = 0.01  # classic Cornell box data is in millimetres; scene units are 10 cm
 
@@ -110,9 +111,102 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
     return scene, integ
 
 
+def procedural_envmap(width=1024, height=512, seed=0x5EED):
+    """Deterministic lat-long sky (the 'procedural 1024x512 PFM envmap' of BASELINE.md C3):
+    elevation gradient, warm horizon, dark ground, a small bright sun and three
+    rectangular soft boxes, with mild multiplicative noise.  (H, W, 3) float32."""
+    rng = np.random.default_rng(seed)
+    v = (np.arange(height, dtype=np.float64) + 0.5) / height          # 0 = zenith (envmap.cpp:384-388)
+    u = (np.arange(width, dtype=np.float64) + 0.5) / width
+    theta = v * np.pi
+    phi = u * 2 * np.pi
+    elev = (np.pi / 2 - theta)[:, None] * np.ones((1, width))
+    t = np.clip(elev / (np.pi / 2), -1, 1)
+    sky = np.where(t[..., None] >= 0,
+                   (1 - t[..., None]) * np.array([1.2, 1.05, 0.9]) + t[..., None] * np.array([0.25, 0.45, 1.0]),
+                   np.array([0.18, 0.16, 0.13]) * (1 + 0.5 * t[..., None]))
+    # sun: 3 degree disk at elevation 35, azimuth 60 (radiance 400)
+    sd = np.array([np.cos(np.radians(35)) * np.sin(np.radians(60)), np.sin(np.radians(35)),
+                   -np.cos(np.radians(35)) * np.cos(np.radians(60))])
+    st, sp = np.sin(theta)[:, None], phi[None, :]
+    dirs = np.stack([np.sin(sp) * st, np.cos(theta)[:, None] * np.ones_like(sp), -np.cos(sp) * st], -1)
+    cosang = dirs @ sd
+    sky = sky + (cosang > np.cos(np.radians(3.0)))[..., None] * np.array([400.0, 380.0, 330.0])
+    # soft boxes
+    for (u0, u1, v0, v1, rad) in ((0.05, 0.12, 0.30, 0.40, 12.0), (0.55, 0.70, 0.20, 0.28, 8.0),
+                                  (0.80, 0.84, 0.35, 0.47, 15.0)):
+        uu, vv = u[None, :], v[:, None]
+        box = (uu >= u0) & (uu < u1) & (vv >= v0) & (vv < v1)
+        sky = sky + box[..., None] * rad
+    sky = sky * rng.uniform(0.9, 1.1, size=(height, width, 1))
+    return sky.astype(np.float32)
+
+
+def blob_mesh(nu=236, nv=148, radius=1.0, center=(0.0, 1.0, 0.0)):
+    """Procedural stand-in for data/tests/bunny.ply (~69k triangles, closed,
+    smooth vertex normals left to computeNormals): a displaced UV sphere."""
+    th = np.linspace(0, np.pi, nv)
+    ph = np.linspace(0, 2 * np.pi, nu, endpoint=False)
+    T, P = np.meshgrid(th, ph, indexing='ij')
+    r = radius * (1 + 0.12 * np.sin(5 * T) * np.sin(4 * P) + 0.05 * np.cos(9 * P + 3 * T))
+    pos = np.stack([r * np.sin(T) * np.cos(P), r * np.cos(T), r * np.sin(T) * np.sin(P)], -1).reshape(-1, 3)
+    pos = (pos + np.asarray(center)).astype(np.float32)
+    idx = []
+    for i in range(nv - 1):
+        for j in range(nu):
+            a, b = i * nu + j, i * nu + (j + 1) % nu
+            c, d = (i + 1) * nu + j, (i + 1) * nu + (j + 1) % nu
+            if i > 0:
+                idx.append((a, b, d))
+            if i < nv - 2:
+                idx.append((a, d, c))
+    return pos, np.asarray(idx, np.uint32)
+
+
+def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env_size=(1024, 512),
+               blob=(236, 148), area_light=False, env_weight=1.0):
+    """Config C3: a ~69k-triangle object in roughconductor GGX alpha=0.1 (copper) on a
+    diffuse checker ground, lit only by a 1024x512 environment map."""
+    cu = BSDF('roughconductor', distribution='ggx', alpha=0.1, material=None, eta=CU_ETA, k=CU_K)
+    g0 = BSDF('diffuse', reflectance=(0.4, 0.4, 0.4))
+    g1 = BSDF('diffuse', reflectance=(0.15, 0.15, 0.15))
+    bsdfs = [cu, g0, g1]
+    meshes = []
+    p, i = blob_mesh(*blob)
+    meshes.append(Mesh(p, i, bsdf=0, name='object'))
+    # 12x12 checker of quads, y = 0 (two meshes, one per colour)
+    n, half = 12, 6.0
+    for col in (0, 1):
+        pos, idx = [], []
+        for a in range(n):
+            for b in range(n):
+                if (a + b) % 2 != col:
+                    continue
+                x0, z0 = -half + a * (2 * half / n), -half + b * (2 * half / n)
+                x1, z1 = x0 + 2 * half / n, z0 + 2 * half / n
+                base = len(pos)
+                pos += [(x0, 0, z0), (x0, 0, z1), (x1, 0, z1), (x1, 0, z0)]
+                idx += [(base, base + 1, base + 2), (base, base + 2, base + 3)]
+        meshes.append(Mesh(np.asarray(pos, np.float32), np.asarray(idx, np.uint32), bsdf=1 + col,
+                           faceNormals=True, name='ground%d' % col))
+    env = Emitter('envmap', bitmap=procedural_envmap(*env_size), scale=1.0, samplingWeight=env_weight,
+                  toWorld=Transform().rotate((0, 1, 0), 30.0))
+    emitters = [env]
+    if area_light:   # parity coverage: an area light next to the environment (emitter PDF over both)
+        meshes.append(Mesh(np.array([(-1, 3.5, -1), (1, 3.5, -1), (1, 3.5, 1), (-1, 3.5, 1)], np.float32),
+                           np.array([(0, 1, 2), (0, 2, 3)], np.uint32), emitter=1, faceNormals=True, name='lamp'))
+        emitters.append(Emitter('area', radiance=(6.0, 6.0, 5.0)))
+    cam = Transform.look_at_((0.0, 2.6, 7.6), (0.0, 0.9, 0.0), (0, 1, 0)).m
+    sensor = Sensor(fov=35.0, fovAxis='x', nearClip=0.01, farClip=100.0, toWorld=cam, width=width, height=height)
+    scene = Scene(sensor, meshes, bsdfs, emitters, name='matpreview')
+    integ = PathIntegrator(maxDepth=max_depth, rrDepth=5, sampleCount=spp, rfilter=rfilter, rfilterParam=0.5)
+    return scene, integ
+
+
 CONFIGS = {
     'C1': dict(builder='cornell_box', width=512, height=512, spp=64),
     'C2': dict(builder='cornell_box', width=1280, height=720, spp=512),
+    'C3': dict(builder='matpreview', width=1280, height=720, spp=512),
 }
 
 

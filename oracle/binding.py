@@ -12,9 +12,21 @@ LIB = os.path.join(HERE, '_build', 'liboracle.so')
 _lib = None
 
 
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    srcs = [os.path.join(HERE, f) for f in ('mts_oracle.c', 'mts_oracle.h', 'Makefile')]
+    srcs.append(os.path.join(os.path.dirname(HERE), 'include', 'mtsgpu.h'))
+    return any(os.path.getmtime(f) > t for f in srcs if os.path.exists(f))
+
+
 def lib():
     global _lib
     if _lib is None:
+        if _stale():   # a stale checker silently compares against old semantics: rebuild it
+            import subprocess
+            subprocess.run(['make', '-s', '-C', HERE], check=True)
         import sys
         sys.path.insert(0, os.path.dirname(HERE))
         from pkgimport import mitsuba_amd

@@ -1092,6 +1092,360 @@ static inline int triaccel_intersect(const TriAccel *ta, const Ray *ray, float m
 /* ------------------------------------------------------------------------ */
 /* scene (configure): meshes, emitters, acceleration                          */
 /* ------------------------------------------------------------------------ */
+/* ------------------------------------------------------------------------ */
+/* environment emitter (emitters/envmap.cpp) and its MIP map                  */
+/* (render/mipmap.h, core/rfilter.h Resampler, rfilters/lanczos.cpp)          */
+/* ------------------------------------------------------------------------ */
+#define ENV_MAX_LEVELS 18
+#define EWA_LUT 64 /* MTS_MIPMAP_LUT_SIZE, mipmap.h:37 */
+
+typedef struct Env {
+    int levels, w0, h0;
+    int lw[ENV_MAX_LEVELS], lh[ENV_MAX_LEVELS];
+    float ratioX[ENV_MAX_LEVELS], ratioY[ENV_MAX_LEVELS];
+    uint16_t *lv[ENV_MAX_LEVELS]; /* RGB halves per texel (SpectrumHalf) */
+    float *cdfRows, *cdfCols, *rowWeights;
+    float normalization, pixelX, pixelY, scale;
+    V3 center; float radius;
+    M4 toWorld, toLocal;
+    float lut[EWA_LUT];
+    float maxAniso;
+} Env;
+
+/* half::half(float) (core/half.h:434-488, libcore/half.cpp:78-200) */
+static uint16_t o_float_to_half(float f) {
+    uint32_t i; memcpy(&i, &f, 4);
+    const int s = (i >> 16) & 0x00008000;
+    int e = ((i >> 23) & 0x000000ff) - (127 - 15);
+    int m = i & 0x007fffff;
+    if (e <= 0) {
+        if (e < -10) return (uint16_t)s;
+        m = m | 0x00800000;
+        int t = 14 - e;
+        int a = (1 << (t - 1)) - 1;
+        int b = (m >> t) & 1;
+        m = (m + a + b) >> t;
+        return (uint16_t)(s | m);
+    } else if (e == 0xff - (127 - 15)) {
+        if (m == 0) return (uint16_t)(s | 0x7c00);
+        m >>= 13;
+        return (uint16_t)(s | 0x7c00 | m | (m == 0));
+    } else {
+        m = m + 0x00000fff + ((m >> 13) & 1);
+        if (m & 0x00800000) { m = 0; e += 1; }
+        if (e > 30) return (uint16_t)(s | 0x7c00);
+        return (uint16_t)(s | (e << 10) | (m >> 13));
+    }
+}
+/* half::operator float (exact) */
+static float o_half_to_float(uint16_t h) {
+    int s = (h >> 15) & 1, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    float r;
+    if (e == 0) r = ldexpf((float)m, -24);
+    else if (e == 31) r = m ? NAN : INFINITY;
+    else r = ldexpf((float)(m | 0x400), e - 25);
+    return s ? -r : r;
+}
+static inline float lum3(V3 c) { return c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f; } /* spectrum.h:638-640 */
+
+/* LanczosSincFilter::eval, lobes = 2 (lanczos.cpp:43-55); glibc sinf as the reference */
+static float lanczos2(float x) {
+    x = fabsf(x);
+    if (x < EPSILON) return 1.0f;
+    else if (x > 2.0f) return 0.0f;
+    float x1 = M_PI_F * x; /* M_PI = M_PI_FLT under SINGLE_PRECISION (constants.h:80-83) */
+    float x2 = x1 / 2.0f;
+    return (sinf(x1) * sinf(x2)) / (x1 * x2);
+}
+
+/* one pass of Bitmap::resample (bitmap.cpp:2258-2329) with Resampler<float>
+   (rfilter.h:123-198) and resampleAndClamp(0, +inf) (rfilter.h:232-280) */
+static void resample_pass(const float *src, int srcRes, size_t sStride, float *dst, int dstRes, size_t tStride,
+                          int nlines, size_t sLine, size_t tLine, int repeat) {
+    float filterRadius = 2.0f, scale = 1.0f, invScale = 1.0f;
+    if (dstRes < srcRes) { scale = (float)srcRes / (float)dstRes; invScale = 1 / scale; filterRadius *= scale; }
+    int taps = (int)ceilf(filterRadius * 2);
+    int *start = (int *)malloc(sizeof(int) * dstRes);
+    float *w = (float *)malloc(sizeof(float) * (size_t)taps * dstRes);
+    for (int i = 0; i < dstRes; i++) {
+        float center = (i + 0.5f) / dstRes * srcRes;
+        start[i] = (int)floorf(center - filterRadius + 0.5f);
+        float sum = 0;
+        for (int j = 0; j < taps; j++) {
+            float pos = start[i] + j + 0.5f - center;
+            float weight = lanczos2(pos * invScale);
+            w[i * taps + j] = weight;
+            sum += weight;
+        }
+        float normalization = 1.0f / sum;
+        for (int j = 0; j < taps; j++) w[i * taps + j] = w[i * taps + j] * normalization;
+    }
+    for (int line = 0; line < nlines; ++line) {
+        const float *s = src + line * sLine;
+        float *t = dst + line * tLine;
+        for (int i = 0; i < dstRes; ++i)
+            for (int ch = 0; ch < 3; ++ch) {
+                float result = 0;
+                for (int j = 0; j < taps; ++j) {
+                    int pos = start[i] + j;
+                    if (pos < 0 || pos >= srcRes) {
+                        if (repeat) { pos = pos % srcRes; if (pos < 0) pos += srcRes; }
+                        else pos = pos < 0 ? 0 : (pos > srcRes - 1 ? srcRes - 1 : pos);
+                    }
+                    result += s[sStride * 3 * pos + ch] * w[i * taps + j];
+                }
+                float r = smax(0.0f, result);
+                t[tStride * 3 * i + ch] = smin(INFINITY, r);
+            }
+    }
+    free(start); free(w);
+}
+
+static void env_free(Env *E) {
+    for (int l = 0; l < ENV_MAX_LEVELS; ++l) free(E->lv[l]);
+    free(E->cdfRows); free(E->cdfCols); free(E->rowWeights);
+}
+
+static V3 env_texel(const Env *E, int level, int x, int y) { /* evalTexel, mipmap.h:427-490 */
+    int w = E->lw[level], h = E->lh[level];
+    if (x < 0 || x >= w) { x = x % w; if (x < 0) x += w; }          /* ERepeat */
+    if (y < 0 || y >= h) y = y < 0 ? 0 : (y > h - 1 ? h - 1 : y);   /* EClamp */
+    const uint16_t *t = E->lv[level] + 3 * ((size_t)y * w + x);
+    return v3(o_half_to_float(t[0]), o_half_to_float(t[1]), o_half_to_float(t[2]));
+}
+
+/* EnvironmentMap ctor + configure (envmap.cpp:105-185,261-321), TMIPMap ctor (mipmap.h:155-301) */
+static int env_configure(const mtsgpu_emitter_desc *e, Env *E) {
+    memset(E, 0, sizeof *E);
+    int W = (int)e->env_width, H = (int)e->env_height;
+    if (!e->env_rgb || W <= 0 || H <= 0 || W > 0xFFFF || H > 0xFFFF) return MTSGPU_EINVAL;
+    E->w0 = W; E->h0 = H; E->scale = e->env_scale; E->maxAniso = 10.0f;
+    size_t n = (size_t)W * H * 3;
+    float *cur = (float *)malloc(sizeof(float) * n);
+    memcpy(cur, e->env_rgb, sizeof(float) * n);
+    float mn = INFINITY;
+    for (size_t i = 0; i < n; ++i) mn = smin(mn, cur[i]);
+    if (mn < 0) for (size_t i = 0; i < n; ++i) cur[i] = smax(0.0f, cur[i]);   /* clampNegative */
+    int w = W, h = H, level = 0;
+    for (;;) {
+        E->lw[level] = w; E->lh[level] = h;
+        E->ratioX[level] = (float)w / (float)W; E->ratioY[level] = (float)h / (float)H;
+        E->lv[level] = (uint16_t *)malloc(sizeof(uint16_t) * 3 * (size_t)w * h);
+        for (size_t i = 0; i < (size_t)w * h * 3; ++i) E->lv[level][i] = o_float_to_half(cur[i]);
+        ++level;
+        if (!(w > 1 || h > 1)) break;
+        if (level >= ENV_MAX_LEVELS) { free(cur); return MTSGPU_EINVAL; }
+        int nw = (w + 1) / 2, nh = (h + 1) / 2;   /* std::max(1, (size + 1) / 2) */
+        if (nw < 1) nw = 1;
+        if (nh < 1) nh = 1;
+        float *tmp = cur;
+        if (nw != w) {
+            float *t = (float *)malloc(sizeof(float) * 3 * (size_t)nw * h);
+            resample_pass(tmp, w, 1, t, nw, 1, h, (size_t)w * 3, (size_t)nw * 3, 1);
+            free(tmp); tmp = t;
+        }
+        if (nh != h) {
+            float *t = (float *)malloc(sizeof(float) * 3 * (size_t)nw * nh);
+            resample_pass(tmp, h, nw, t, nh, nw, nw, 3, 3, 0);
+            free(tmp); tmp = t;
+        }
+        cur = tmp; w = nw; h = nh;
+    }
+    free(cur);
+    E->levels = level;
+    for (int i = 0; i < EWA_LUT; ++i) {
+        float r2 = (float)i / (float)(EWA_LUT - 1);
+        E->lut[i] = o_fastexp(-2.0f * r2) - o_fastexp(-2.0f);
+    }
+    E->cdfCols = (float *)malloc(sizeof(float) * (size_t)(W + 1) * H);
+    E->cdfRows = (float *)malloc(sizeof(float) * (H + 1));
+    E->rowWeights = (float *)malloc(sizeof(float) * H);
+    size_t colPos = 0, rowPos = 0;
+    float rowSum = 0.0f;
+    E->cdfRows[rowPos++] = 0;
+    for (int y = 0; y < H; ++y) {
+        float colSum = 0;
+        E->cdfCols[colPos++] = 0;
+        for (int x = 0; x < W; ++x) {
+            colSum += lum3(env_texel(E, 0, x, y));
+            E->cdfCols[colPos++] = colSum;
+        }
+        float normalization = 1.0f / colSum;
+        for (int x = 1; x < W; ++x) E->cdfCols[colPos - x - 1] *= normalization;
+        E->cdfCols[colPos - 1] = 1.0f;
+        float weight = sinf((y + 0.5f) * M_PI_F / H);
+        E->rowWeights[y] = weight;
+        rowSum += colSum * weight;
+        E->cdfRows[rowPos++] = rowSum;
+    }
+    float normalization = 1.0f / rowSum;
+    for (int y = 1; y < H; ++y) E->cdfRows[rowPos - y - 1] *= normalization;
+    E->cdfRows[rowPos - 1] = 1.0f;
+    if (rowSum == 0 || !isfinite(rowSum)) return MTSGPU_EINVAL;
+    E->normalization = 1.0f / (rowSum * (2 * M_PI_F / W) * (M_PI_F / H));
+    E->pixelX = 2 * M_PI_F / W;
+    E->pixelY = M_PI_F / H;
+    int haveInv = 0;
+    for (int i = 0; i < 16; ++i) {
+        E->toWorld.m[i / 4][i % 4] = e->env_to_world[i];
+        E->toLocal.m[i / 4][i % 4] = e->env_to_world_inv[i];
+        haveInv |= e->env_to_world_inv[i] != 0.0f;
+    }
+    if (!haveInv && !m4_invert(&E->toWorld, &E->toLocal)) return MTSGPU_EINVAL;
+    return MTSGPU_OK;
+}
+
+static V3 env_eval_box(const Env *E, int level, float u, float v) { /* mipmap.h:493-497 */
+    return env_texel(E, level, (int)floorf(u * E->lw[level]), (int)floorf(v * E->lh[level]));
+}
+static V3 env_eval_bilinear(const Env *E, int level, float uvx, float uvy) { /* mipmap.h:500-522 */
+    if (!isfinite(uvx) || !isfinite(uvy)) return v3(0, 0, 0);
+    if (level >= E->levels) return env_eval_box(E, E->levels - 1, uvx, uvy);
+    float u = uvx * E->lw[level] - 0.5f, v = uvy * E->lh[level] - 0.5f;
+    int xPos = (int)floorf(u), yPos = (int)floorf(v);
+    float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+    V3 r = vmul(vmul(env_texel(E, level, xPos, yPos), dx2), dy2);
+    r = vadd(r, vmul(vmul(env_texel(E, level, xPos, yPos + 1), dx2), dy1));
+    r = vadd(r, vmul(vmul(env_texel(E, level, xPos + 1, yPos), dx1), dy2));
+    r = vadd(r, vmul(vmul(env_texel(E, level, xPos + 1, yPos + 1), dx1), dy1));
+    return r;
+}
+static V3 env_eval_ewa(const Env *E, int level, float uvx, float uvy, float A, float B, float C) { /* mipmap.h:760-836 */
+    if (!isfinite(A + B + C + uvx + uvy)) return v3(0, 0, 0);
+    if (level >= E->levels) return env_eval_box(E, E->levels - 1, uvx, uvy);
+    float u = uvx * E->lw[level] - 0.5f;
+    float v = uvy * E->lh[level] - 0.5f;
+    A /= E->ratioX[level] * E->ratioX[level];
+    B /= E->ratioX[level] * E->ratioY[level];
+    C /= E->ratioY[level] * E->ratioY[level];
+    float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * sqrtf(C * invDet), deltaV = 2.0f * sqrtf(A * invDet);
+    int u0 = (int)ceilf(u - deltaU), u1 = (int)floorf(u + deltaU);
+    int v0 = (int)ceilf(v - deltaV), v1 = (int)floorf(v + deltaV);
+    float As = A * EWA_LUT, Bs = B * EWA_LUT, Cs = C * EWA_LUT;
+    V3 result = v3(0, 0, 0);
+    float denominator = 0.0f;
+    float ddq = 2 * As, uu0 = (float)u0 - u;
+    for (int vt = v0; vt <= v1; ++vt) {
+        const float vv = (float)vt - v;
+        float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+        float dq = As * (2 * uu0 + 1) + Bs * vv;
+        for (int ut = u0; ut <= u1; ++ut) {
+            if (q < (float)EWA_LUT) {
+                uint32_t qi = (uint32_t)(long long)q;
+                if (qi < EWA_LUT) {
+                    const float weight = E->lut[(int)q];
+                    result = vadd(result, vmul(env_texel(E, level, ut, vt), weight));
+                    denominator += weight;
+                }
+            }
+            q += dq;
+            dq += ddq;
+        }
+    }
+    if (denominator == 0) return env_eval_bilinear(E, level, uvx, uvy);
+    return vdiv(result, denominator);
+}
+static float o_hypot2(float a, float b) { /* math.cpp:74-86 */
+    float r;
+    if (fabsf(a) > fabsf(b)) { r = b / a; r = fabsf(a) * sqrtf(1.0f + r * r); }
+    else if (b != 0.0f) { r = a / b; r = fabsf(b) * sqrtf(1.0f + r * r); }
+    else r = 0.0f;
+    return r;
+}
+static inline float o_log2(float v) { /* math.cpp:103-106 */
+    const float invLn2 = 1.0f / logf(2.0f);
+    return o_fastlog(v) * invLn2;
+}
+static V3 env_eval_filtered(const Env *E, float uvx, float uvy, float d0x, float d0y, float d1x, float d1y) { /* mipmap.h:560-660 */
+    float du0 = d0x * E->w0, dv0 = d0y * E->h0, du1 = d1x * E->w0, dv1 = d1y * E->h0;
+    float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1, F = A * C - B * B * 0.25f;
+    float root = o_hypot2(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
+    float majorRadius = Aprime != 0 ? sqrtf(F / Aprime) : 0, minorRadius = Cprime != 0 ? sqrtf(F / Cprime) : 0;
+    if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
+        float level = o_log2(smax(majorRadius, EPSILON));
+        int ilevel = (int)floorf(level);
+        if (ilevel < 0) return env_eval_bilinear(E, 0, uvx, uvy);
+        float a = level - ilevel;
+        return vadd(vmul(env_eval_bilinear(E, ilevel, uvx, uvy), 1.0f - a), vmul(env_eval_bilinear(E, ilevel + 1, uvx, uvy), a));
+    }
+    if (minorRadius * E->maxAniso < majorRadius) {
+        minorRadius = majorRadius / E->maxAniso;
+        float theta = 0.5f * o_atan(B / (A - C)), sinTheta, cosTheta;
+        o_sincos(theta, &sinTheta, &cosTheta);
+        float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
+              cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
+        A = a2 * cosTheta2 + b2 * sinTheta2;
+        B = (a2 - b2) * sin2Theta;
+        C = a2 * sinTheta2 + b2 * cosTheta2;
+        F = a2 * b2;
+    }
+    float scale = 1.0f / F;
+    A *= scale; B *= scale; C *= scale;
+    float level = smax(0.0f, o_log2(minorRadius));
+    int ilevel = (int)level;
+    float a = level - ilevel;
+    if (majorRadius < 1 || !(A > 0 && C > 0)) return env_eval_bilinear(E, ilevel, uvx, uvy);
+    return vadd(vmul(env_eval_ewa(E, ilevel, uvx, uvy, A, B, C), 1.0f - a), vmul(env_eval_ewa(E, ilevel + 1, uvx, uvy, A, B, C), a));
+}
+static inline float safe_acosf(float v) { return o_acos(smin(1.0f, smax(-1.0f, v))); } /* math.h:250-252 */
+
+/* EnvironmentMap::evalEnvironment (envmap.cpp:380-410) */
+static V3 env_eval(const Env *E, const Ray *ray) {
+    V3 v = xf_vector(&E->toLocal, ray->d);
+    float uvx = o_atan2(v.x, -v.z) * INV_TWOPI_F, uvy = safe_acosf(v.y) * INV_PI_F;
+    V3 value;
+    if (!ray->hasDiff) {
+        value = env_eval_bilinear(E, 0, uvx, uvy);
+    } else {
+        V3 dvdx = vsub(xf_vector(&E->toLocal, ray->rxD), v), dvdy = vsub(xf_vector(&E->toLocal, ray->ryD), v);
+        float t1 = INV_TWOPI_F / (v.x * v.x + v.z * v.z), t2 = -INV_PI_F / smax(safe_sqrt(1.0f - v.y * v.y), EPSILON);
+        value = env_eval_filtered(E, uvx, uvy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y,
+                                  t1 * (dvdy.z * v.x - dvdy.x * v.z), t2 * dvdy.y);
+    }
+    return vmul(value, E->scale);
+}
+
+/* solveQuadratic (util.cpp:447-485), BSphere::rayIntersect (bsphere.h:88-95) */
+static int solve_quadratic(float a, float b, float c, float *x0, float *x1) {
+    if (a == 0) {
+        if (b != 0) { *x0 = *x1 = -c / b; return 1; }
+        return 0;
+    }
+    float discrim = b * b - 4.0f * a * c;
+    if (discrim < 0) return 0;
+    float temp, sqrtDiscrim = sqrtf(discrim);
+    if (b < 0) temp = -0.5f * (b - sqrtDiscrim);
+    else temp = -0.5f * (b + sqrtDiscrim);
+    *x0 = temp / a;
+    *x1 = c / temp;
+    if (*x0 > *x1) { float t = *x0; *x0 = *x1; *x1 = t; }
+    return 1;
+}
+static int env_bsphere(const Env *E, V3 ro, V3 d, float *nearT, float *farT) {
+    V3 o = vsub(ro, E->center);
+    float A = vlen2(d), B = 2 * vdot(o, d), C = vlen2(o) - E->radius * E->radius;
+    return solve_quadratic(A, B, C, nearT, farT);
+}
+
+/* sampleReuse over the envmap CDFs (envmap.cpp:687-692) */
+static uint32_t env_sample_reuse(const float *cdf, uint32_t size, float *sample) {
+    uint32_t lo = 0, hi = size + 1;
+    while (lo < hi) { uint32_t mid = (lo + hi) / 2; if (cdf[mid] < *sample) lo = mid + 1; else hi = mid; }
+    long e = (long)lo - 1;
+    uint32_t index = (uint32_t)(e < 0 ? 0 : e);
+    if (index > size - 1) index = size - 1;
+    *sample = (*sample - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return index;
+}
+static float interval_to_tent(float sample) { /* warp.cpp:143-155 */
+    float sign;
+    if (sample < 0.5f) { sign = 1; sample *= 2; }
+    else { sign = -1; sample = 2 * (sample - 0.5f); }
+    return sign * (1 - sqrtf(sample));
+}
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+
 typedef struct {
     V3 *pos, *nrm;        /* nrm NULL: face normals */
     float *uv;
@@ -1117,6 +1471,7 @@ typedef struct {
     float aabbMin[3], aabbMax[3];
     Camera cam;
     int envIndex;
+    Env *env;
 } Scene;
 
 /* unitAngle (core/util.h:309-314) -- uses float asin */
@@ -1272,6 +1627,7 @@ static void scene_free(Scene *S) {
     }
     free(S->meshes); free(S->bsdfs); free(S->emitters); free(S->emCdf);
     free(S->ta); free(S->taMesh); free(S->taTri); free(S->nodes); free(S->order);
+    if (S->env) { env_free(S->env); free(S->env); }
     memset(S, 0, sizeof *S);
 }
 
@@ -1299,7 +1655,14 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
         S->emitters[i].radiance = v3(e->radiance[0], e->radiance[1], e->radiance[2]);
         S->emitters[i].weight = e->sampling_weight;
         S->emitters[i].mesh = -1;
-        if (e->type != MTSGPU_EMITTER_AREA) return MTSGPU_EINVAL; /* envmap: next row */
+        if (e->type == MTSGPU_EMITTER_ENVMAP) {
+            if (S->env) return MTSGPU_EINVAL; /* one environment emitter per scene (scene.cpp:510-513) */
+            S->env = (Env *)calloc(1, sizeof(Env));
+            S->envIndex = (int)i;
+            if ((rc = env_configure(e, S->env))) return rc;
+        } else if (e->type != MTSGPU_EMITTER_AREA) {
+            return MTSGPU_EINVAL;
+        }
     }
     if (D->num_emitters == 0) return MTSGPU_EINVAL; /* sunsky fallback is out of scope */
 
@@ -1382,6 +1745,14 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
         amin[a] -= (amax[a] - amin[a]) * eps + eps;
         amax[a] += (amax[a] - amin[a]) * eps + eps;
         S->aabbMin[a] = amin[a]; S->aabbMax[a] = amax[a];
+    }
+    if (S->env) { /* EnvironmentMap::createShape (envmap.cpp:331-345) via scene.cpp:385-413 */
+        V3 cp = xf_point(&S->cam.toWorld, v3(0.0f, 0.0f, 0.0f));
+        float mn[3], mx[3];
+        for (int a = 0; a < 3; ++a) { mn[a] = smin(S->aabbMin[a], vget(cp, a)); mx[a] = smax(S->aabbMax[a], vget(cp, a)); }
+        V3 mxv = v3(mx[0], mx[1], mx[2]);
+        S->env->center = vmul(vadd(mxv, v3(mn[0], mn[1], mn[2])), 0.5f);
+        S->env->radius = smax(EPSILON, vlen(vsub(S->env->center, mxv)) * 1.5f);
     }
     S->order = (uint32_t *)malloc(sizeof(uint32_t) * prims);
     for (uint32_t i = 0; i < prims; ++i) S->order[i] = i;
@@ -1551,6 +1922,53 @@ typedef struct {
     int emitter;
 } DRec;
 
+/* EnvironmentMap::sampleDirect (envmap.cpp:516-543) + internalSampleDirection (:567-603) */
+static V3 env_sample_direct(const Env *E, DRec *dRec, float sx, float sy) {
+    uint32_t row = env_sample_reuse(E->cdfRows, (uint32_t)E->h0, &sy);
+    uint32_t col = env_sample_reuse(E->cdfCols + (size_t)row * (E->w0 + 1), (uint32_t)E->w0, &sx);
+    float posx = (float)col + interval_to_tent(sx), posy = (float)row + interval_to_tent(sy);
+    int xPos = (int)floorf(posx), yPos = (int)floorf(posy);
+    float dx1 = posx - xPos, dx2 = 1.0f - dx1, dy1 = posy - yPos, dy2 = 1.0f - dy1;
+    V3 value1 = vadd(vmul(vmul(env_texel(E, 0, xPos, yPos), dx2), dy2), vmul(vmul(env_texel(E, 0, xPos + 1, yPos), dx1), dy2));
+    V3 value2 = vadd(vmul(vmul(env_texel(E, 0, xPos, yPos + 1), dx2), dy1), vmul(vmul(env_texel(E, 0, xPos + 1, yPos + 1), dx1), dy1));
+    V3 value = vmul(vadd(value1, value2), E->scale);
+    float pdf = (lum3(value1) * E->rowWeights[clampi(yPos, 0, E->h0 - 1)] +
+                 lum3(value2) * E->rowWeights[clampi(yPos + 1, 0, E->h0 - 1)]) * E->normalization;
+    float sinPhi, cosPhi, sinTheta, cosTheta;
+    o_sincos(E->pixelX * (posx + 0.5f), &sinPhi, &cosPhi);
+    o_sincos(E->pixelY * (posy + 0.5f), &sinTheta, &cosTheta);
+    V3 d = v3(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
+    pdf /= smax(fabsf(sinTheta), EPSILON);
+    V3 dw = xf_vector(&E->toWorld, d);
+    float nearT, farT;
+    if (vzero(value) || pdf == 0 || !env_bsphere(E, dRec->ref, dw, &nearT, &farT) || nearT >= 0 || farT <= 0) {
+        dRec->pdf = 0.0f;
+        return v3(0, 0, 0);
+    }
+    dRec->pdf = pdf;
+    dRec->p = vadd(dRec->ref, vmul(dw, farT));
+    dRec->n = vnormalize(vsub(E->center, dRec->p));
+    dRec->dist = farT;
+    dRec->d = dw;
+    dRec->measureSolidAngle = 1;
+    return vdiv(value, pdf);
+}
+
+/* internalPdfDirection (envmap.cpp:606-633), called with trafo.inverse()(d) by pdfDirect (:545-556) */
+static float env_pdf_direction(const Env *E, V3 dw) {
+    V3 d = xf_vector(&E->toLocal, dw);
+    float uvx = o_atan2(d.x, -d.z) * INV_TWOPI_F, uvy = safe_acosf(d.y) * INV_PI_F;
+    if (!isfinite(uvx) || !isfinite(uvy)) return 0.0f;
+    float u = uvx * E->w0 - 0.5f, v = uvy * E->h0 - 0.5f;
+    int xPos = (int)floorf(u), yPos = (int)floorf(v);
+    float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+    V3 value1 = vadd(vmul(vmul(env_texel(E, 0, xPos, yPos), dx2), dy2), vmul(vmul(env_texel(E, 0, xPos + 1, yPos), dx1), dy2));
+    V3 value2 = vadd(vmul(vmul(env_texel(E, 0, xPos, yPos + 1), dx2), dy1), vmul(vmul(env_texel(E, 0, xPos + 1, yPos + 1), dx1), dy1));
+    float sinTheta = safe_sqrt(1 - d.y * d.y);
+    return (lum3(value1) * E->rowWeights[clampi(yPos, 0, E->h0 - 1)] + lum3(value2) * E->rowWeights[clampi(yPos + 1, 0, E->h0 - 1)])
+           * E->normalization / smax(fabsf(sinTheta), EPSILON);
+}
+
 /* AreaLight::eval (area.cpp:104-109) */
 static V3 its_Le(const Scene *S, const Its *its, V3 d) {
     const Emitter *e = &S->emitters[S->meshes[its->mesh].emitter];
@@ -1566,6 +1984,10 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
     float emPdf;
     uint32_t index = dd_sample_reuse(S->emCdf, S->nemitters, &sx, &emPdf);
     const Emitter *e = &S->emitters[index];
+    V3 value;
+    if (e->type == MTSGPU_EMITTER_ENVMAP) {
+        value = env_sample_direct(S->env, dRec, sx, sy);
+    } else {
     const Mesh *m = &S->meshes[e->mesh];
     /* samplePosition */
     float py = sy;
@@ -1590,12 +2012,12 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
     float dp = vabsdot(dRec->d, dRec->n);
     dRec->pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
     dRec->measureSolidAngle = 1;
-    V3 value;
     if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0 && dRec->pdf != 0) {
         value = vdiv(e->radiance, dRec->pdf);
     } else {
         dRec->pdf = 0.0f;
         value = zero;
+    }
     }
     if (dRec->pdf != 0) {
         Ray sray;
@@ -1618,7 +2040,9 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
 static float pdf_emitter_direct(const Scene *S, const DRec *dRec) {
     const Emitter *e = &S->emitters[dRec->emitter];
     float pdf = 0.0f;
-    if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0) {
+    if (e->type == MTSGPU_EMITTER_ENVMAP) {
+        pdf = env_pdf_direction(S->env, dRec->d);
+    } else if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0) {
         float pdfPos = S->meshes[e->mesh].invArea;
         pdf = pdfPos * (dRec->dist * dRec->dist) / vabsdot(dRec->d, dRec->n);
     }
@@ -1648,7 +2072,9 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
     float eta = 1.0f;
     while (depth <= P->maxDepth || P->maxDepth < 0) {
         if (!its.valid) {
-            /* no environment emitter in this row: evalEnvironment = 0 */
+            /* Scene::evalEnvironment (scene.h:910-913) with the camera ray's differentials */
+            if (S->env && emitted && (!P->hide || scattered))
+                L = vadd(L, vmulv(throughput, env_eval(S->env, &ray)));
             break;
         }
         const Bsdf *bsdf = &S->bsdfs[S->meshes[its.mesh].bsdf];
@@ -1707,7 +2133,20 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
                 hitEmitter = 1;
             }
         } else {
-            break; /* no environment emitter */
+            /* path.cpp:233-247 */
+            if (!S->env) break;
+            if (P->hide && !scattered) break;
+            value = env_eval(S->env, &ray);
+            /* EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374) */
+            float nearT, farT;
+            if (!env_bsphere(S->env, ray.o, ray.d, &nearT, &farT) || nearT > 0 || farT < 0) break;
+            dRec.p = ray_at(&ray, farT);
+            dRec.n = vnormalize(vsub(S->env->center, dRec.p));
+            dRec.measureSolidAngle = 1;
+            dRec.emitter = S->envIndex;
+            dRec.d = ray.d;
+            dRec.dist = farT;
+            hitEmitter = 1;
         }
         throughput = vmulv(throughput, bsdfWeight);
         eta *= bRec.eta;
@@ -1836,7 +2275,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     Counters tot = {0, 0, 0, 0};
     uint64_t pathLen = 0, nsamples = 0;
     int err = 0;
-    const float diffScale = 1.0f / sqrtf((float)P->spp); (void)diffScale;
+    const float diffScale = 1.0f / sqrtf((float)P->spp);
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : pathLen, nsamples) reduction(| : err)
@@ -1855,6 +2294,11 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
             const float sx = (float)px + ux, sy = (float)py + uy;
             Ray ray;
             camera_sample_ray(&S.cam, sx, sy, &ray);
+            /* sensorRay.scaleDifferential(diffScaleFactor) (integrator.cpp:181, ray.h:163-168) */
+            ray.rxO = vadd(ray.o, vmul(vsub(ray.rxO, ray.o), diffScale));
+            ray.ryO = vadd(ray.o, vmul(vsub(ray.ryO, ray.o), diffScale));
+            ray.rxD = vadd(ray.d, vmul(vsub(ray.rxD, ray.d), diffScale));
+            ray.ryD = vadd(ray.d, vmul(vsub(ray.ryD, ray.d), diffScale));
             float alpha; int depth;
             V3 L = Li(&S, &PP, ray, &smp, &alpha, &depth, &C);
             if (smp.err) err = 1;
@@ -1965,5 +2409,36 @@ int oracle_bsdf_eval(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *
     V3 v = bsdf_eval(&b, &r);
     value3[0] = v.x; value3[1] = v.y; value3[2] = v.z;
     *pdf = bsdf_pdf(&b, &r);
+    return MTSGPU_OK;
+}
+
+int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
+                      float *rows, float *cols, float *weights) {
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    if (rc || !S.env) { scene_free(&S); return rc ? rc : MTSGPU_EINVAL; }
+    const Env *E = S.env;
+    size_t total = 0;
+    for (int l = 0; l < E->levels; ++l) total += (size_t)E->lw[l] * E->lh[l];
+    if (params) {
+        memset(params, 0, 64 * sizeof(float));
+        params[0] = (float)E->levels; params[1] = (float)E->w0; params[2] = (float)E->h0;
+        params[3] = E->normalization; params[4] = E->pixelX; params[5] = E->pixelY; params[6] = E->scale;
+        params[7] = E->center.x; params[8] = E->center.y; params[9] = E->center.z; params[10] = E->radius;
+        params[11] = (float)total;
+        for (int l = 0; l < E->levels; ++l) { params[16 + l] = (float)E->lw[l]; params[34 + l] = (float)E->lh[l]; }
+    }
+    if (texels) {
+        if (texel_cap < 4 * total) { scene_free(&S); return MTSGPU_EINVAL; }
+        size_t k = 0;
+        for (int l = 0; l < E->levels; ++l)
+            for (size_t t = 0; t < (size_t)E->lw[l] * E->lh[l]; ++t) {
+                texels[k++] = E->lv[l][3 * t]; texels[k++] = E->lv[l][3 * t + 1]; texels[k++] = E->lv[l][3 * t + 2]; texels[k++] = 0;
+            }
+    }
+    if (rows) memcpy(rows, E->cdfRows, sizeof(float) * (E->h0 + 1));
+    if (cols) memcpy(cols, E->cdfCols, sizeof(float) * (size_t)E->h0 * (E->w0 + 1));
+    if (weights) memcpy(weights, E->rowWeights, sizeof(float) * E->h0);
+    scene_free(&S);
     return MTSGPU_OK;
 }

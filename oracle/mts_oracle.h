@@ -33,6 +33,10 @@ int oracle_triaccel_load(const float *A, const float *B, const float *C, float *
 int oracle_triaccel_intersect(const float *ta10, const float *o, const float *d,
                               float mint, float maxt, float *uvt);
 /* Camera: returns sampleToCamera (16) and near-plane differentials dx,dy (3+3) */
+/* environment emitter tables of `scene` (same layout as mtsgpu_debug_env_tables,
+ * texels with 4 halves per texel) */
+int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
+                      float *rows, float *cols, float *weights);
 int oracle_camera(const mtsgpu_sensor_desc *s, float *sample_to_camera16, float *dxdy6);
 /* Microfacet / BSDF probes for consistency tests: see mts_oracle.c */
 int oracle_bsdf_sample(const mtsgpu_bsdf_desc *b, const float *wi3, const float *u3,
