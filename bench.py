@@ -29,10 +29,10 @@ from pkgimport import mitsuba_amd  # noqa: E402
 
 mitsuba_amd()
 from mitsuba_amd import film_border, scenes  # noqa: E402
+from mitsuba_amd.distributed import ROW_BLOCK, RowSharding  # noqa: E402
 from mitsuba_amd.integrator import Context  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-ROW_BLOCK = 8
 
 
 def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
@@ -79,12 +79,12 @@ def main():
     b = film_border(integ.rfilter, integ.rfilterParam)
     film = torch.zeros(((H + 2 * b) * (W + 2 * b) * 5,), dtype=torch.float32, device='cuda')
     stream = torch.cuda.current_stream().cuda_stream
-    row = (ROW_BLOCK, world, rank)
+    shard = RowSharding(rank, world, ROW_BLOCK)
+    row = shard.row_params()
 
     def step():
         st = ctx.render_device(integ, film.data_ptr(), stream, row=row)
-        if world > 1:
-            dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
+        shard.reduce(film, dist)
         return st
 
     for _ in range(args.warmup):

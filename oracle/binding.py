@@ -48,6 +48,8 @@ def lib():
         L.oracle_camera.argtypes = [C.POINTER(abi.SensorDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 6 + [C.c_int]
         L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 4 + [C.c_int]
+        L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                       C.POINTER(C.c_float)]
         rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
         if rc != 0:
             raise RuntimeError('oracle_sobol_init failed: %d' % rc)

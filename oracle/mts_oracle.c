@@ -2442,3 +2442,31 @@ int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *t
     scene_free(&S);
     return MTSGPU_OK;
 }
+
+/* ShapeKDTree::rayIntersect(ray, its) probe (tests/test_oracle_kat.py, after
+ * src/tests/test_dgeom.cpp:35-176): out16 = {valid, t, p[3], geoN[3], shN[3], shS[3], mesh, tri} */
+int oracle_intersect(const mtsgpu_scene_desc *scene, const float *o, const float *d, float *out16) {
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    if (rc) { scene_free(&S); return rc; }
+    Ray ray;
+    memset(&ray, 0, sizeof ray);
+    ray.o = v3(o[0], o[1], o[2]);
+    ray_set_dir(&ray, v3(d[0], d[1], d[2]));
+    ray.mint = EPSILON; ray.maxt = INFINITY;
+    Its its;
+    Counters C = {0, 0, 0, 0};
+    scene_intersect(&S, &ray, &its, &C);
+    memset(out16, 0, 16 * sizeof(float));
+    out16[0] = (float)its.valid;
+    if (its.valid) {
+        out16[1] = its.t;
+        out16[2] = its.p.x; out16[3] = its.p.y; out16[4] = its.p.z;
+        out16[5] = its.geoN.x; out16[6] = its.geoN.y; out16[7] = its.geoN.z;
+        out16[8] = its.sh.n.x; out16[9] = its.sh.n.y; out16[10] = its.sh.n.z;
+        out16[11] = its.sh.s.x; out16[12] = its.sh.s.y; out16[13] = its.sh.s.z;
+        out16[14] = (float)its.mesh; out16[15] = (float)its.tri;
+    }
+    scene_free(&S);
+    return MTSGPU_OK;
+}

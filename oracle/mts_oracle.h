@@ -37,6 +37,7 @@ int oracle_triaccel_intersect(const float *ta10, const float *o, const float *d,
  * texels with 4 halves per texel) */
 int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
                       float *rows, float *cols, float *weights);
+int oracle_intersect(const mtsgpu_scene_desc *scene, const float *o, const float *d, float *out16);
 int oracle_camera(const mtsgpu_sensor_desc *s, float *sample_to_camera16, float *dxdy6);
 /* Microfacet / BSDF probes for consistency tests: see mts_oracle.c */
 int oracle_bsdf_sample(const mtsgpu_bsdf_desc *b, const float *wi3, const float *u3,
