@@ -33,6 +33,12 @@ from mitsuba_amd.distributed import ROW_BLOCK, RowSharding  # noqa: E402
 from mitsuba_amd.integrator import Context  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+WORKLOADS = {
+    'C1': 'C1: Cornell box 512x512 64 spp (plumbing config)',
+    'C2': 'C2: Cornell box (32 tris, diffuse, area light), path maxDepth=-1 rrDepth=5, sobol, box filter',
+    'C3': 'C3: matpreview (69k-tri object, roughconductor GGX a=0.1 Cu, diffuse checker ground, 1024x512 '
+          'envmap only), path maxDepth=-1 rrDepth=5, sobol, box filter',
+}
 
 
 def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
@@ -135,8 +141,7 @@ def main():
             'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed_max / args.steps * 1e3, 2), 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-            'config': {'workload': 'C2: Cornell box (32 tris, diffuse, area light), path maxDepth=-1 rrDepth=5, '
-                                   'sobol, box filter', 'width': W, 'height': H, 'spp': spp,
+            'config': {'workload': WORKLOADS.get(args.config, args.config), 'width': W, 'height': H, 'spp': spp,
                        'samples_per_frame': frame_samples, 'parallelism': 'rows sharded x%d + RCCL film reduce' % world,
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},
             'roofline': roofline,

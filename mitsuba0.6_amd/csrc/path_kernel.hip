@@ -455,8 +455,11 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 // next iteration's two rays.  Sampler dimensions are consumed in the
 // reference's order (NEE 2D, BSDF 2D [+1D], RR 1D), and radiance is
 // accumulated in the reference's order (NEE term before the BSDF-hit term).
-template <bool SAMPLES, bool STATS, bool SCENE_LDS>
+// INSTR: traversal statistics + optional per-sample records (tests, roofline
+// pass); SCENE_LDS: BVH + TriAccel staged in LDS; ENV: scene has an envmap
+template <bool INSTR, bool SCENE_LDS, bool ENV>
 __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaunch L) {
+    constexpr bool STATS = INSTR;
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
     // LDS: [Sobol nibble tables][look_up column tables][BVH + TriAccel (small scenes)][stacks]
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                     vertex = true;
                 } else if (!P.its.valid) {
                     // missed: the environment emitter, if any (path.cpp:233-247)
-                    if (S.env_emitter >= 0 && !(L.hide_emitters && !P.scattered)) {
+                    if (ENV && !(L.hide_emitters && !P.scattered)) {
                         glb_env *E = (glb_env *)S.env;
                         const f3 value = env_eval(E, rd);
                         float nT, fT;
@@ -666,7 +669,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                 } else if (!P.its.valid) {
                     // camera ray missed: scene->evalEnvironment(ray) with the sensor's ray
                     // differentials (path.cpp:136-142, perspective.cpp:271-298, integrator.cpp:181)
-                    if (S.env_emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered)) {
+                    if (ENV && P.emitted && (!L.hide_emitters || P.scattered)) {
                         const MtsgCamera &cam = S.cam;
                         const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
                         const f3 rxl = normalize(add(nearP, ld3(cam.dx))), ryl = normalize(add(nearP, ld3(cam.dy)));
@@ -700,7 +703,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                             const MtsgEmitter &e = S.emitters[ei];
                             f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
                             float pdf = 0.0f, dist = 0.0f;
-                            if (e.type == MTSG_EMITTER_ENVMAP) {
+                            if (ENV && e.type == MTSG_EMITTER_ENVMAP) {
                                 value = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey, dd, dist, pdf);
                             } else {
                             // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
@@ -795,7 +798,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha == 0.0f ? -ownW : ownW);
             else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
-            if (SAMPLES) {
+            if (INSTR && L.samples) {
                 const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
                 float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
                 rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
@@ -878,18 +881,20 @@ size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
     return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + (size_t)L.stack_depth * 2 * BLOCK) * 4;
 }
 
-template <bool SCENE_LDS>
-static void launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
+template <bool SCENE_LDS, bool ENV>
+static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
     const size_t lds = mtsg_path_lds_bytes(L);
-    if (samples && stats) hipLaunchKernelGGL((path_kernel<true, true, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else if (samples) hipLaunchKernelGGL((path_kernel<true, false, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else if (stats) hipLaunchKernelGGL((path_kernel<false, true, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else hipLaunchKernelGGL((path_kernel<false, false, SCENE_LDS>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, ENV>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, ENV>), dim3(grid), dim3(BLOCK), lds, stream, L);
 }
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
-    if (L.scene_lds) launch_path<true>(L, grid, samples, stats, stream);
-    else launch_path<false>(L, grid, samples, stats, stream);
+    const bool instr = samples || stats, env = L.scene.env_emitter >= 0;
+    if (L.scene_lds) {
+        if (env) launch_path<true, true>(L, grid, instr, stream); else launch_path<true, false>(L, grid, instr, stream);
+    } else {
+        if (env) launch_path<false, true>(L, grid, instr, stream); else launch_path<false, false>(L, grid, instr, stream);
+    }
     return hipGetLastError();
 }
 
@@ -913,9 +918,11 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
 }
 
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
+    const size_t lds = mtsg_path_lds_bytes(L);
+    const bool env = L.scene.env_emitter >= 0;
     if (L.scene_lds)
-        return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, true>, BLOCK,
-                                                                 mtsg_path_lds_bytes(L));
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, false>, BLOCK,
-                                                             mtsg_path_lds_bytes(L));
+        return (int)(env ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, true, true>, BLOCK, lds)
+                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, true, false>, BLOCK, lds));
+    return (int)(env ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, true>, BLOCK, lds)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, false>, BLOCK, lds));
 }
