@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round profiling on the GPU box (run through gpurun from the repo root):
+#  1. rocprofv3 --kernel-trace --stats of the bench command itself (C2, C3)
+#  2. separate PMC passes FETCH_SIZE / WRITE_SIZE (MI355X_MICROARCH.md "HBM")
+#     over one full frame of each config, for bench.py's roofline.traffic
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -eu
+OUT=${1:-gpurun_out/prof}
+ROOT=$(pwd)
+mkdir -p $OUT
+export TMPDIR=/tmp
+for cfg in C2 C3; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench_$cfg -o bench --output-format csv \
+      -- python3 $ROOT/bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_$cfg.log 2>&1
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/pmc_${cfg}_$ctr -o pmc --output-format csv \
+        -- python3 $ROOT/tools/prof_run.py $cfg 1 1 > $OUT/pmc_${cfg}_$ctr.log 2>&1
+  done
+done
+echo done > $OUT/ok

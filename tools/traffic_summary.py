@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Summarise a prof_round.sh output directory into profiles/<round>_*.
+
+For each config: the path kernel's per-launch FETCH_SIZE / WRITE_SIZE (KiB, as
+rocprofv3 reports them) and HBM bytes corrected per MI355X_MICROARCH.md: on
+gfx950 FETCH_SIZE counts half the bytes of wide reads (x2), WRITE_SIZE is
+exact.  Writes profiles/<round>_traffic_<cfg>.json and copies the kernel
+stats CSVs of the bench runs."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+src, rnd = sys.argv[1], sys.argv[2]
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(REPO, 'profiles')
+
+
+def counter(path_glob, name):
+    vals = []
+    for f in glob.glob(path_glob, recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r['Counter_Name'] == name and 'path_kernel' in r['Kernel_Name']:
+                vals.append(float(r['Counter_Value']))
+    return vals
+
+
+for cfg in ('C2', 'C3'):
+    fetch = counter(os.path.join(src, 'pmc_%s_FETCH_SIZE' % cfg, '**', '*counter_collection.csv'), 'FETCH_SIZE')
+    write = counter(os.path.join(src, 'pmc_%s_WRITE_SIZE' % cfg, '**', '*counter_collection.csv'), 'WRITE_SIZE')
+    if fetch and write:
+        f, w = sum(fetch) / len(fetch), sum(write) / len(write)
+        out = {'config': cfg, 'kernel': 'path_kernel', 'launches': len(fetch), 'FETCH_SIZE_KiB': f, 'WRITE_SIZE_KiB': w,
+               'hbm_bytes_per_launch': 2 * f * 1024 + w * 1024,
+               'note': 'one full frame (tools/prof_run.py %s 1 1); FETCH_SIZE doubled (gfx950 counts half of wide '
+                       'reads), WRITE_SIZE as reported' % cfg}
+        json.dump(out, open(os.path.join(prof, '%s_traffic_%s.json' % (rnd, cfg)), 'w'), indent=1)
+        print(cfg, out)
+    for f in glob.glob(os.path.join(src, 'bench_%s' % cfg, '**', '*kernel_stats.csv'), recursive=True):
+        shutil.copy(f, os.path.join(prof, '%s_bench_%s_kernel_stats.csv' % (rnd, cfg)))
+        print('copied', f)
+    log = os.path.join(src, 'bench_%s.log' % cfg)
+    if os.path.exists(log):
+        shutil.copy(log, os.path.join(prof, '%s_bench_%s.log' % (rnd, cfg)))
