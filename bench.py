@@ -38,6 +38,8 @@ WORKLOADS = {
     'C2': 'C2: Cornell box (32 tris, diffuse, area light), path maxDepth=-1 rrDepth=5, sobol, box filter',
     'C3': 'C3: matpreview (69k-tri object, roughconductor GGX a=0.1 Cu, diffuse checker ground, 1024x512 '
           'envmap only), path maxDepth=-1 rrDepth=5, sobol, box filter',
+    'C4': 'C4: atrium (195k tris, 24 fluted columns, roughdielectric GGX a=0.2 eta=1.5 on ~30% of meshes, '
+          'diffuse elsewhere, 4 area lights) 1280x720 256 spp, path maxDepth=-1 rrDepth=5, sobol, box filter',
 }
 
 

@@ -203,10 +203,114 @@ def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env
     return scene, integ
 
 
+def _box_mesh(lo, hi, n=1, inward=False):
+    """Axis-aligned box, each face an n x n grid of quads (2n^2 triangles per face)."""
+    lo, hi = np.asarray(lo, np.float64), np.asarray(hi, np.float64)
+    pos, idx = [], []
+    for axis in range(3):
+        for side in (0, 1):
+            u, v = [a for a in range(3) if a != axis]
+            base = len(pos)
+            for i in range(n + 1):
+                for j in range(n + 1):
+                    p = np.empty(3)
+                    p[axis] = hi[axis] if side else lo[axis]
+                    p[u] = lo[u] + (hi[u] - lo[u]) * i / n
+                    p[v] = lo[v] + (hi[v] - lo[v]) * j / n
+                    pos.append(p)
+            outward_sign = 1 if side else -1
+            # (u, v, axis) right-handed? orient so the normal points outward (or inward)
+            flip = (np.cross(np.eye(3)[u], np.eye(3)[v])[axis] * outward_sign < 0) != inward
+            for i in range(n):
+                for j in range(n):
+                    a, b = base + i * (n + 1) + j, base + (i + 1) * (n + 1) + j
+                    c, d = b + 1, a + 1
+                    tris = [(a, b, c), (a, c, d)]
+                    if flip:
+                        tris = [(a, c, b), (a, d, c)]
+                    idx += tris
+    return np.asarray(pos, np.float32), np.asarray(idx, np.uint32)
+
+
+def _column_mesh(cx, cz, radius, height, seg, rings, rng):
+    """Fluted column: a cylinder with a sinusoidal flute profile, capped top and bottom."""
+    th = np.linspace(0, 2 * np.pi, seg, endpoint=False)
+    ys = np.linspace(0.0, height, rings + 1)
+    flute = 1 + 0.06 * np.cos(16 * th + rng.uniform(0, 2 * np.pi))
+    pos = []
+    for y in ys:
+        taper = 1 - 0.12 * y / height
+        for t, f in zip(th, flute):
+            r = radius * f * taper
+            pos.append((cx + r * np.cos(t), y, cz + r * np.sin(t)))
+    idx = []
+    for k in range(rings):
+        for i in range(seg):
+            a, b = k * seg + i, k * seg + (i + 1) % seg
+            c, d = a + seg, b + seg
+            idx += [(a, c, d), (a, d, b)]
+    # caps (fans around a centre vertex)
+    for y, top in ((0.0, False), (height, True)):
+        ci = len(pos)
+        pos.append((cx, y, cz))
+        ring0 = rings * seg if top else 0
+        for i in range(seg):
+            a, b = ring0 + i, ring0 + (i + 1) % seg
+            idx.append((ci, b, a) if top else (ci, a, b))
+    return np.asarray(pos, np.float32), np.asarray(idx, np.uint32)
+
+
+def atrium(width=1280, height=720, spp=256, rfilter='box', max_depth=-1, columns=(4, 6), seg=96, rings=40,
+           seed=0x5EED):
+    """Config C4: procedural ~200k-triangle atrium -- a hall with 24 fluted columns,
+    tiled floor, four ceiling lights; roughdielectric GGX alpha=0.2 eta=1.5 on ~30%
+    of the meshes, diffuse elsewhere."""
+    rng = np.random.default_rng(seed)
+    glass = BSDF('roughdielectric', distribution='ggx', alpha=0.2, intIOR=1.5, extIOR=1.0)
+    bsdfs = [BSDF('diffuse', reflectance=(0.7, 0.68, 0.62)),     # 0 walls
+             BSDF('diffuse', reflectance=(0.35, 0.3, 0.25)),     # 1 floor
+             glass]                                              # 2
+    meshes, emitters = [], []
+    W, D, H = 16.0, 28.0, 9.0
+    p, i = _box_mesh((-W / 2, 0, -D / 2), (W / 2, H, D / 2), n=12, inward=True)
+    meshes.append(Mesh(p, i, bsdf=0, faceNormals=True, name='hall'))
+    p, i = _box_mesh((-W / 2 + 0.2, 0.0, -D / 2 + 0.2), (W / 2 - 0.2, 0.05, D / 2 - 0.2), n=20)
+    meshes.append(Mesh(p, i, bsdf=1, faceNormals=True, name='floor'))
+    nx, nz = columns
+    k = 0
+    for a in range(nx):
+        for b in range(nz):
+            cx = -W / 2 + (a + 0.5) * W / nx
+            cz = -D / 2 + (b + 0.5) * D / nz
+            if abs(cx) < 1.0 and cz > 4:
+                cz += 0.0
+            c = rng.uniform(0.2, 0.8, 3)
+            if rng.random() < 0.3:
+                bi = 2
+            else:
+                bsdfs.append(BSDF('diffuse', reflectance=tuple(float(x) for x in c)))
+                bi = len(bsdfs) - 1
+            p, i = _column_mesh(cx, cz, 0.45, H - 0.5, seg, rings, rng)
+            meshes.append(Mesh(p, i, bsdf=bi, name='column%d' % k))
+            k += 1
+    for lx, lz in ((-3.5, -7), (3.5, -7), (-3.5, 7), (3.5, 7)):
+        q = np.array([(lx - 1, H - 0.01, lz - 1.5), (lx + 1, H - 0.01, lz - 1.5), (lx + 1, H - 0.01, lz + 1.5),
+                      (lx - 1, H - 0.01, lz + 1.5)], np.float32)
+        meshes.append(Mesh(q, np.array([(0, 1, 2), (0, 2, 3)], np.uint32), emitter=len(emitters),
+                           faceNormals=True, name='light'))
+        emitters.append(Emitter('area', radiance=(14.0, 13.0, 11.0)))
+    cam = Transform.look_at_((0.0, 3.2, -13.0), (0.0, 3.0, 4.0), (0, 1, 0)).m
+    sensor = Sensor(fov=60.0, fovAxis='x', nearClip=0.01, farClip=100.0, toWorld=cam, width=width, height=height)
+    scene = Scene(sensor, meshes, bsdfs, emitters, name='atrium')
+    integ = PathIntegrator(maxDepth=max_depth, rrDepth=5, sampleCount=spp, rfilter=rfilter, rfilterParam=0.5)
+    return scene, integ
+
+
 CONFIGS = {
     'C1': dict(builder='cornell_box', width=512, height=512, spp=64),
     'C2': dict(builder='cornell_box', width=1280, height=720, spp=512),
     'C3': dict(builder='matpreview', width=1280, height=720, spp=512),
+    'C4': dict(builder='atrium', width=1280, height=720, spp=256),
 }
 
 

@@ -116,3 +116,14 @@ def test_envmap_variants(gpu_ctx, oracle):
         film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
         same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
         assert same.mean() > 0.999, (kw, hide, same.mean())
+
+
+def test_atrium_bitexact(gpu_ctx, oracle):
+    """C4 at small size: ~195k triangles in HBM (no LDS staging), roughdielectric columns,
+    four area lights -- the global-memory traversal path."""
+    sc, it = scenes.build('C4', width=48, height=27, spp=4)
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1, threads=8)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
