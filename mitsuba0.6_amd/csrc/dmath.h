@@ -48,6 +48,17 @@ __device__ __forceinline__ float signum(float v) { return copysignf(1.0f, v); } 
 __device__ __forceinline__ float smaxc(f3 s) { float r = s.x; r = smax(r, s.y); r = smax(r, s.z); return r; }
 
 // libm (glibc in the reference) -> double precision, rounded once
+#ifdef MTSG_ABL_FAST_LIBM   // timing ablation only (not parity-exact): single-precision libm
+__device__ __forceinline__ void d_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
+__device__ __forceinline__ float d_acos(float x) { return acosf(x); }
+__device__ __forceinline__ float d_atan2(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ float d_tan(float x) { return tanf(x); }
+__device__ __forceinline__ float d_atan(float x) { return atanf(x); }
+__device__ __forceinline__ float d_expf(float x) { return expf(x); }
+__device__ __forceinline__ float d_powf(float x, float y) { return powf(x, y); }
+__device__ __forceinline__ float d_fastexp(float x) { return expf(x); }
+__device__ __forceinline__ float d_fastlog(float x) { return logf(x); }
+#else
 __device__ __forceinline__ void d_sincos(float x, float *s, float *c) {
     double sd, cd;
     sincos((double)x, &sd, &cd);
@@ -61,6 +72,7 @@ __device__ __forceinline__ float d_expf(float x) { return (float)exp((double)x);
 __device__ __forceinline__ float d_powf(float x, float y) { return (float)pow((double)x, (double)y); }
 __device__ __forceinline__ float d_fastexp(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float d_fastlog(float x) { return (float)log((double)x); }
+#endif
 
 struct Frame { f3 s, t, n; };
 __device__ __forceinline__ f3 to_local(const Frame &f, f3 v) { return mk(dot(v, f.s), dot(v, f.t), dot(v, f.n)); }

@@ -119,9 +119,17 @@ struct Hit {
 // ---------------------------------------------------------------------------
 // BVH2 traversal
 // ---------------------------------------------------------------------------
+// LDS traversal stack, lane-strided: node index (4 B) + entry distance as the
+// top 16 bits of the (non-negative) float, i.e. bfloat16 rounded toward zero:
+// a lower bound of the true entry distance, so culling on pop stays
+// conservative (6 B/entry keeps 3 blocks per CU on large scenes)
+typedef __attribute__((address_space(3))) int lds_stk_n;
+typedef __attribute__((address_space(3))) uint16_t lds_stk_d;
+__device__ __forceinline__ uint16_t dist_down16(float t) { return (uint16_t)(__float_as_uint(fmaxf(t, 0.0f)) >> 16); }
+__device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 template <bool ANY, bool STATS, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
-                                         int *__restrict__ stk, uint32_t &bestSlot, float &bu, float &bv,
+                                         lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
                                          float &bt, unsigned long long &nodes, unsigned long long &tests) {
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
@@ -161,8 +169,8 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 int nearC = e.x, farC = e.y;
                 float farT = n1;
                 if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
-                stk[sp * (2 * BLOCK)] = farC;
-                stk[sp * (2 * BLOCK) + BLOCK] = __float_as_int(farT);
+                stkN[sp * BLOCK] = farC;
+                stkD[sp * BLOCK] = dist_down16(farT);
                 ++sp;
                 node = nearC;
                 continue;
@@ -212,8 +220,7 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         bool popped = false;
         while (sp > 0) {
             --sp;
-            const float tEntry = __int_as_float(stk[sp * (2 * BLOCK) + BLOCK]);
-            if (ANY || tEntry <= bt) { node = stk[sp * (2 * BLOCK)]; popped = true; break; }
+            if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) { node = stkN[sp * BLOCK]; popped = true; break; }
         }
         if (!popped) break;
     }
@@ -496,7 +503,8 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
     SC.lds_dims = L.lds_dims;
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
-    int *stk = reinterpret_cast<int *>(lds + base2 + sceneWords) + threadIdx.x;
+    lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
 
     unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
     unsigned long long cHits = 0, cNee = 0, cSobol = 0;
@@ -576,9 +584,9 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
 #endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS)
-                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
                 else
-                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
             }
         }
         bool hit = false;
@@ -589,9 +597,9 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
             float mint, maxt;
             if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
-                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
                 else
-                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
             }
         }
 
@@ -680,7 +688,11 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                                     W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
                         rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
                         ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
+#ifdef MTSG_ABL_BILINEAR_PRIMARY   // timing ablation only
+                        P.L = add(P.L, mulv(P.thr, env_eval((glb_env *)S.env, rd)));
+#else
                         P.L = add(P.L, mulv(P.thr, env_eval_diff((glb_env *)S.env, rd, rxd, ryd)));
+#endif
                     }
                     endPath = true;
                 } else {
@@ -704,7 +716,9 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaun
                             f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
                             float pdf = 0.0f, dist = 0.0f;
                             if (ENV && e.type == MTSG_EMITTER_ENVMAP) {
+#ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
                                 value = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey, dd, dist, pdf);
+#endif
                             } else {
                             // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
                             float py2 = ey;
@@ -878,7 +892,7 @@ __global__ void arith_probe(const float *a, const float *b, float *out, int n) {
 // ---------------------------------------------------------------------------
 size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
     const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
-    return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + (size_t)L.stack_depth * 2 * BLOCK) * 4;
+    return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2) * 4;
 }
 
 template <bool SCENE_LDS, bool ENV>
