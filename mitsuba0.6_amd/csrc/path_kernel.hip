@@ -127,6 +127,122 @@ typedef __attribute__((address_space(3))) int lds_stk_n;
 typedef __attribute__((address_space(3))) uint16_t lds_stk_d;
 __device__ __forceinline__ uint16_t dist_down16(float t) { return (uint16_t)(__float_as_uint(fmaxf(t, 0.0f)) >> 16); }
 __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+#ifndef MTSG_TRAV_IFIF
+// Speculative while-while traversal (Aila & Laine 2009): a lane that reaches a
+// leaf parks it and keeps descending until every lane of the wave holds a
+// leaf; then all lanes test their parked leaves together.  Same closest hit
+// (tie rule included) as a plain depth-first traversal.
+template <bool ANY, bool STATS, typename NodeT, typename TriT>
+__device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
+                                         lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
+    const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
+    const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
+    const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
+    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
+    constexpr int DONE = 0x7fffffff;
+    bool found = false;
+    uint32_t bestPrim = 0;
+    bt = maxt;
+    int sp = 0;
+    int node = 0, leaf = 0;
+    auto pop = [&]() -> int {
+        while (sp > 0) {
+            --sp;
+            if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
+        }
+        return DONE;
+    };
+    while (node != DONE) {
+        // inner nodes
+        while ((uint32_t)node < (uint32_t)DONE) {
+            if (STATS) nodes++;
+            NodeT *n = nodesArr + node;
+            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
+            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
+            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
+            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+            // slab tests; node boxes are conservatively inflated on the host
+            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
+            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
+            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
+            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
+            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
+            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
+            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
+            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
+            const bool h0 = n0 <= f0, h1 = n1 <= f1;
+            if (h0 && h1) {
+                int nearC = e.x, farC = e.y;
+                float farT = n1;
+                if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
+                stkN[sp * BLOCK] = farC;
+                stkD[sp * BLOCK] = dist_down16(farT);
+                ++sp;
+                node = nearC;
+            } else if (h0) {
+                node = e.x;
+            } else if (h1) {
+                node = e.y;
+            } else {
+                node = pop();
+            }
+            // park the first leaf reached and keep descending
+            if (node < 0 && leaf == 0) {
+                leaf = node;
+                node = pop();
+            }
+            if (!__any(leaf == 0)) break;
+        }
+        // leaves
+        while (leaf < 0) {
+            const uint32_t ref = (uint32_t)(~leaf);
+            const uint32_t first = ref >> 4, count = ref & 15u;
+            for (uint32_t i = first; i < first + count; ++i) {
+                if (STATS) tests++;
+                TriT *tr = trisArr + i;
+                const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
+                const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
+                const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
+                const uint32_t k = __float_as_uint(q0.x);
+                // TriAccel::rayIntersect (triaccel.h:92-160)
+                float o_u, o_v, o_k, d_u, d_v, d_k;
+                if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+                else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+                else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+                else continue;
+                const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
+                const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
+                const float c_nu = q2.x, c_nv = q2.y;
+                const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+                if (t < mint || t > bt) continue;
+                const float hu = o_u + t * d_u - a_u;
+                const float hv = o_v + t * d_v - a_v;
+                const float u = hv * b_nu + hu * b_nv;
+                const float v = hu * c_nu + hv * c_nv;
+                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                    if (ANY) return true;
+                    const uint32_t prim = __float_as_uint(q2.z);
+                    // ties (t == bt): the larger primitive index wins
+                    if (!found || t < bt || prim > bestPrim) {
+                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+                    }
+                }
+            }
+            leaf = 0;
+            if (node < 0) {   // the next stack entry is a leaf too: take it now
+                leaf = node;
+                node = pop();
+            }
+        }
+    }
+    return found;
+}
+#else
 template <bool ANY, bool STATS, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
@@ -226,6 +342,8 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     }
     return found;
 }
+
+#endif
 
 // AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
 __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, float &nearT, float &farT) {
