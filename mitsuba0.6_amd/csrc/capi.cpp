@@ -29,6 +29,7 @@ int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
 namespace {
 
 thread_local std::string g_create_error;
+constexpr size_t BLOCK_THREADS = 256;   // = BLOCK in path_kernel.hip
 
 struct DevBuf {
     void *p = nullptr;
@@ -273,6 +274,21 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // small scenes: stage the whole BVH + TriAccel array in LDS (<= 32 KiB)
     const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri);
     L.scene_lds = (sceneBytes <= (32u << 10) && !std::getenv("MTSGPU_NO_SCENE_LDS")) ? 1u : 0u;
+    // large scenes are latency-bound: run 4 waves/SIMD when 4 blocks' traversal
+    // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
+    // LDS as the rest allows (the others are read through L1/L2)
+    L.waves = 3;
+    if (!L.scene_lds) {
+        const size_t perBlock = (160u << 10) / 4;
+        const size_t fixed = ((size_t)L.stack_depth * 3 * BLOCK_THREADS + 1) / 2 * 4 + 16 * 16 * 4;
+        if (fixed < perBlock) {
+            L.waves = 4;
+            L.lds_dims = (uint32_t)std::min<size_t>(32, (perBlock - fixed) / ((size_t)L.nibbles * 16 * 4));
+        }
+    }
+    if (const char *env = std::getenv("MTSGPU_WAVES")) L.waves = std::atoi(env) == 4 ? 4u : 3u;
+    if (const char *env = std::getenv("MTSGPU_SOBOL_LDS_DIMS"))
+        L.lds_dims = (uint32_t)std::min(1024l, std::max(0l, std::strtol(env, nullptr, 10)));
     // own-pixel splat buffer [5][chunk][pixels]; spp processed in chunks that fit the budget
     size_t budget = (size_t)8 << 30;
     if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);

@@ -166,6 +166,7 @@ struct MtsgLaunch {
     uint32_t stack_depth;             // LDS traversal stack entries per lane
     uint32_t num_nodes;               // BVH2 inner nodes
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
+    uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

@@ -582,8 +582,8 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 // accumulated in the reference's order (NEE term before the BSDF-hit term).
 // INSTR: traversal statistics + optional per-sample records (tests, roofline
 // pass); SCENE_LDS: BVH + TriAccel staged in LDS; ENV: scene has an envmap
-template <bool INSTR, bool SCENE_LDS, bool ENV>
-__global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void path_kernel(MtsgLaunch L) {
+template <bool INSTR, bool SCENE_LDS, bool ENV, int WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     constexpr bool STATS = INSTR;
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
@@ -1013,20 +1013,27 @@ size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
     return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2) * 4;
 }
 
-template <bool SCENE_LDS, bool ENV>
-static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
+// variants: small scenes (BVH in LDS) run 3 waves/SIMD with 32 Sobol dims in
+// LDS; large scenes run 4 waves/SIMD (128 VGPRs) when the traversal stacks fit
+// 4 blocks per CU, else 3 (capi.cpp picks L.waves and L.lds_dims)
+template <bool SCENE_LDS, bool ENV, int WAVES>
+static void launch_path_w(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
     const size_t lds = mtsg_path_lds_bytes(L);
-    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, ENV>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, ENV>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, ENV, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, ENV, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
+}
+
+template <bool ENV>
+static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
+    if (L.scene_lds) launch_path_w<true, ENV, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+    else if (L.waves == 4) launch_path_w<false, ENV, 4>(L, grid, instr, stream);
+    else launch_path_w<false, ENV, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
 }
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
-    const bool instr = samples || stats, env = L.scene.env_emitter >= 0;
-    if (L.scene_lds) {
-        if (env) launch_path<true, true>(L, grid, instr, stream); else launch_path<true, false>(L, grid, instr, stream);
-    } else {
-        if (env) launch_path<false, true>(L, grid, instr, stream); else launch_path<false, false>(L, grid, instr, stream);
-    }
+    const bool instr = samples || stats;
+    if (L.scene.env_emitter >= 0) launch_path<true>(L, grid, instr, stream);
+    else launch_path<false>(L, grid, instr, stream);
     return hipGetLastError();
 }
 
@@ -1049,12 +1056,17 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
     return hipGetLastError();
 }
 
+template <bool SCENE_LDS, bool ENV, int WAVES>
+static int occupancy_w(const MtsgLaunch &L, int *bpc) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, path_kernel<false, SCENE_LDS, ENV, WAVES>, BLOCK,
+                                                             mtsg_path_lds_bytes(L));
+}
+template <bool ENV>
+static int occupancy_e(const MtsgLaunch &L, int *bpc) {
+    if (L.scene_lds) return occupancy_w<true, ENV, MTSG_WAVES_PER_EU>(L, bpc);
+    if (L.waves == 4) return occupancy_w<false, ENV, 4>(L, bpc);
+    return occupancy_w<false, ENV, MTSG_WAVES_PER_EU>(L, bpc);
+}
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
-    const size_t lds = mtsg_path_lds_bytes(L);
-    const bool env = L.scene.env_emitter >= 0;
-    if (L.scene_lds)
-        return (int)(env ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, true, true>, BLOCK, lds)
-                         : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, true, false>, BLOCK, lds));
-    return (int)(env ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, true>, BLOCK, lds)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocksPerCU, path_kernel<false, false, false>, BLOCK, lds));
+    return L.scene.env_emitter >= 0 ? occupancy_e<true>(L, blocksPerCU) : occupancy_e<false>(L, blocksPerCU);
 }

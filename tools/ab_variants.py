@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of libmtsgpu variants in one process (guide rule 24).
-usage: ab_variants.py <config> <rounds> <rows_stride> name=path ..."""
+usage: ab_variants.py <config> <rounds> <rows_stride> name=path[,ENV=VAL...] ...
+(environment overrides are applied around each variant's render calls)"""
 import os
 import sys
 
@@ -13,18 +14,38 @@ from mitsuba_amd import scenes  # noqa: E402
 from mitsuba_amd.integrator import Context  # noqa: E402
 
 cfg, rounds, stride = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-variants = [a.split('=', 1) for a in sys.argv[4:]]
+variants, envs = [], {}
+for a in sys.argv[4:]:
+    name, rest = a.split('=', 1)
+    parts = rest.split(',')
+    variants.append((name, parts[0]))
+    envs[name] = dict(p.split('=', 1) for p in parts[1:])
+
+
+def with_env(name, fn):
+    saved = {k: os.environ.get(k) for k in envs[name]}
+    os.environ.update(envs[name])
+    try:
+        return fn()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 sc, it = scenes.build(cfg, rfilter='box')
 ctxs = {}
 for name, path in variants:
     c = Context(0, lib_path=path)
     c.upload(sc)
-    c.render(it, row=(8, stride, 0))   # warm up
+    with_env(name, lambda: c.render(it, row=(8, stride, 0)))   # warm up
     ctxs[name] = c
 res = {n: [] for n, _ in variants}
 for r in range(rounds):
     for name, _ in variants:
-        _, _, st = ctxs[name].render(it, row=(8, stride, 0))
+        _, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0)))
         res[name].append(st['samples'] / st['kernel_ms'] / 1e3)
 for name, v in res.items():
     v = sorted(v)
