@@ -95,6 +95,8 @@ __device__ __forceinline__ float m_hypot2(float a, float b) {
 
 // ---- MicrofacetDistribution -----------------------------------------------
 struct Distr { int type; float alphaU, alphaV; int sampleVisible; float expU, expV; };
+// BSDF records are read straight from global memory (no generic/flat loads)
+typedef const __attribute__((address_space(1))) MtsgBsdf GBsdf;
 
 __device__ __forceinline__ void distr_phong_exp(Distr &d) {      // microfacet.h:673-676
     d.expU = smax(2.0f / (d.alphaU * d.alphaU) - 2.0f, 0.0f);
@@ -116,7 +118,7 @@ __device__ __forceinline__ float distr_interp_phong(const Distr &d, f3 v) {   //
     return d.expU * (v.x * v.x * inv) + d.expV * (v.y * v.y * inv);
 }
 
-__device__ __noinline__ float distr_eval(const Distr &d, f3 m) {   // :191-238
+__device__ __noinline__ float distr_eval(Distr d, f3 m) {   // :191-238
     if (m.z <= 0) return 0.0f;
     float cosTheta2 = m.z * m.z;
     float be = ((m.x * m.x) / (d.alphaU * d.alphaU) + (m.y * m.y) / (d.alphaV * d.alphaV)) / cosTheta2;
@@ -142,7 +144,7 @@ __device__ __forceinline__ float distr_project_roughness(const Distr &d, f3 v) {
     return dsqrt(cosPhi2 * d.alphaU * d.alphaU + sinPhi2 * d.alphaV * d.alphaV);
 }
 
-__device__ __noinline__ float distr_smithG1(const Distr &d, f3 v, f3 m) {   // :477-518
+__device__ __noinline__ float distr_smithG1(Distr d, f3 v, f3 m) {   // :477-518
     if (dot(v, m) * v.z <= 0) return 0.0f;
     float tanTheta = fabsf(tan_theta(v));
     if (tanTheta == 0.0f) return 1.0f;
@@ -164,7 +166,7 @@ __device__ __forceinline__ void distr_first_quadrant(const Distr &d, float u1, f
     exponent = d.expU * c * c + d.expV * s * s;
 }
 
-__device__ __noinline__ f3 distr_sample_all(const Distr &d, float sx, float sy, float &pdf) {  // :287-402
+__device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy, float &pdf) {  // :287-402
     float cosThetaM = 0.0f, sinPhiM, cosPhiM, alphaSqr;
     if (d.type != DISTR_PHONG) {
         if (distr_iso(d)) {
@@ -214,8 +216,8 @@ __device__ __noinline__ f3 distr_sample_all(const Distr &d, float sx, float sy, 
     return mk(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
 }
 
-__device__ __noinline__ void distr_sample_visible11(const Distr &d, float thetaI, float sx, float sy,
-                                                    float &slx, float &sly) {   // :573-670
+__device__ __forceinline__ void distr_sample_visible11_impl(Distr d, float thetaI, float sx, float sy,
+                                                           float &slx, float &sly) {   // :573-670
     const float SQRT_PI_INV = 1 / dsqrt(D_PI);
     if (d.type == DISTR_BECKMANN) {
         if (thetaI < 1e-4f) {
@@ -272,6 +274,20 @@ __device__ __noinline__ void distr_sample_visible11(const Distr &d, float thetaI
     sly = S * z * dsqrt(1.0f + slx * slx);
 }
 
+// out-of-line entry points return their results by value (no stack round trip)
+struct F2 { float x, y; };
+struct MPdf { f3 m; float pdf; };
+__device__ __noinline__ F2 distr_sample_visible11(Distr d, float thetaI, float sx, float sy) {
+    F2 r;
+    distr_sample_visible11_impl(d, thetaI, sx, sy, r.x, r.y);
+    return r;
+}
+__device__ __noinline__ MPdf distr_sample_all(Distr d, float sx, float sy) {
+    MPdf r;
+    r.m = distr_sample_all_impl(d, sx, sy, r.pdf);
+    return r;
+}
+
 __device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float sx, float sy) {  // :421-460
     f3 wi = normalize(mk(d.alphaU * _wi.x, d.alphaV * _wi.y, _wi.z));
     float theta = 0, phi = 0;
@@ -281,8 +297,8 @@ __device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float
     }
     float sinPhi, cosPhi;
     d_sincos(phi, &sinPhi, &cosPhi);
-    float slx, sly;
-    distr_sample_visible11(d, theta, sx, sy, slx, sly);
+    const F2 sl = distr_sample_visible11(d, theta, sx, sy);
+    const float slx = sl.x, sly = sl.y;
     float nx = cosPhi * slx - sinPhi * sly;
     float ny = sinPhi * slx + cosPhi * sly;
     nx *= d.alphaU;
@@ -305,7 +321,9 @@ __device__ __forceinline__ f3 distr_sample(const Distr &d, f3 wi, float sx, floa
         pdf = distr_pdf_visible(d, wi, m);
         return m;
     }
-    return distr_sample_all(d, sx, sy, pdf);
+    const MPdf r = distr_sample_all(d, sx, sy);
+    pdf = r.pdf;
+    return r.m;
 }
 __device__ __forceinline__ void distr_scale_alpha(Distr &d, float v) {              // :181-186
     d.alphaU *= v; d.alphaV *= v;
@@ -346,9 +364,10 @@ __device__ __forceinline__ f3 refract_v(f3 wi, f3 n, float eta, float cosThetaT)
 }
 
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ f3 ld3(const __attribute__((address_space(1))) float *p) { return mk(p[0], p[1], p[2]); }
 
 // ---- BSDF::eval / pdf / sample --------------------------------------------
-BSDF_CALL f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
+BSDF_CALL f3 bsdf_eval(GBsdf &b, f3 wi, f3 wo) {
     const f3 zero = mk(0, 0, 0);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
         if (wi.z <= 0 || wo.z <= 0) return zero;
@@ -392,7 +411,7 @@ BSDF_CALL f3 bsdf_eval(const MtsgBsdf &b, f3 wi, f3 wo) {
     return mul(ld3(b.spec_t), fabsf(value * factor * factor));
 }
 
-BSDF_CALL float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
+BSDF_CALL float bsdf_pdf(GBsdf &b, f3 wi, f3 wo) {
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
@@ -431,7 +450,7 @@ BSDF_CALL float bsdf_pdf(const MtsgBsdf &b, f3 wi, f3 wo) {
 // the caller, which draws it from the sampler only for that BSDF.
 struct BSample { f3 wo; f3 weight; float pdf; float eta; int sampledType; };
 
-BSDF_CALL BSample bsdf_sample(const MtsgBsdf &b, f3 wi, float sx, float sy, float u1d) {
+BSDF_CALL BSample bsdf_sample(GBsdf &b, f3 wi, float sx, float sy, float u1d) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150

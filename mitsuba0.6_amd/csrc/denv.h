@@ -10,6 +10,9 @@
 #include "layout.h"
 
 typedef __attribute__((address_space(1))) const MtsgEnv glb_env;
+typedef __attribute__((address_space(1))) const float glb_f32;
+typedef unsigned int env_u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const env_u2 glb_u2;
 
 __device__ __forceinline__ float half_bits_to_float(uint32_t h) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
@@ -23,7 +26,7 @@ __device__ __forceinline__ f3 env_texel(glb_env *E, int level, int x, int y) {
         if (x < 0) x += w;
     }
     if (y < 0 || y >= h) y = y < 0 ? 0 : (y > h - 1 ? h - 1 : y);
-    const uint2 raw = *reinterpret_cast<const uint2 *>(E->texels + 4 * ((size_t)E->loff[level] + (size_t)y * w + x));
+    const env_u2 raw = ((glb_u2 *)(uintptr_t)E->texels)[(size_t)E->loff[level] + (size_t)y * w + x];
     return mk(half_bits_to_float(raw.x & 0xffffu), half_bits_to_float(raw.x >> 16), half_bits_to_float(raw.y & 0xffffu));
 }
 
@@ -195,7 +198,7 @@ __device__ __forceinline__ bool env_bsphere(glb_env *E, f3 ro, f3 d, float &near
 }
 
 // sampleReuse of the envmap's float CDFs (envmap.cpp:687-692)
-__device__ __forceinline__ uint32_t env_sample_reuse(const float *__restrict__ cdf, uint32_t size, float &sample) {
+__device__ __forceinline__ uint32_t env_sample_reuse(glb_f32 *__restrict__ cdf, uint32_t size, float &sample) {
     uint32_t lo = 0, hi = size + 1;                        // std::lower_bound
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -216,10 +219,10 @@ __device__ __forceinline__ float interval_to_tent(float s) {   // warp.cpp:143-1
 
 // EnvironmentMap::sampleDirect (envmap.cpp:516-543) + internalSampleDirection
 // (envmap.cpp:567-603): returns value/pdf; pdf = 0 on failure
-__device__ __noinline__ f3 env_sample_direct(glb_env *E, f3 ref, float sx, float sy, f3 &dOut, float &dist, float &pdfOut) {
+__device__ __forceinline__ f3 env_sample_direct_impl(glb_env *E, f3 ref, float sx, float sy, f3 &dOut, float &dist, float &pdfOut) {
     const uint32_t W = (uint32_t)E->w0, H = (uint32_t)E->h0;
-    const uint32_t row = env_sample_reuse(E->cdf_rows, H, sy);
-    const uint32_t col = env_sample_reuse(E->cdf_cols + (size_t)row * (W + 1), W, sx);
+    const uint32_t row = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_rows, H, sy);
+    const uint32_t col = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_cols + (size_t)row * (W + 1), W, sx);
     const float posx = (float)col + interval_to_tent(sx), posy = (float)row + interval_to_tent(sy);
     const int xPos = (int)floorf(posx), yPos = (int)floorf(posy);
     const float dx1 = posx - (float)xPos, dx2 = 1.0f - dx1, dy1 = posy - (float)yPos, dy2 = 1.0f - dy1;
@@ -228,7 +231,7 @@ __device__ __noinline__ f3 env_sample_direct(glb_env *E, f3 ref, float sx, float
     const f3 value = mul(add(value1, value2), E->scale);
     const int y0c = yPos < 0 ? 0 : (yPos > (int)H - 1 ? (int)H - 1 : yPos);
     const int y1c = yPos + 1 < 0 ? 0 : (yPos + 1 > (int)H - 1 ? (int)H - 1 : yPos + 1);
-    float pdf = (env_lum(value1) * E->row_weights[y0c] + env_lum(value2) * E->row_weights[y1c]) * E->normalization;
+    float pdf = (env_lum(value1) * ((glb_f32 *)(uintptr_t)E->row_weights)[y0c] + env_lum(value2) * ((glb_f32 *)(uintptr_t)E->row_weights)[y1c]) * E->normalization;
     float sinPhi, cosPhi, sinTheta, cosTheta;
     d_sincos(E->pixel_x * (posx + 0.5f), &sinPhi, &cosPhi);
     d_sincos(E->pixel_y * (posy + 0.5f), &sinTheta, &cosTheta);
@@ -260,6 +263,15 @@ __device__ __noinline__ float env_pdf_direction(glb_env *E, f3 dw) {
     const float sinTheta = safe_sqrt(1 - d.y * d.y);
     const int y0c = yPos < 0 ? 0 : (yPos > H - 1 ? H - 1 : yPos);
     const int y1c = yPos + 1 < 0 ? 0 : (yPos + 1 > H - 1 ? H - 1 : yPos + 1);
-    return (env_lum(value1) * E->row_weights[y0c] + env_lum(value2) * E->row_weights[y1c]) * E->normalization /
+    return (env_lum(value1) * ((glb_f32 *)(uintptr_t)E->row_weights)[y0c] + env_lum(value2) * ((glb_f32 *)(uintptr_t)E->row_weights)[y1c]) * E->normalization /
            smax(fabsf(sinTheta), D_EPSILON);
+}
+
+struct EnvSample { f3 value, d; float dist, pdf; };
+__device__ __noinline__ EnvSample env_sample_direct(glb_env *E, f3 ref, float sx, float sy) {
+    EnvSample r;
+    r.d = mk(0, 0, 1);
+    r.dist = 0.0f;
+    r.value = env_sample_direct_impl(E, ref, sx, sy, r.d, r.dist, r.pdf);
+    return r;
 }

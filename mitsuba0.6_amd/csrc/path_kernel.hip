@@ -815,7 +815,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     endPath = true;
                 } else {
                     const MtsgShape &sh = S.shapes[P.its.shape];
-                    const MtsgBsdf &bsdf = S.bsdfs[sh.bsdf];
+                    GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
                     if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
                         P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
                     if ((P.depth >= L.max_depth && L.max_depth > 0) ||
@@ -835,7 +835,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             float pdf = 0.0f, dist = 0.0f;
                             if (ENV && e.type == MTSG_EMITTER_ENVMAP) {
 #ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
-                                value = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey, dd, dist, pdf);
+                                const EnvSample es = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey);
+                                value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
 #endif
                             } else {
                             // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
