@@ -39,9 +39,9 @@ class BSDF:
     sampleVisible: bool = True
     specularReflectance: tuple = (1.0, 1.0, 1.0)
     specularTransmittance: tuple = (1.0, 1.0, 1.0)
-    eta: tuple = (0.0, 0.0, 0.0)       # roughconductor RGB eta (see conductors.py)
-    k: tuple = (1.0, 1.0, 1.0)
-    material: Optional[str] = None
+    eta: Optional[tuple] = None        # roughconductor: explicit RGB eta/k override `material`
+    k: Optional[tuple] = None
+    material: Optional[str] = 'Cu'     # roughconductor.cpp:174 default
     extEta: object = 'air'
     intIOR: object = 'bk7'
     extIOR: object = 'air'
@@ -69,16 +69,11 @@ class BSDF:
         d.specular_reflectance[:] = self.specularReflectance
         d.specular_transmittance[:] = self.specularTransmittance
         if self.type == 'roughconductor':
-            if self.material is not None and self.material.lower() == 'none':
-                eta, k = (0.0, 0.0, 0.0), (1.0, 1.0, 1.0)
-            elif self.material is not None:
-                raise NotImplementedError(
-                    "roughconductor 'material' lookup (data/ior/*.spd -> RGB) is host-side and not "
-                    "implemented; pass explicit RGB 'eta'/'k' with material=None")
-            else:
-                eta, k = self.eta, self.k
-            d.eta[:] = eta
-            d.k[:] = k
+            # intEta/intK from the material, overridden by explicit 'eta'/'k' (roughconductor.cpp:172-190)
+            from .conductors import conductor_rgb
+            eta, k = conductor_rgb(self.material or 'Cu')
+            d.eta[:] = self.eta if self.eta is not None else eta
+            d.k[:] = self.k if self.k is not None else k
         d.ext_eta = lookup_ior(self.extEta)
         d.int_ior = lookup_ior(self.intIOR)
         d.ext_ior = lookup_ior(self.extIOR)

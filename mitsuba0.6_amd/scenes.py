@@ -53,9 +53,8 @@ def _quads_mesh(quads, inward=True, center=_CENTER, uv=False):
     return p, i
 
 
-# RGB complex IOR of copper (linear sRGB primaries; used as explicit 'eta'/'k'
-# properties -- the reference's named-material .spd -> RGB conversion is a
-# host-side step outside the hot path)
+# an explicit RGB complex IOR (the 'eta'/'k' override path); named materials
+# come from conductors.py
 CU_ETA = (0.200438, 0.924033, 1.10221)
 CU_K = (3.91295, 2.45285, 2.14219)
 
@@ -73,6 +72,8 @@ def rough_materials():
         BSDF('roughconductor', distribution='ggx', alphaU=0.05, alphaV=0.4, material=None, eta=CU_ETA, k=CU_K),
         BSDF('roughdielectric', distribution='beckmann', alphaU=0.3, alphaV=0.08, intIOR=1.5),
         BSDF('roughconductor', distribution='phong', alphaU=0.1, alphaV=0.3, material=None, eta=CU_ETA, k=CU_K),
+        BSDF('roughconductor', distribution='ggx', alpha=0.15, material='Au'),
+        BSDF('roughconductor', distribution='beckmann', alpha=0.2, material='Al', extEta=1.33),
     ]
 
 
@@ -167,7 +168,7 @@ def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env
                blob=(236, 148), area_light=False, env_weight=1.0):
     """Config C3: a ~69k-triangle object in roughconductor GGX alpha=0.1 (copper) on a
     diffuse checker ground, lit only by a 1024x512 environment map."""
-    cu = BSDF('roughconductor', distribution='ggx', alpha=0.1, material=None, eta=CU_ETA, k=CU_K)
+    cu = BSDF('roughconductor', distribution='ggx', alpha=0.1, material='Cu')
     g0 = BSDF('diffuse', reflectance=(0.4, 0.4, 0.4))
     g1 = BSDF('diffuse', reflectance=(0.15, 0.15, 0.15))
     bsdfs = [cu, g0, g1]
