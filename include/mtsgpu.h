@@ -134,7 +134,9 @@ typedef struct {
     int32_t has_alpha;              /* film has an alpha channel (EOpacity)        */
     int32_t rfilter;                /* MTSGPU_RFILTER_*                            */
     float rfilter_param;            /* box: radius (0.5); gaussian: stddev (0.5)   */
-    /* pixel window rendered by this call (image coordinates, crop = film) */
+    /* the film's crop window (hdrfilm cropOffsetX/Y, cropWidth/Height; film.cpp:
+       35-43), image coordinates: the pixels rendered, and max(width, height)
+       sets the Sobol resolution (Integrator::configureSampler, integrator.cpp:37-41) */
     uint32_t x0, y0, width, height;
     /* row interleave for tile sharding: render rows y with
        ((y - y0) / row_block) % row_stride == row_phase (stride 1 = all rows) */

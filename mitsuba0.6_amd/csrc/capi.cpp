@@ -230,7 +230,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     std::string err;
     if (mtsg_configure_filter(P->rfilter, P->rfilter_param, L.filter, err)) return fail(ctx, MTSGPU_EINVAL, err);
     // SobolSampler::setFilmResolution(cropSize, bucketed = true) (sobol.cpp:147-158)
-    const uint32_t mx = std::max(H.film_w, H.film_h);
+    // the render window is the film's crop window: cropSize drives the sampler
+    // (Integrator::configureSampler, integrator.cpp:37-41)
+    const uint32_t mx = std::max(P->width, P->height);
     uint32_t r = mx - 1;
     r |= r >> 1; r |= r >> 2; r |= r >> 4; r |= r >> 8; r |= r >> 16; r += 1;
     uint32_t m = 0;

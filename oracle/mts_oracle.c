@@ -2285,7 +2285,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
         const int px = (int)P->x0 + lx, py = (int)P->y0 + ly;
         if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
         Sampler smp;
-        sampler_init(&smp, P->scramble, (uint32_t)W, (uint32_t)H);
+        sampler_init(&smp, P->scramble, P->width, P->height);   /* crop size (integrator.cpp:37-41) */
         sampler_generate(&smp, px, py);
         Counters C = {0, 0, 0, 0};
         for (uint32_t j = 0; j < P->spp; ++j) {
