@@ -89,7 +89,7 @@ class Context:
         """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict)."""
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
-        x0, y0, w, h = window if window else (0, 0, W, H)
+        x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
         if traversal_stats:
             p.flags |= abi.FLAG_TRAVERSAL_STATS
@@ -105,7 +105,7 @@ class Context:
     def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0)):
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
-        x0, y0, w, h = window if window else (0, 0, W, H)
+        x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
         st = abi.Stats()
         self._check(self.L.mtsgpu_render_device(self.h, C.byref(p), C.c_void_p(film_ptr),

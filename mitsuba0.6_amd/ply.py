@@ -157,3 +157,28 @@ def load_ply(path, toWorld=None, bsdf=-1, emitter=-1, faceNormals=False, flipNor
     idx = np.asarray(tris, np.uint32)
     return Mesh(pos, idx, normals=nrm, texcoords=uv, bsdf=bsdf, emitter=emitter, faceNormals=faceNormals,
                 flipNormals=flipNormals, name=name)
+
+
+def write_ply(path, mesh):
+    """Binary little-endian PLY of a Mesh (positions, optional normals/texcoords, triangles)."""
+    P = np.asarray(mesh.positions, '<f4')
+    cols = [P]
+    props = ['x', 'y', 'z']
+    if mesh.normals is not None:
+        cols.append(np.asarray(mesh.normals, '<f4'))
+        props += ['nx', 'ny', 'nz']
+    if mesh.texcoords is not None:
+        cols.append(np.asarray(mesh.texcoords, '<f4'))
+        props += ['u', 'v']
+    V = np.ascontiguousarray(np.concatenate(cols, axis=1), '<f4')
+    idx = np.asarray(mesh.indices, '<i4')
+    head = ['ply', 'format binary_little_endian 1.0', 'element vertex %d' % len(P)]
+    head += ['property float %s' % p for p in props]
+    head += ['element face %d' % len(idx), 'property list uchar int vertex_indices', 'end_header']
+    faces = np.empty(len(idx), np.dtype([('c', 'u1'), ('i', '<i4', (3,))]))
+    faces['c'] = 3
+    faces['i'] = idx
+    with open(path, 'wb') as fh:
+        fh.write(('\n'.join(head) + '\n').encode())
+        fh.write(V.tobytes())
+        fh.write(faces.tobytes())

@@ -225,6 +225,7 @@ class PathIntegrator:
     rfilter: str = 'gaussian'      # film default (film.cpp:93)
     rfilterParam: float = 0.5      # box radius / gaussian stddev
     hasAlpha: bool = False         # hdrfilm pixelFormat default "rgb" (hdrfilm.cpp:216)
+    crop: Optional[tuple] = None   # hdrfilm crop window (x0, y0, w, h) (film.cpp:35-43); None = whole film
 
     def __post_init__(self):
         if self.rrDepth <= 0:

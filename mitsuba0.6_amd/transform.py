@@ -56,6 +56,14 @@ class Transform:
     def __init__(self, m=None, inv=None):
         self.m = np.eye(4, dtype=f32) if m is None else np.asarray(m, f32).copy()
         self.inv = np.eye(4, dtype=f32) if inv is None else np.asarray(inv, f32).copy()
+        # XML steps that built this transform (None once composed arbitrarily);
+        # lets the scene writer reproduce the exact matrix *and* inverse
+        self.steps = [] if m is None and inv is None else None
+
+    def _then(self, t, step):
+        r = t * self
+        r.steps = None if self.steps is None else self.steps + [step]
+        return r
 
     def __mul__(self, t):                           # transform.cpp:28-31
         return Transform(_matmul(self.m, t.m), _matmul(t.inv, self.inv))
@@ -109,18 +117,20 @@ class Transform:
 
     # XML-style builders: each step left-multiplies (scenehandler.cpp:352-439)
     def translate(self, x, y, z):
-        return Transform.translate_(x, y, z) * self
+        return self._then(Transform.translate_(x, y, z), ('translate', {'x': x, 'y': y, 'z': z}))
 
     def scale(self, x, y=None, z=None):
         if y is None:
             y = z = x
-        return Transform.scale_(x, y, z) * self
+        return self._then(Transform.scale_(x, y, z), ('scale', {'x': x, 'y': y, 'z': z}))
 
     def rotate(self, axis, angle):
-        return Transform.rotate_(axis, angle) * self
+        return self._then(Transform.rotate_(axis, angle),
+                          ('rotate', {'x': axis[0], 'y': axis[1], 'z': axis[2], 'angle': angle}))
 
     def look_at(self, origin, target, up):
-        return Transform.look_at_(origin, target, up) * self
+        return self._then(Transform.look_at_(origin, target, up),
+                          ('lookat', {'origin': tuple(origin), 'target': tuple(target), 'up': tuple(up)}))
 
     def apply_points(self, p):
         """Transform::operator()(Point) (transform.h:108-125), row-wise over (n, 3)."""

@@ -65,7 +65,7 @@ def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row
     m = mitsuba_amd()
     L = lib()
     W, H = scene.sensor.width, scene.sensor.height
-    x0, y0, w, h = window if window else (0, 0, W, H)
+    x0, y0, w, h = window if window else (getattr(integ, 'crop', None) or (0, 0, W, H))
     p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
     b = m.film_border(integ.rfilter, integ.rfilterParam)
     film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)

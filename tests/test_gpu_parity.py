@@ -127,3 +127,15 @@ def test_atrium_bitexact(gpu_ctx, oracle):
     film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1, threads=8)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
+def test_xml_scene_bitexact(gpu_ctx, oracle, tmp_path):
+    """A scene written to Mitsuba XML (+PLY/PFM) and loaded back renders on the
+    GPU bit-identically to the oracle."""
+    from mitsuba_amd.xmlscene import load_scene, save_scene
+    sc, it = scenes.build('C3', width=32, height=18, spp=4, env_size=(64, 32), blob=(24, 16), area_light=True)
+    sc2, it2 = load_scene(save_scene(sc, it, str(tmp_path)))
+    gpu_ctx.upload(sc2)
+    film_g, smp_g, _ = gpu_ctx.render(it2, samples=True)
+    film_o, smp_o, _ = oracle.render(sc2, it2, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
