@@ -190,6 +190,29 @@ int mtsgpu_render(mtsgpu_ctx *ctx, const mtsgpu_render_params *params,
  * and the stream has been synchronised. */
 int mtsgpu_render_device(mtsgpu_ctx *ctx, const mtsgpu_render_params *params,
                          float *film_device, void *stream, mtsgpu_stats *stats);
+/* hdrfilm develop (HDRFilm::develop, src/films/hdrfilm.cpp:481-495 ->
+ * Bitmap::convert, src/libcore/fmtconv.cpp:955-1030, 1137-1160): divides the
+ * film interior by its weights (invWeight = w != 0 ? 1/w : w) and converts it
+ * to `pixel_format` / `component_format`.  Output: (film_height-2*border) rows
+ * of (film_width-2*border) pixels, channels interleaved in the order the
+ * pixel format names them, components of 2 (float16) or 4 bytes.
+ * `multiplier` = 1 for Film::develop (Bitmap::convert's argument). */
+enum { MTSGPU_PIX_LUMINANCE = 0, MTSGPU_PIX_LUMINANCE_ALPHA = 1, MTSGPU_PIX_RGB = 2, MTSGPU_PIX_RGBA = 3,
+       MTSGPU_PIX_XYZ = 4, MTSGPU_PIX_XYZA = 5 };
+enum { MTSGPU_COMP_FLOAT16 = 0, MTSGPU_COMP_FLOAT32 = 1, MTSGPU_COMP_UINT32 = 2 };
+typedef struct {
+    uint32_t film_width, film_height;   /* the rendered film incl. borders (W+2b, H+2b) */
+    uint32_t border;                    /* b                                             */
+    int32_t pixel_format;               /* MTSGPU_PIX_*                                  */
+    int32_t component_format;           /* MTSGPU_COMP_*                                 */
+    float multiplier;
+} mtsgpu_develop_params;
+/* `film_device` / `out_device` are device pointers; `stream` a hipStream_t
+ * (NULL: the context's stream).  Returns after the stream is synchronised. */
+int mtsgpu_develop_device(mtsgpu_ctx *ctx, const mtsgpu_develop_params *params, const float *film_device,
+                          void *out_device, void *stream);
+/* Same from and to host memory (stages both through the context's buffers). */
+int mtsgpu_develop(mtsgpu_ctx *ctx, const mtsgpu_develop_params *params, const float *film, void *out);
 /* Diagnostics (tests): device arithmetic probe -- for each i, out[8i..8i+7] =
  * {a/b, sqrt|a|, sin a, cos a, acos(clamp a), atan2(a,b), exp(-|a|), a*b+a}
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */

@@ -17,6 +17,8 @@ EMITTER_AREA, EMITTER_ENVMAP = 0, 1
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 SAMPLE_RECORD_FLOATS = 8
+PIX_LUMINANCE, PIX_LUMINANCE_ALPHA, PIX_RGB, PIX_RGBA, PIX_XYZ, PIX_XYZA = 0, 1, 2, 3, 4, 5
+COMP_FLOAT16, COMP_FLOAT32, COMP_UINT32 = 0, 1, 2
 
 _f3 = C.c_float * 3
 _f16 = C.c_float * 16
@@ -68,6 +70,11 @@ class RenderParams(C.Structure):
 
 
 FLAG_TRAVERSAL_STATS = 1
+
+
+class DevelopParams(C.Structure):
+    _fields_ = [('film_width', C.c_uint32), ('film_height', C.c_uint32), ('border', C.c_uint32),
+                ('pixel_format', C.c_int32), ('component_format', C.c_int32), ('multiplier', C.c_float)]
 
 
 class Stats(C.Structure):

@@ -25,6 +25,9 @@ hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
+hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
+                               hipStream_t s);
+int mtsg_develop_channels(int pixel_format);
 
 namespace {
 
@@ -62,6 +65,7 @@ struct mtsgpu_ctx {
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights;
     DevBuf film_own, film_spill, samples, counters, contrib;
+    DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
 };
 
 namespace {
@@ -372,6 +376,55 @@ int mtsgpu_render_device(mtsgpu_ctx *ctx, const mtsgpu_render_params *params, fl
     return render_impl(ctx, params, nullptr, film_device, nullptr, (hipStream_t)stream, stats);
 }
 
+// hdrfilm develop (film_kernel.hip)
+namespace {
+int develop_check(mtsgpu_ctx *ctx, const mtsgpu_develop_params *P, size_t *out_bytes) {
+    if (!ctx) return MTSGPU_EINVAL;
+    if (!P) return fail(ctx, MTSGPU_EINVAL, "develop params are NULL");
+    const int ch = mtsg_develop_channels(P->pixel_format);
+    if (!ch) return fail(ctx, MTSGPU_EINVAL, "develop: unknown pixel format");
+    if (P->component_format < MTSGPU_COMP_FLOAT16 || P->component_format > MTSGPU_COMP_UINT32)
+        return fail(ctx, MTSGPU_EINVAL, "develop: unknown component format");
+    if (P->film_width <= 2 * P->border || P->film_height <= 2 * P->border)
+        return fail(ctx, MTSGPU_EINVAL, "develop: film smaller than its borders");
+    const size_t n = (size_t)(P->film_width - 2 * P->border) * (P->film_height - 2 * P->border);
+    *out_bytes = n * ch * (P->component_format == MTSGPU_COMP_FLOAT16 ? 2 : 4);
+    return MTSGPU_OK;
+}
+}  // namespace
+
+int mtsgpu_develop_device(mtsgpu_ctx *ctx, const mtsgpu_develop_params *P, const float *film_device,
+                          void *out_device, void *stream) {
+    size_t ob = 0;
+    int rc = develop_check(ctx, P, &ob);
+    if (rc != MTSGPU_OK) return rc;
+    if (!film_device || !out_device) return fail(ctx, MTSGPU_EINVAL, "develop: NULL buffer");
+    (void)hipSetDevice(ctx->device);
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    hipError_t e = mtsg_launch_develop(*P, film_device, out_device, ctx->num_cus, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "develop");
+}
+
+int mtsgpu_develop(mtsgpu_ctx *ctx, const mtsgpu_develop_params *P, const float *film, void *out) {
+    size_t ob = 0;
+    int rc = develop_check(ctx, P, &ob);
+    if (rc != MTSGPU_OK) return rc;
+    if (!film || !out) return fail(ctx, MTSGPU_EINVAL, "develop: NULL buffer");
+    (void)hipSetDevice(ctx->device);
+    const size_t ib = (size_t)P->film_width * P->film_height * 5 * sizeof(float);
+    hipError_t e;
+    if ((e = ctx->dev_in.ensure(ib)) != hipSuccess || (e = ctx->dev_out.ensure(ob)) != hipSuccess)
+        return hip_fail(ctx, e, "develop buffers");
+    hipStream_t s = ctx->stream;
+    if ((e = hipMemcpyAsync(ctx->dev_in.p, film, ib, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = mtsg_launch_develop(*P, (const float *)ctx->dev_in.p, ctx->dev_out.p, ctx->num_cus, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(out, ctx->dev_out.p, ob, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(ctx, e, "develop");
+    return MTSGPU_OK;
+}
+
 const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() : g_create_error.c_str(); }
 
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
@@ -379,7 +432,9 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
-                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib};
+                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
+                      &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights,
+                      &ctx->dev_in, &ctx->dev_out};
     for (DevBuf *b : bufs) b->release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);

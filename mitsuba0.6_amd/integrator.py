@@ -27,7 +27,7 @@ class MtsgpuError(RuntimeError):
 
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
-           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info']
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device']
 
 _lib = None
 
@@ -52,6 +52,8 @@ def load_library(path=None):
     L.mtsgpu_destroy.argtypes = [C.c_void_p]
     L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
+    L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
+    L.mtsgpu_develop_device.argtypes = [C.c_void_p, P(abi.DevelopParams), C.c_void_p, C.c_void_p, C.c_void_p]
     if L.mtsgpu_abi_version() != 1:
         raise NativeUnavailable('ABI version mismatch')
     if path is None:
@@ -111,6 +113,24 @@ class Context:
         self._check(self.L.mtsgpu_render_device(self.h, C.byref(p), C.c_void_p(film_ptr),
                                                  C.c_void_p(stream_ptr) if stream_ptr else None, C.byref(st)))
         return st.as_dict()
+
+    def develop(self, film, border, hdrfilm):
+        """hdrfilm develop on the device (mtsgpu_develop): `film` (H+2b, W+2b, 5)
+        float32 host array -> (H, W, C) in hdrfilm's component dtype."""
+        film = np.ascontiguousarray(film, np.float32)
+        if film.ndim != 3 or film.shape[2] != 5:
+            raise ValueError('develop: film must be (H+2b, W+2b, 5) float32')
+        p = hdrfilm.develop_params(film.shape, border)
+        out = hdrfilm.output_array(film.shape, border)
+        self._check(self.L.mtsgpu_develop(self.h, C.byref(p), abi.fptr(film), out.ctypes.data_as(C.c_void_p)))
+        return out
+
+    def develop_device(self, film_ptr, film_shape, border, hdrfilm, out_ptr, stream_ptr=None):
+        """Same on device buffers (e.g. torch tensors' data_ptr()); the output
+        holds hdrfilm.output_array(film_shape, border).nbytes bytes."""
+        p = hdrfilm.develop_params(film_shape, border)
+        self._check(self.L.mtsgpu_develop_device(self.h, C.byref(p), C.c_void_p(film_ptr), C.c_void_p(out_ptr),
+                                                  C.c_void_p(stream_ptr) if stream_ptr else None))
 
     def debug_arith(self, a, b):
         a = np.ascontiguousarray(a, np.float32)

@@ -226,12 +226,16 @@ class PathIntegrator:
     rfilterParam: float = 0.5      # box radius / gaussian stddev
     hasAlpha: bool = False         # hdrfilm pixelFormat default "rgb" (hdrfilm.cpp:216)
     crop: Optional[tuple] = None   # hdrfilm crop window (x0, y0, w, h) (film.cpp:35-43); None = whole film
+    film: Optional['HDRFilm'] = None   # hdrfilm output format (film.py); None = the hdrfilm defaults
 
     def __post_init__(self):
         if self.rrDepth <= 0:
             raise ValueError("'rrDepth' must be set to a value greater than zero!")
         if self.maxDepth <= 0 and self.maxDepth != -1:
             raise ValueError("'maxDepth' must be set to -1 (infinite) or a value greater than zero!")
+        if self.film is None:
+            from .film import HDRFilm
+            self.film = HDRFilm()
 
     def params(self, width, height, x0=0, y0=0, w=None, h=None, row_block=0, row_stride=1, row_phase=0):
         p = abi.RenderParams()
@@ -254,12 +258,3 @@ def film_border(rfilter, param):
     import math
     radius = np.float32(param) + np.float32(1e-5) if rfilter == 'box' else np.float32(4) * np.float32(param)
     return int(math.ceil(np.float32(radius - np.float32(0.5))))
-
-
-def develop(film, border):
-    """Divide accumulated RGB by the filter weight (film develop); returns (H,W,3)."""
-    f = film[border:film.shape[0] - border, border:film.shape[1] - border]
-    w = f[..., 4:5]
-    with np.errstate(divide='ignore', invalid='ignore'):
-        rgb = np.where(w != 0, f[..., :3] / w, 0.0)
-    return rgb.astype(np.float32)

@@ -32,6 +32,7 @@ import xml.etree.ElementTree as ET
 
 import numpy as np
 
+from .film import HDRFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
 from .obj import load_obj, srgb_to_linear, strtof
 from .ply import load_ply
 from .scene import BSDF, Emitter, Mesh, PathIntegrator, Scene, Sensor
@@ -43,49 +44,6 @@ f32 = np.float32
 
 class SceneError(ValueError):
     pass
-
-
-# ---------------------------------------------------------------------------
-# images
-# ---------------------------------------------------------------------------
-def read_pfm(path):
-    """Bitmap::readPFM (libcore/bitmap.cpp:3764-3813): 'PF' RGB or 'Pf' luminance,
-    negative scale = little endian, |scale| != 1 multiplies, rows stored
-    bottom-up (flipped).  Returns (H, W, 3) float32."""
-    with open(path, 'rb') as fh:
-        data = fh.read()
-    if data[:2] not in (b'PF', b'Pf'):
-        raise SceneError('readPFM(): Invalid header!')
-    color = data[:2] == b'PF'
-    # header tokens separated by whitespace (pfmReadString)
-    pos, toks = 2, []
-    while len(toks) < 3:
-        while data[pos:pos + 1].isspace():
-            pos += 1
-        start = pos
-        while not data[pos:pos + 1].isspace():
-            pos += 1
-        toks.append(data[start:pos].decode())
-    pos += 1
-    w, h, scale = int(toks[0]), int(toks[1]), np.float32(float(toks[2]))
-    ch = 3 if color else 1
-    dt = '<f4' if scale <= 0 else '>f4'
-    img = np.frombuffer(data, dt, w * h * ch, pos).astype(np.float32).reshape(h, w, ch)
-    if abs(scale) != 1:
-        img = (img * np.float32(abs(scale))).astype(np.float32)
-    img = img[::-1].copy()
-    if ch == 1:
-        img = np.repeat(img, 3, axis=2)
-    return img
-
-
-def write_pfm(path, img):
-    """Bitmap::writePFM layout (little endian, bottom-up rows)."""
-    img = np.asarray(img, np.float32)
-    h, w = img.shape[:2]
-    with open(path, 'wb') as fh:
-        fh.write(b'PF\n%d %d\n-1\n' % (w, h))
-        fh.write(np.ascontiguousarray(img[::-1, :, :3], '<f4').tobytes())
 
 
 # ---------------------------------------------------------------------------
@@ -326,11 +284,9 @@ class XMLSceneLoader:
         if fn is None:
             raise SceneError('envmap: missing filename')
         path = self.resolve(fn)
-        if not path.lower().endswith('.pfm'):
-            raise NotImplementedError('envmap image format of "%s" (PFM is supported)' % fn)
         if p.get('gamma', 0) not in (0, 1):
             raise NotImplementedError('envmap gamma override')
-        return Emitter('envmap', bitmap=read_pfm(path), scale=float(p.get('scale', 1.0)),
+        return Emitter('envmap', bitmap=load_bitmap(path), scale=float(p.get('scale', 1.0)),
                        samplingWeight=float(p.get('samplingWeight', 1.0)), toWorld=p.get('toWorld'))
 
     def make_shapes(self, p):
@@ -462,15 +418,21 @@ class XMLSceneLoader:
         film = next((c for _, c in p.children if c.tag == 'film'), None)
         sampler = next((c for _, c in p.children if c.tag == 'sampler'), None)
         width, height = 768, 576
-        rfilter, rparam, has_alpha, crop = 'gaussian', 0.5, False, None
+        rfilter, rparam, has_alpha, crop, hdr = 'gaussian', 0.5, False, None, HDRFilm()
         if film is not None:
             if film.plugin != 'hdrfilm':
                 raise NotImplementedError('film "%s" (hdrfilm)' % film.plugin)
             width, height = film.get('width', 768), film.get('height', 576)
-            fmt = film.get('pixelFormat', 'rgb').lower()
-            if fmt not in ('rgb', 'rgba'):
-                raise NotImplementedError('hdrfilm pixelFormat "%s"' % fmt)
-            has_alpha = fmt == 'rgba'
+            try:
+                hdr = HDRFilm(fileFormat=film.get('fileFormat', 'openexr'), pixelFormat=film.get('pixelFormat', 'rgb'),
+                              componentFormat=film.get('componentFormat', 'float16'),
+                              channelNames=film.get('channelNames', ''), banner=film.get('banner', True),
+                              attachLog=film.get('attachLog', True))
+            except ValueError as e:
+                raise SceneError(str(e))
+            if film.get('highQualityEdges', False):
+                raise NotImplementedError('hdrfilm highQualityEdges=true (renders the border pixels outside the crop)')
+            has_alpha = hdr.hasAlpha
             crop = (film.get('cropOffsetX', 0), film.get('cropOffsetY', 0), film.get('cropWidth', width),
                     film.get('cropHeight', height))
             rf = next((c for _, c in film.children if c.tag == 'rfilter'), None)
@@ -511,6 +473,7 @@ class XMLSceneLoader:
         integ.sampleCount, integ.scramble = spp, scramble
         integ.rfilter, integ.rfilterParam, integ.hasAlpha = rfilter, rparam, has_alpha
         integ.crop = crop
+        integ.film = hdr
         return sensor, integ
 
 
@@ -601,7 +564,12 @@ def save_scene(scene, integ, directory, name='scene.xml'):
              '<integer name="scramble" value="%d"/></sampler>' % (integ.sampleCount, integ.scramble))
     L.append('    <film type="hdrfilm">')
     L.append('      <integer name="width" value="%d"/><integer name="height" value="%d"/>' % (s.width, s.height))
-    L.append('      <string name="pixelFormat" value="%s"/>' % ('rgba' if integ.hasAlpha else 'rgb'))
+    hf = integ.film or HDRFilm()
+    fmt = hf.pixel_format if hf.hasAlpha == bool(integ.hasAlpha) else ('rgba' if integ.hasAlpha else 'rgb')
+    L.append('      <string name="pixelFormat" value="%s"/>' % fmt)
+    L.append('      <string name="fileFormat" value="%s"/><string name="componentFormat" value="%s"/>'
+             % (hf.fileFormat, hf.componentFormat))
+    L.append('      <boolean name="banner" value="%s"/>' % str(bool(hf.banner)).lower())
     if integ.crop:
         x0, y0, w, h = integ.crop
         L.append('      <integer name="cropOffsetX" value="%d"/><integer name="cropOffsetY" value="%d"/>'

@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 STRUCTS = {'mtsgpu_bsdf_desc': abi.BsdfDesc, 'mtsgpu_emitter_desc': abi.EmitterDesc,
            'mtsgpu_mesh_desc': abi.MeshDesc, 'mtsgpu_sensor_desc': abi.SensorDesc,
            'mtsgpu_scene_desc': abi.SceneDesc, 'mtsgpu_render_params': abi.RenderParams,
-           'mtsgpu_stats': abi.Stats}
+           'mtsgpu_stats': abi.Stats, 'mtsgpu_develop_params': abi.DevelopParams}
 
 
 def test_struct_layout_matches_python_mirror(tmp_path):
