@@ -40,6 +40,9 @@ WORKLOADS = {
           'envmap only), path maxDepth=-1 rrDepth=5, sobol, box filter',
     'C4': 'C4: atrium (195k tris, 24 fluted columns, roughdielectric GGX a=0.2 eta=1.5 on ~30% of meshes, '
           'diffuse elsewhere, 4 area lights) 1280x720 256 spp, path maxDepth=-1 rrDepth=5, sobol, box filter',
+    'C5': 'C5: matpreview with the object in roughplastic GGX, checkerboard-textured alpha (0.05/0.3) -> '
+          '2D rough-transmittance slice (50 alpha x 100 theta) per shading point, 1024x512 envmap, 1024 spp, '
+          'path maxDepth=-1 rrDepth=5, sobol, box filter',
 }
 
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 1
+#define MTSGPU_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -52,7 +52,8 @@ enum {
 enum { /* BSDF plugins on the path (src/bsdfs) */
     MTSGPU_BSDF_DIFFUSE = 0,         /* diffuse.cpp         */
     MTSGPU_BSDF_ROUGHCONDUCTOR = 1,  /* roughconductor.cpp  */
-    MTSGPU_BSDF_ROUGHDIELECTRIC = 2  /* roughdielectric.cpp */
+    MTSGPU_BSDF_ROUGHDIELECTRIC = 2, /* roughdielectric.cpp */
+    MTSGPU_BSDF_ROUGHPLASTIC = 3     /* roughplastic.cpp + rtrans.h */
 };
 
 enum { /* MicrofacetDistribution::EType (src/bsdfs/microfacet.h:48-57) */
@@ -60,6 +61,18 @@ enum { /* MicrofacetDistribution::EType (src/bsdfs/microfacet.h:48-57) */
     MTSGPU_DISTR_GGX = 1,
     MTSGPU_DISTR_PHONG = 2
 };
+
+enum { /* Texture plugins a BSDF parameter may hold (src/textures) */
+    MTSGPU_TEX_NONE = 0,             /* the constant value of the parameter         */
+    MTSGPU_TEX_CHECKERBOARD = 1      /* checkerboard.cpp (Texture2D uv transform)   */
+};
+
+typedef struct {                    /* Texture2D (librender/texture.cpp:81-121)    */
+    int32_t type;                   /* MTSGPU_TEX_*                                */
+    float color0[3], color1[3];     /* checkerboard 'color0' (.4), 'color1' (.2)   */
+    float uoffset, voffset;         /* 'uoffset', 'voffset' (0)                    */
+    float uscale, vscale;           /* 'uscale'/'vscale' (default 'uvscale' = 1)   */
+} mtsgpu_texture_desc;
 
 typedef struct {
     int32_t type;                   /* MTSGPU_BSDF_*                               */
@@ -72,7 +85,16 @@ typedef struct {
     float specular_transmittance[3];/* roughdielectric (default 1)                 */
     float eta[3], k[3];             /* roughconductor: RGB eta/k, before /extEta   */
     float ext_eta;                  /* roughconductor 'extEta' (air = 1.000277)    */
-    float int_ior, ext_ior;         /* roughdielectric (bk7 = 1.5046, air)         */
+    float int_ior, ext_ior;         /* roughdielectric (bk7 = 1.5046, air);        */
+                                    /* roughplastic (polypropylene = 1.49, air)    */
+    /* roughplastic (roughplastic.cpp:197-300) */
+    float diffuse_reflectance[3];   /* 'diffuseReflectance' (default 0.5)          */
+    int32_t nonlinear;              /* 'nonlinear' (default 0)                     */
+    const void *rtrans_data;        /* the bytes of data/microfacet/<distr>.dat    */
+    uint64_t rtrans_bytes;          /* (RoughTransmittance, rtrans.h:46-150)       */
+    /* textured parameters; type NONE -> the constant field above is used */
+    mtsgpu_texture_desc reflectance_tex;   /* diffuse 'reflectance' / roughplastic 'diffuseReflectance' */
+    mtsgpu_texture_desc alpha_tex;         /* rough*: isotropic 'alpha' (value = texture average)       */
 } mtsgpu_bsdf_desc;
 
 enum { MTSGPU_EMITTER_AREA = 0, MTSGPU_EMITTER_ENVMAP = 1 };
@@ -178,6 +200,10 @@ typedef struct mtsgpu_ctx mtsgpu_ctx;
 int mtsgpu_create(int device, mtsgpu_ctx **out);
 /* Configure + upload a scene (copies everything; replaces any previous one). */
 int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene);
+/* Host-only (no device needed): run the configure() steps of upload_scene on
+ * `scene` and report the first error as the reference would raise it
+ * (Log(EError) message into msg[cap]).  Returns MTSGPU_OK or the error code. */
+int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap);
 /* Border size b of the film for the given filter parameters. */
 int mtsgpu_film_border(int32_t rfilter, float rfilter_param);
 /* Render the window into `film` (host memory, layout above).  `samples` may be

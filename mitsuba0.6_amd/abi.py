@@ -11,7 +11,9 @@ OK, EINVAL, EHIP, ENOMEM, ESTATE, EDIM, ECANCEL, ENODEV = 0, -1, -2, -3, -4, -5,
 STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTATE: 'ESTATE',
                 EDIM: 'EDIM', ECANCEL: 'ECANCEL', ENODEV: 'ENODEV'}
 
-BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC = 0, 1, 2
+BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC, BSDF_ROUGHPLASTIC = 0, 1, 2, 3
+TEX_NONE, TEX_CHECKERBOARD = 0, 1
+ABI_VERSION = 2
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP = 0, 1
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
@@ -24,13 +26,21 @@ _f3 = C.c_float * 3
 _f16 = C.c_float * 16
 
 
+class TextureDesc(C.Structure):
+    _fields_ = [('type', C.c_int32), ('color0', _f3), ('color1', _f3), ('uoffset', C.c_float),
+                ('voffset', C.c_float), ('uscale', C.c_float), ('vscale', C.c_float)]
+
+
 class BsdfDesc(C.Structure):
     _fields_ = [('type', C.c_int32), ('distribution', C.c_int32), ('sample_visible', C.c_int32),
                 ('ensure_energy_conservation', C.c_int32),
                 ('alpha_u', C.c_float), ('alpha_v', C.c_float),
                 ('reflectance', _f3), ('specular_reflectance', _f3), ('specular_transmittance', _f3),
                 ('eta', _f3), ('k', _f3), ('ext_eta', C.c_float),
-                ('int_ior', C.c_float), ('ext_ior', C.c_float)]
+                ('int_ior', C.c_float), ('ext_ior', C.c_float),
+                ('diffuse_reflectance', _f3), ('nonlinear', C.c_int32),
+                ('rtrans_data', C.c_void_p), ('rtrans_bytes', C.c_uint64),
+                ('reflectance_tex', TextureDesc), ('alpha_tex', TextureDesc)]
 
 
 class EmitterDesc(C.Structure):

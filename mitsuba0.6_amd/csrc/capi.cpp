@@ -64,6 +64,7 @@ struct mtsgpu_ctx {
     MtsgDeviceScene dscene;
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights;
+    DevBuf rtrans, texcoords;
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
 };
@@ -179,6 +180,9 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
             return hip_fail(ctx, e, "envmap upload");
         denv = (const MtsgEnv *)ctx->env.p;
     }
+    if ((!H.rtrans.empty() && (e = upload(ctx->rtrans, H.rtrans, s)) != hipSuccess) ||
+        (!H.texcoords.empty() && (e = upload(ctx->texcoords, H.texcoords, s)) != hipSuccess))
+        return hip_fail(ctx, e, "texture/table upload");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "scene upload sync");
     MtsgDeviceScene &D = ctx->dscene;
     std::memset(&D, 0, sizeof D);
@@ -199,10 +203,24 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     D.em_norm = H.em_norm;
     D.env = denv;
     D.env_emitter = H.env.emitter;
+    D.rtrans = H.rtrans.empty() ? nullptr : (const float *)ctx->rtrans.p;
+    D.texcoords = H.texcoords.empty() ? nullptr : (const float *)ctx->texcoords.p;
     for (int a = 0; a < 3; ++a) { D.aabb_min[a] = H.aabb_min[a]; D.aabb_max[a] = H.aabb_max[a]; }
     D.cam = H.cam;
     ctx->have_scene = true;
     return MTSGPU_OK;
+}
+
+int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap) {
+    if (!scene) return MTSGPU_EINVAL;
+    HostScene H;
+    std::string err;
+    int rc = mtsg_configure_scene(scene, H, err);
+    if (msg && cap) {
+        std::strncpy(msg, err.c_str(), cap - 1);
+        msg[cap - 1] = 0;
+    }
+    return rc;
 }
 
 int mtsgpu_film_border(int32_t rfilter, float rfilter_param) {
@@ -283,6 +301,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // large scenes are latency-bound: run 4 waves/SIMD when 4 blocks' traversal
     // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
     // LDS as the rest allows (the others are read through L1/L2)
+    L.ext = H.ext ? 1u : 0u;
     L.waves = 3;
     if (!L.scene_lds) {
         const size_t perBlock = (160u << 10) / 4;
@@ -434,6 +453,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights,
+                      &ctx->rtrans, &ctx->texcoords,
                       &ctx->dev_in, &ctx->dev_out};
     for (DevBuf *b : bufs) b->release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);

@@ -1,8 +1,12 @@
-// dbsdf.h -- device BSDFs of the path: diffuse, roughconductor, roughdielectric
-// and the MicrofacetDistribution they share (Beckmann, GGX, Phong/AS).
+// dbsdf.h -- device BSDFs of the path: diffuse, roughconductor, roughdielectric,
+// roughplastic and the MicrofacetDistribution they share (Beckmann, GGX,
+// Phong/AS), with checkerboard-textured reflectance / roughness.
 //
 //   src/bsdfs/diffuse.cpp:110-150        src/bsdfs/microfacet.h:67-670
 //   src/bsdfs/roughconductor.cpp:257-410 src/bsdfs/roughdielectric.cpp:270-615
+//   src/bsdfs/roughplastic.cpp:300-470   src/bsdfs/rtrans.h:179-260
+//   src/libcore/spline.cpp:23-60,236-304 src/textures/checkerboard.cpp
+//   src/librender/texture.cpp:112-121
 //   src/libcore/util.cpp:651-771 (Fresnel, reflect, refract)
 //   src/libcore/math.cpp:25-95 (erf, erfinv, hypot2)
 #pragma once
@@ -16,7 +20,7 @@ enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
 #else
 #define BSDF_CALL __device__ __noinline__
 #endif
-enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2 };
+enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2, BSDF_ROUGHPLASTIC = 3 };
 
 __device__ __forceinline__ float tan_theta(f3 v) {           // frame.h:117-122
     float temp = 1 - v.z * v.z;
@@ -366,17 +370,178 @@ __device__ __forceinline__ f3 refract_v(f3 wi, f3 n, float eta, float cosThetaT)
 __device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
 __device__ __forceinline__ f3 ld3(const __attribute__((address_space(1))) float *p) { return mk(p[0], p[1], p[2]); }
 
+struct BSample { f3 wo; f3 weight; float pdf; float eta; int sampledType; };
+
+// ---- textures (Texture2D::eval, texture.cpp:112-121; checkerboard.cpp) -----
+typedef const __attribute__((address_space(1))) MtsgTex GTex;
+typedef const __attribute__((address_space(1))) float glb_f32;
+
+// (int) of a float as x86-64 cvttss2si does it: out of range / NaN -> INT_MIN
+__device__ __forceinline__ int x86_f2i(float f) {
+    return (f > -2147483648.0f && f < 2147483648.0f) ? (int)f : (int)0x80000000u;
+}
+__device__ __forceinline__ int imodulo(int a, int b) { int r = a % b; return (r < 0) ? r + b : r; }   // math.h:42
+
+__device__ __forceinline__ f3 tex_eval(GTex &t, float u, float v) {
+    const float uu = u * t.uscale + t.uoff, vv = v * t.vscale + t.voff;
+    const int x = 2 * imodulo(x86_f2i(uu * 2), 2) - 1, y = 2 * imodulo(x86_f2i(vv * 2), 2) - 1;
+    return (x * y == 1) ? ld3(t.c0) : ld3(t.c1);
+}
+__device__ __forceinline__ float avg3(f3 s) { float r = 0.0f; r += s.x; r += s.y; r += s.z; return r * (1.0f / 3); }
+
+// reflectance / diffuseReflectance at the hit (texture or constant)
+template <bool EXT>
+__device__ __forceinline__ f3 bsdf_refl(GBsdf &b, float u, float v) {
+    if constexpr (EXT) { if (b.refl_tex.type) return tex_eval(b.refl_tex, u, v); }
+    return ld3(b.refl);
+}
+// the rough BSDF's distribution at the hit: m_alpha->eval(its).average() for a
+// textured alpha (MicrofacetDistribution(type, alpha, sampleVisible) clamps)
+template <bool EXT>
+__device__ __forceinline__ Distr bsdf_distr(GBsdf &b, float u, float v) {
+    if constexpr (EXT) {
+        if (b.alpha_tex.type) {
+            const float a = avg3(tex_eval(b.alpha_tex, u, v));
+            return distr_make(b.distr, a, a, b.sample_visible);
+        }
+    }
+    return distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+}
+
+// ---- RoughTransmittance on the eta-reduced tables (rtrans.h:179-260) -------
+// evalCubicInterp1D / 2D (spline.cpp:23-60, 236-304), extrapolate = false
+__device__ __forceinline__ float cubic1d(float x, glb_f32 *values, uint32_t size) {
+    if (!(x >= 0.0f && x <= 1.0f)) return 0.0f;
+    float t = ((x - 0.0f) * (float)(size - 1)) / (1.0f - 0.0f);
+    uint32_t k = (uint32_t)t;
+    if (k > size - 2) k = size - 2;
+    const float f0 = values[k], f1 = values[k + 1];
+    float d0, d1;
+    if (k > 0) d0 = 0.5f * (values[k + 1] - values[k - 1]);
+    else d0 = values[k + 1] - values[k];
+    if (k + 2 < size) d1 = 0.5f * (values[k + 2] - values[k]);
+    else d1 = values[k + 1] - values[k];
+    t = t - (float)k;
+    const float t2 = t * t, t3 = t2 * t;
+    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+}
+
+struct KnotW { uint32_t knot; float w[4]; };
+__device__ __forceinline__ bool cubic_weights(float p, uint32_t size, KnotW &k) {
+    if (!(p >= 0.0f && p <= 1.0f)) return false;
+    float t = ((p - 0.0f) * (float)(size - 1)) / (1.0f - 0.0f);
+    uint32_t kn = (uint32_t)t;
+    if (kn > size - 2) kn = size - 2;
+    k.knot = kn;
+    t = t - (float)kn;
+    const float t2 = t * t, t3 = t2 * t;
+    k.w[0] = 0.0f;
+    k.w[1] = 2 * t3 - 3 * t2 + 1;
+    k.w[2] = -2 * t3 + 3 * t2;
+    k.w[3] = 0.0f;
+    const float d0 = t3 - 2 * t2 + t, d1 = t3 - t2;
+    if (kn > 0) { k.w[2] += 0.5f * d0; k.w[0] -= 0.5f * d0; }
+    else { k.w[2] += d0; k.w[1] -= d0; }
+    if (kn + 2 < size) { k.w[3] += 0.5f * d1; k.w[1] -= 0.5f * d1; }
+    else { k.w[2] += d1; k.w[1] -= d1; }
+    return true;
+}
+
+__device__ __noinline__ float cubic2d(float px, float py, glb_f32 *values, uint32_t sx, uint32_t sy) {
+    KnotW kx, ky;
+    if (!cubic_weights(px, sx, kx)) return 0.0f;
+    if (!cubic_weights(py, sy, ky)) return 0.0f;
+    float result = 0.0f;
+    for (int y = -1; y <= 2; ++y) {
+        const float wy = ky.w[y + 1];
+        for (int x = -1; x <= 2; ++x) {
+            const float wxy = kx.w[x + 1] * wy;
+            if (wxy == 0) continue;
+            const size_t pos = (size_t)(ky.knot + y) * sx + kx.knot + x;
+            result += values[pos] * wxy;
+        }
+    }
+    return result;
+}
+
+// external table: eval(cosTheta, alpha) with m_etaFixed (rtrans.h:184-208)
+__device__ __forceinline__ float rt_eval(GBsdf &b, glb_f32 *rt, float cosTheta, float alpha) {
+    const float warpedCosTheta = d_powf(fabsf(cosTheta), 0.25f);
+    if (!(cosTheta >= 0)) return 0.f;
+    float result;
+    if (b.rt_alpha_fixed) {
+        result = cubic1d(warpedCosTheta, rt + b.rt_ext, (uint32_t)b.rt_theta);
+    } else {
+        const float warpedAlpha = d_powf((alpha - b.rt_alpha_min) / (b.rt_alpha_max - b.rt_alpha_min), 0.25f);
+        result = cubic2d(warpedCosTheta, warpedAlpha, rt + b.rt_ext, (uint32_t)b.rt_theta, (uint32_t)b.rt_alpha);
+    }
+    return smin(1.0f, smax(0.0f, result));
+}
+// internal table: evalDiffuse(alpha) with m_etaFixed (rtrans.h:236-247)
+__device__ __forceinline__ float rt_eval_diffuse(GBsdf &b, glb_f32 *rt, float alpha) {
+    const float warpedAlpha = d_powf((alpha - b.rt_alpha_min) / (b.rt_alpha_max - b.rt_alpha_min), 0.25f);
+    const float result = cubic1d(warpedAlpha, rt + b.rt_int, (uint32_t)b.rt_alpha);
+    return smin(1.0f, smax(0.0f, result));
+}
+
+// probSpecular of roughplastic's pdf()/sample() (roughplastic.cpp:371-378, 424-431)
+__device__ __forceinline__ float rp_prob_specular(GBsdf &b, glb_f32 *rt, float cosThetaI, float alpha) {
+    float probSpecular = 1 - rt_eval(b, rt, cosThetaI, alpha);
+    probSpecular = (probSpecular * b.spec_weight) /
+                   (probSpecular * b.spec_weight + (1 - probSpecular) * (1 - b.spec_weight));
+    return probSpecular;
+}
+
+// RoughPlastic::eval (roughplastic.cpp:300-345)
+__device__ __noinline__ f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
+    const Distr d = bsdf_distr<true>(b, u, v);
+    f3 result = mk(0, 0, 0);
+    {
+        const f3 H = normalize(add(wo, wi));
+        const float D = distr_eval(d, H);
+        float ct;
+        const float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
+        const float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+        const float value = F * D * G / (4.0f * wi.z);
+        result = add(result, mul(ld3(b.spec_r), value));
+    }
+    f3 diff = bsdf_refl<true>(b, u, v);
+    const float T12 = rt_eval(b, rt, wi.z, d.alphaU);
+    const float T21 = rt_eval(b, rt, wo.z, d.alphaU);
+    const float Fdr = 1 - rt_eval_diffuse(b, rt, d.alphaU);
+    if (b.nonlinear) diff = divv(diff, sub(mk(1.0f, 1.0f, 1.0f), mul(diff, Fdr)));
+    else diff = divs(diff, 1 - Fdr);
+    return add(result, mul(diff, D_INV_PI * wo.z * T12 * T21 * b.inv_eta2));
+}
+
+// RoughPlastic::pdf (roughplastic.cpp:347-393)
+__device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    const Distr d = bsdf_distr<true>(b, u, v);
+    const f3 H = normalize(add(wo, wi));
+    const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
+    const float probDiffuse = 1 - probSpecular;
+    const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+    const float prob = distr_pdf(d, wi, H);
+    float result = prob * dwh_dwo * probSpecular;
+    result += probDiffuse * (D_INV_PI * wo.z);
+    return result;
+}
+
 // ---- BSDF::eval / pdf / sample --------------------------------------------
-BSDF_CALL f3 bsdf_eval(GBsdf &b, f3 wi, f3 wo) {
+template <bool EXT>
+BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     const f3 zero = mk(0, 0, 0);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
         if (wi.z <= 0 || wo.z <= 0) return zero;
-        return mul(ld3(b.refl), D_INV_PI * wo.z);
+        return mul(bsdf_refl<EXT>(b, u, v), D_INV_PI * wo.z);
     }
+    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_eval(b, rt, wi, wo, u, v); }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:257-292
         if (wi.z <= 0 || wo.z <= 0) return zero;
         f3 H = normalize(add(wo, wi));
-        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        Distr d = bsdf_distr<EXT>(b, u, v);
         float D = distr_eval(d, H);
         if (D == 0) return zero;
         f3 F = mulv(fresnel_conductor_exact(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
@@ -394,7 +559,7 @@ BSDF_CALL f3 bsdf_eval(GBsdf &b, f3 wi, f3 wo) {
         H = normalize(add(wi, mul(wo, eta)));
     }
     H = mul(H, signum(H.z));
-    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+    Distr d = bsdf_distr<EXT>(b, u, v);
     float D = distr_eval(d, H);
     if (D == 0) return zero;
     float ct;
@@ -411,15 +576,17 @@ BSDF_CALL f3 bsdf_eval(GBsdf &b, f3 wi, f3 wo) {
     return mul(ld3(b.spec_t), fabsf(value * factor * factor));
 }
 
-BSDF_CALL float bsdf_pdf(GBsdf &b, f3 wi, f3 wo) {
+template <bool EXT>
+BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
     }
+    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf(b, rt, wi, wo, u, v); }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:294-319
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         f3 H = normalize(add(wo, wi));
-        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        Distr d = bsdf_distr<EXT>(b, u, v);
         if (b.sample_visible) return distr_eval(d, H) * distr_smithG1(d, wi, H) / (4.0f * wi.z);
         return distr_pdf(d, wi, H) / (4 * absdot(wo, H));
     }
@@ -436,7 +603,7 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, f3 wi, f3 wo) {
         dwh_dwo = (eta * eta * dot(wo, H)) / (sqrtDenom * sqrtDenom);
     }
     H = mul(H, signum(H.z));
-    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+    Distr d = bsdf_distr<EXT>(b, u, v);
     if (!b.sample_visible) distr_scale_alpha(d, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
     float prob = distr_pdf(d, mul(wi, signum(wi.z)), H);
     float ct;
@@ -448,9 +615,40 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, f3 wi, f3 wo) {
 // BSDF::sample(bRec, pdf, sample): roughdielectric consumes one more 1D sample
 // for the lobe choice (roughdielectric.cpp:554); it is passed in as `u1d` by
 // the caller, which draws it from the sampler only for that BSDF.
-struct BSample { f3 wo; f3 weight; float pdf; float eta; int sampledType; };
 
-BSDF_CALL BSample bsdf_sample(GBsdf &b, f3 wi, float sx, float sy, float u1d) {
+// RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458)
+__device__ __noinline__ BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v) {
+    BSample r;
+    r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
+    if (wi.z <= 0) return r;
+    bool choseSpecular = true;
+    const Distr d = bsdf_distr<true>(b, u, v);
+    const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
+    if (sy < probSpecular) {
+        sy /= probSpecular;
+    } else {
+        sy = (sy - probSpecular) / (1 - probSpecular);
+        choseSpecular = false;
+    }
+    if (choseSpecular) {
+        float mpdf;
+        const f3 m = distr_sample(d, wi, sx, sy, mpdf);
+        r.wo = reflect_v(wi, m);
+        r.sampledType = MTSG_F_GLOSSY_REFL;
+        if (r.wo.z <= 0) return r;
+    } else {
+        r.sampledType = MTSG_F_DIFF_REFL;
+        r.wo = square_to_cosine_hemisphere(sx, sy);
+    }
+    r.eta = 1.0f;
+    r.pdf = rp_pdf(b, rt, wi, r.wo, u, v);
+    if (r.pdf == 0) return r;
+    r.weight = divs(rp_eval(b, rt, wi, r.wo, u, v), r.pdf);
+    return r;
+}
+
+template <bool EXT>
+BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150
@@ -459,12 +657,13 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, f3 wi, float sx, float sy, float u1d) {
         r.eta = 1.0f;
         r.sampledType = MTSG_F_DIFF_REFL;
         r.pdf = D_INV_PI * r.wo.z;
-        r.weight = ld3(b.refl);
+        r.weight = bsdf_refl<EXT>(b, u, v);
         return r;
     }
+    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_sample(b, rt, wi, sx, sy, u, v); }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:357-406
         if (wi.z < 0) return r;
-        Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);
+        Distr d = bsdf_distr<EXT>(b, u, v);
         float pdf;
         f3 m = distr_sample(d, wi, sx, sy, pdf);
         r.pdf = pdf;
@@ -481,7 +680,7 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, f3 wi, float sx, float sy, float u1d) {
         r.weight = mul(F, weight);
         return r;
     }
-    Distr d = distr_make(b.distr, b.alpha_u, b.alpha_v, b.sample_visible);   // roughdielectric.cpp:525-615
+    Distr d = bsdf_distr<EXT>(b, u, v);                                    // roughdielectric.cpp:525-615
     Distr sd = d;
     if (!b.sample_visible) distr_scale_alpha(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
     float microfacetPDF;

@@ -50,18 +50,33 @@ enum {
 #define MTSG_F_TRANSMISSION (MTSG_F_DIFF_TRANS | MTSG_F_GLOSSY_TRANS | MTSG_F_DELTA_TRANS | MTSG_F_NULL)
 #define MTSG_F_DELTA (MTSG_F_NULL | MTSG_F_DELTA_REFL | MTSG_F_DELTA_TRANS)
 
+struct MtsgTex {             // Texture2D + checkerboard (texture.cpp:112-121, checkerboard.cpp)
+    int32_t type;            // MTSGPU_TEX_*: 0 = the BSDF's constant value
+    float c0[3], c1[3];
+    float uoff, voff, uscale, vscale;
+};
+
 struct MtsgBsdf {            // configured BSDF (after ctor + configure)
     int32_t type, flags, distr, sample_visible;
     float alpha_u, alpha_v;  // texture average, clamped (microfacet.h:89-97)
-    float eta, inv_eta;      // roughdielectric
+    float eta, inv_eta;      // roughdielectric / roughplastic
     float refl[3], spec_r[3], spec_t[3], eta3[3], k3[3];
     float pad;
+    // roughplastic (roughplastic.cpp:255-300): refl = diffuseReflectance
+    float inv_eta2, spec_weight;
+    int32_t nonlinear;
+    int32_t rt_ext, rt_int;          // offsets (floats) into MtsgDeviceScene::rtrans
+    int32_t rt_theta, rt_alpha;      // table sizes
+    int32_t rt_alpha_fixed;          // external table reduced to 1D (constant alpha)
+    float rt_alpha_min, rt_alpha_max;
+    MtsgTex refl_tex, alpha_tex;     // textured reflectance / alpha (type 0: constant)
 };
 
-enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
+enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };
+enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2 };   // path_kernel variants   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
 
 struct MtsgShape {
-    int32_t bsdf, emitter, has_normals, pad;
+    int32_t bsdf, emitter, has_normals, has_uv;
 };
 
 struct MtsgEmitter {
@@ -126,6 +141,8 @@ struct MtsgDeviceScene {
     const float *em_cdf;        // num_emitters + 1
     const uint32_t *sobol;      // MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE
     const MtsgEnv *env;         // device copy, or null without an environment emitter
+    const float *rtrans;        // roughplastic rough-transmittance slices (rtrans.h)
+    const float *texcoords;     // 2 per vertex (textured scenes), else null
     uint32_t num_emitters, num_prims;
     float em_norm;
     int32_t env_emitter;        // index of the environment emitter, -1: none
@@ -167,6 +184,7 @@ struct MtsgLaunch {
     uint32_t num_nodes;               // BVH2 inner nodes
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)
+    uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

@@ -114,6 +114,7 @@ struct Hit {
     f3 p, geoN, wi;
     Frame sh;
     int shape;
+    float u, v;       // its.uv (textured scenes only; dead otherwise)
 };
 
 // ---------------------------------------------------------------------------
@@ -391,7 +392,8 @@ __device__ __forceinline__ Frame shading_frame(f3 n, f3 dpdu) {
     return f;
 }
 
-// fillIntersectionRecord<true> (skdtree.h:343-429)
+// fillIntersectionRecord<true> (skdtree.h:343-429); UV = TEX
+template <bool TEX>
 __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot, float u, float v, float t, f3 d,
                                          Hit &h) {
     const uint32_t prim = S.tris[slot].prim;
@@ -420,6 +422,16 @@ __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot
     h.geoN = faceNormal;
     h.sh = shading_frame(shN, dpdu);
     h.wi = to_local(h.sh, neg(d));
+    if constexpr (TEX) {   // skdtree.h:398-405: t0*b.x + t1*b.y + t2*b.z, else (b.y, b.z)
+        if (S.shapes[h.shape].has_uv) {
+            const float *tc = S.texcoords;
+            h.u = tc[2 * (size_t)pv.x] * bx + tc[2 * (size_t)pv.y] * by + tc[2 * (size_t)pv.z] * bz;
+            h.v = tc[2 * (size_t)pv.x + 1] * bx + tc[2 * (size_t)pv.y + 1] * by + tc[2 * (size_t)pv.z + 1] * bz;
+        } else {
+            h.u = by;
+            h.v = bz;
+        }
+    }
 }
 
 // DiscreteDistribution::sample/sampleReuse (core/pmf.h:124-169)
@@ -581,10 +593,12 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 // reference's order (NEE 2D, BSDF 2D [+1D], RR 1D), and radiance is
 // accumulated in the reference's order (NEE term before the BSDF-hit term).
 // INSTR: traversal statistics + optional per-sample records (tests, roofline
-// pass); SCENE_LDS: BVH + TriAccel staged in LDS; ENV: scene has an envmap
-template <bool INSTR, bool SCENE_LDS, bool ENV, int WAVES>
+// pass); SCENE_LDS: BVH + TriAccel staged in LDS; FEAT: MTSG_FEAT_ENV (scene
+// has an envmap) | MTSG_FEAT_EXT (roughplastic or textured BSDFs)
+template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     constexpr bool STATS = INSTR;
+    constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0;
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
     // LDS: [Sobol nibble tables][look_up column tables][BVH + TriAccel (small scenes)][stacks]
@@ -732,7 +746,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 endPath = true;   // the BSDF sample at the previous vertex failed
             } else {
                 // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
-                if (hit) fill_hit(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+                if (hit) fill_hit<EXT>(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
                 if (STATS && hit) cHits++;
                 if (primary) {
                     P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
@@ -877,9 +891,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                 f3 c = mk(0, 0, 0);
                                 if (!is_zero(value)) {
                                     const f3 wo = to_local(P.its.sh, dd);
-                                    const f3 bsdfVal = bsdf_eval(bsdf, P.its.wi, wo);
+                                    const f3 bsdfVal = bsdf_eval<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, wo, P.its.u, P.its.v);
                                     if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                        const float bsdfPdf = bsdf_pdf(bsdf, P.its.wi, wo);
+                                        const float bsdfPdf = bsdf_pdf<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, wo, P.its.u, P.its.v);
                                         const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
                                         const float weight = pa / (pa + pb);
                                         c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
@@ -897,7 +911,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                         next2d(SC, L.resolution, smp, px, py, bx2, by2);
                         float u1d = 0.0f;
                         if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
-                        const BSample bs = bsdf_sample(bsdf, P.its.wi, bx2, by2, u1d);
+                        const BSample bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
                         if (!is_zero(bs.weight) && !smp.err) {
                             P.scattered |= bs.sampledType != MTSG_F_NULL;
                             const f3 wo = to_world(P.its.sh, bs.wo);
@@ -1017,24 +1031,32 @@ size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
 // variants: small scenes (BVH in LDS) run 3 waves/SIMD with 32 Sobol dims in
 // LDS; large scenes run 4 waves/SIMD (128 VGPRs) when the traversal stacks fit
 // 4 blocks per CU, else 3 (capi.cpp picks L.waves and L.lds_dims)
-template <bool SCENE_LDS, bool ENV, int WAVES>
+template <bool SCENE_LDS, int FEAT, int WAVES>
 static void launch_path_w(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
     const size_t lds = mtsg_path_lds_bytes(L);
-    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, ENV, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, ENV, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, FEAT, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, FEAT, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
 }
 
-template <bool ENV>
+template <int FEAT>
 static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
-    if (L.scene_lds) launch_path_w<true, ENV, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
-    else if (L.waves == 4) launch_path_w<false, ENV, 4>(L, grid, instr, stream);
-    else launch_path_w<false, ENV, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+    if (L.scene_lds) launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+    else if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
+    else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+}
+
+int mtsg_path_features(const MtsgLaunch &L) {
+    return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | (L.ext ? MTSG_FEAT_EXT : 0);
 }
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
     const bool instr = samples || stats;
-    if (L.scene.env_emitter >= 0) launch_path<true>(L, grid, instr, stream);
-    else launch_path<false>(L, grid, instr, stream);
+    switch (mtsg_path_features(L)) {
+        case 0: launch_path<0>(L, grid, instr, stream); break;
+        case MTSG_FEAT_ENV: launch_path<MTSG_FEAT_ENV>(L, grid, instr, stream); break;
+        case MTSG_FEAT_EXT: launch_path<MTSG_FEAT_EXT>(L, grid, instr, stream); break;
+        default: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, instr, stream); break;
+    }
     return hipGetLastError();
 }
 
@@ -1057,17 +1079,22 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
     return hipGetLastError();
 }
 
-template <bool SCENE_LDS, bool ENV, int WAVES>
+template <bool SCENE_LDS, int FEAT, int WAVES>
 static int occupancy_w(const MtsgLaunch &L, int *bpc) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, path_kernel<false, SCENE_LDS, ENV, WAVES>, BLOCK,
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, path_kernel<false, SCENE_LDS, FEAT, WAVES>, BLOCK,
                                                              mtsg_path_lds_bytes(L));
 }
-template <bool ENV>
+template <int FEAT>
 static int occupancy_e(const MtsgLaunch &L, int *bpc) {
-    if (L.scene_lds) return occupancy_w<true, ENV, MTSG_WAVES_PER_EU>(L, bpc);
-    if (L.waves == 4) return occupancy_w<false, ENV, 4>(L, bpc);
-    return occupancy_w<false, ENV, MTSG_WAVES_PER_EU>(L, bpc);
+    if (L.scene_lds) return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
+    if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
+    return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
 }
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
-    return L.scene.env_emitter >= 0 ? occupancy_e<true>(L, blocksPerCU) : occupancy_e<false>(L, blocksPerCU);
+    switch (mtsg_path_features(L)) {
+        case 0: return occupancy_e<0>(L, blocksPerCU);
+        case MTSG_FEAT_ENV: return occupancy_e<MTSG_FEAT_ENV>(L, blocksPerCU);
+        case MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_EXT>(L, blocksPerCU);
+        default: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, blocksPerCU);
+    }
 }

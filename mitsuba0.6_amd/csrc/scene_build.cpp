@@ -178,18 +178,129 @@ float energy_scale(const float *s, int ensure) {   // BSDF::ensureEnergyConserva
     return 1.0f;
 }
 
-int configure_bsdf(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::string &err) {
+// Texture getMaximum/getMinimum/getAverage (checkerboard.cpp, texture.cpp ConstantSpectrumTexture)
+void tex_max(const mtsgpu_texture_desc &t, const float *c, float out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = t.type ? fmax_std(t.color0[i], t.color1[i]) : c[i];
+}
+void tex_min(const mtsgpu_texture_desc &t, const float *c, float out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = t.type ? fmin_std(t.color0[i], t.color1[i]) : c[i];
+}
+void tex_avg(const mtsgpu_texture_desc &t, const float *c, float out[3]) {
+    for (int i = 0; i < 3; ++i) out[i] = t.type ? (t.color0[i] + t.color1[i]) * 0.5f : c[i];
+}
+float avg_spec(const float s[3]) { float r = 0.0f; r += s[0]; r += s[1]; r += s[2]; return r * (1.0f / 3); }
+float luminance(const float s[3]) { return s[0] * 0.212671f + s[1] * 0.715160f + s[2] * 0.072169f; }   // spectrum.h:725
+
+// a textured parameter into the device record; `scale` = ensureEnergyConservation's
+// ScaleTexture factor (eval = nested eval * scale, scale.cpp:85-87)
+int set_tex(const mtsgpu_texture_desc &t, float scale, MtsgTex &o, std::string &err) {
+    std::memset(&o, 0, sizeof o);
+    if (t.type == MTSGPU_TEX_NONE) return MTSGPU_OK;
+    if (t.type != MTSGPU_TEX_CHECKERBOARD) { err = "unsupported texture type"; return MTSGPU_EINVAL; }
+    o.type = t.type;
+    for (int i = 0; i < 3; ++i) {
+        o.c0[i] = scale != 1.0f ? t.color0[i] * scale : t.color0[i];
+        o.c1[i] = scale != 1.0f ? t.color1[i] * scale : t.color1[i];
+    }
+    o.uoff = t.uoffset; o.voff = t.voffset; o.uscale = t.uscale; o.vscale = t.vscale;
+    return MTSGPU_OK;
+}
+
+// RoughPlastic ctor + configure (roughplastic.cpp:197-300)
+int configure_roughplastic(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::vector<float> &rt, std::string &err) {
+    if (d.int_ior < 0 || d.ext_ior < 0 || d.int_ior == d.ext_ior) {
+        err = "The interior and exterior indices of refraction must be positive and differ!";
+        return MTSGPU_EINVAL;
+    }
+    b.eta = d.int_ior / d.ext_ior;
+    b.nonlinear = d.nonlinear ? 1 : 0;
+    if (d.distribution < 0 || d.distribution > 2) {
+        err = "Specified an invalid distribution, must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!";
+        return MTSGPU_EINVAL;
+    }
+    b.distr = d.distribution;
+    b.sample_visible = d.distribution == MTSGPU_DISTR_PHONG ? 0 : d.sample_visible;
+    const float au = fmax_std(d.alpha_u, 1e-4f), av = fmax_std(d.alpha_v, 1e-4f);
+    if (d.alpha_tex.type == MTSGPU_TEX_NONE && au != av) {
+        err = "The 'roughplastic' plugin currently does not support anisotropic microfacet distributions!";
+        return MTSGPU_EINVAL;
+    }
+    // m_alpha = ConstantFloatTexture(distr.getAlpha()) unless a texture was added
+    float alpha3[3] = {au, au, au};
+    b.alpha_u = b.alpha_v = avg3(au);
+    int rc;
+    // ensureEnergyConservation of both reflectances (bsdf.cpp:88-113)
+    float mx[3];
+    tex_max(d.reflectance_tex, d.diffuse_reflectance, mx);
+    const float sd = energy_scale(mx, d.ensure_energy_conservation);
+    const float ss = energy_scale(d.specular_reflectance, d.ensure_energy_conservation);
+    for (int i = 0; i < 3; ++i) {
+        b.refl[i] = sd != 1.0f ? d.diffuse_reflectance[i] * sd : d.diffuse_reflectance[i];
+        b.spec_r[i] = ss != 1.0f ? d.specular_reflectance[i] * ss : d.specular_reflectance[i];
+    }
+    if ((rc = set_tex(d.reflectance_tex, sd, b.refl_tex, err))) return rc;
+    if ((rc = set_tex(d.alpha_tex, 1.0f, b.alpha_tex, err))) return rc;
+    // m_specularSamplingWeight = sAvg / (dAvg + sAvg) of the (scaled) textures' averages
+    float davg[3], savg[3];
+    tex_avg(d.reflectance_tex, d.diffuse_reflectance, davg);
+    for (int i = 0; i < 3; ++i) {
+        if (sd != 1.0f) davg[i] = davg[i] * sd;
+        savg[i] = b.spec_r[i];
+    }
+    const float dAvg = luminance(davg), sAvg = luminance(savg);
+    b.spec_weight = sAvg / (dAvg + sAvg);
+    b.inv_eta2 = 1.0f / (b.eta * b.eta);
+    b.flags = MTSG_F_GLOSSY_REFL | MTSG_F_DIFF_REFL | MTSG_F_FRONT;
+    // RoughTransmittance(m_type): the distribution's table, checked and reduced
+    MtsgRTrans ext;
+    if ((rc = mtsg_rtrans_load(d.rtrans_data, (size_t)d.rtrans_bytes, ext, err))) {
+        if (!d.rtrans_data) err = "roughplastic: no rough transmittance table (data/microfacet/<distribution>.dat)";
+        return rc;
+    }
+    float amin[3], amax[3];
+    tex_min(d.alpha_tex, alpha3, amin);
+    tex_max(d.alpha_tex, alpha3, amax);
+    if ((rc = mtsg_rtrans_check(ext, b.eta, avg_spec(amin), avg_spec(amax), err))) return rc;
+    MtsgRTrans in = ext;
+    mtsg_rtrans_set_eta(ext, b.eta);
+    mtsg_rtrans_set_eta(in, 1 / b.eta);
+    if (d.alpha_tex.type == MTSGPU_TEX_NONE) mtsg_rtrans_set_alpha(ext, b.alpha_u);
+    b.rt_theta = (int32_t)ext.theta;
+    b.rt_alpha = (int32_t)ext.alpha;
+    b.rt_alpha_fixed = ext.alphaFixed ? 1 : 0;
+    b.rt_alpha_min = ext.alphaMin;
+    b.rt_alpha_max = ext.alphaMax;
+    b.rt_ext = (int32_t)rt.size();
+    rt.insert(rt.end(), ext.trans.begin(), ext.trans.end());
+    b.rt_int = (int32_t)rt.size();
+    rt.insert(rt.end(), in.diff.begin(), in.diff.end());
+    return MTSGPU_OK;
+}
+
+int configure_bsdf(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::vector<float> &rt, std::string &err) {
     std::memset(&b, 0, sizeof b);
     b.type = d.type;
     if (d.type == MTSGPU_BSDF_DIFFUSE) {
-        float sc = energy_scale(d.reflectance, d.ensure_energy_conservation);
+        float mx[3];
+        tex_max(d.reflectance_tex, d.reflectance, mx);
+        float sc = energy_scale(mx, d.ensure_energy_conservation);
         for (int i = 0; i < 3; ++i) b.refl[i] = sc != 1.0f ? d.reflectance[i] * sc : d.reflectance[i];
-        float mx = fmax_std(fmax_std(b.refl[0], b.refl[1]), b.refl[2]);
-        b.flags = mx > 0 ? (MTSG_F_DIFF_REFL | MTSG_F_FRONT) : 0;
+        int rc = set_tex(d.reflectance_tex, sc, b.refl_tex, err);
+        if (rc) return rc;
+        float m2[3];
+        tex_max(d.reflectance_tex, b.refl, m2);
+        if (d.reflectance_tex.type) for (int i = 0; i < 3; ++i) m2[i] = fmax_std(b.refl_tex.c0[i], b.refl_tex.c1[i]);
+        float mxs = fmax_std(fmax_std(m2[0], m2[1]), m2[2]);
+        b.flags = mxs > 0 ? (MTSG_F_DIFF_REFL | MTSG_F_FRONT) : 0;
         return MTSGPU_OK;
     }
+    if (d.type == MTSGPU_BSDF_ROUGHPLASTIC) return configure_roughplastic(d, b, rt, err);
     if (d.type != MTSGPU_BSDF_ROUGHCONDUCTOR && d.type != MTSGPU_BSDF_ROUGHDIELECTRIC) {
         err = "unsupported BSDF type"; return MTSGPU_EINVAL;
+    }
+    if (d.alpha_tex.type != MTSGPU_TEX_NONE) {
+        int rc = set_tex(d.alpha_tex, 1.0f, b.alpha_tex, err);
+        if (rc) return rc;
     }
     if (d.distribution < 0 || d.distribution > 2) {
         err = "Specified an invalid distribution, must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!";
@@ -395,7 +506,6 @@ float half_to_float(uint16_t h) {
     std::memcpy(&f, &bits, 4);
     return f;
 }
-inline float luminance(const float *c) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; }
 
 // LanczosSincFilter::eval with lobes = 2 (rfilters/lanczos.cpp:43-55)
 float lanczos2(float x) {
@@ -698,14 +808,17 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     S.film_h = D->sensor.film_height;
     const uint32_t nb = D->num_bsdfs;
     S.bsdfs.resize(nb + 2);
-    for (uint32_t i = 0; i < nb; ++i)
-        if ((rc = configure_bsdf(D->bsdfs[i], S.bsdfs[i], err))) return rc;
+    for (uint32_t i = 0; i < nb; ++i) {
+        if ((rc = configure_bsdf(D->bsdfs[i], S.bsdfs[i], S.rtrans, err))) return rc;
+        const MtsgBsdf &b = S.bsdfs[i];
+        if (b.type == MTSGPU_BSDF_ROUGHPLASTIC || b.refl_tex.type || b.alpha_tex.type) S.ext = true;
+    }
     {   // Shape::configure defaults (shape.cpp:48-70): black for emitters, 0.5 otherwise
         mtsgpu_bsdf_desc dd; std::memset(&dd, 0, sizeof dd);
         dd.type = MTSGPU_BSDF_DIFFUSE; dd.ensure_energy_conservation = 1;
-        configure_bsdf(dd, S.bsdfs[nb], err);
+        configure_bsdf(dd, S.bsdfs[nb], S.rtrans, err);
         dd.reflectance[0] = dd.reflectance[1] = dd.reflectance[2] = 0.5f;
-        configure_bsdf(dd, S.bsdfs[nb + 1], err);
+        configure_bsdf(dd, S.bsdfs[nb + 1], S.rtrans, err);
     }
     if (D->num_emitters == 0) { err = "scene has no emitters (the sunsky fallback is out of scope)"; return MTSGPU_EINVAL; }
     S.emitters.resize(D->num_emitters);
@@ -805,6 +918,11 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
             }
         }
         sh.has_normals = hasNormals ? 1 : 0;
+        sh.has_uv = (S.ext && m.texcoords) ? 1 : 0;
+        if (sh.has_uv) {
+            if (S.texcoords.empty()) S.texcoords.assign((size_t)verts * 2, 0.0f);
+            std::memcpy(&S.texcoords[2 * (size_t)voff], m.texcoords, sizeof(float) * 2 * (size_t)nv);
+        }
         for (uint32_t k = 0; k < nv; ++k) {
             S.positions[3 * (voff + k)] = P[k].x; S.positions[3 * (voff + k) + 1] = P[k].y; S.positions[3 * (voff + k) + 2] = P[k].z;
             if (hasNormals) {

@@ -10,6 +10,20 @@
 #include "../../include/mtsgpu.h"
 #include "layout.h"
 
+// RoughTransmittance table (rtrans.h) and its eta/alpha reductions (rtrans_host.cpp)
+struct MtsgRTrans {
+    size_t eta = 0, alpha = 0, theta = 0;
+    float etaMin = 0, etaMax = 0, alphaMin = 0, alphaMax = 0;
+    bool etaFixed = false, alphaFixed = false;
+    std::vector<float> trans, diff;
+};
+int mtsg_rtrans_load(const void *data, size_t bytes, MtsgRTrans &t, std::string &err);
+void mtsg_rtrans_set_eta(MtsgRTrans &t, float eta);
+void mtsg_rtrans_set_alpha(MtsgRTrans &t, float alpha);
+float mtsg_rtrans_eval(const MtsgRTrans &t, float cosTheta, float alpha);
+float mtsg_rtrans_eval_diffuse(const MtsgRTrans &t, float alpha);
+int mtsg_rtrans_check(const MtsgRTrans &t, float eta, float alphaMin, float alphaMax, std::string &err);
+
 struct HostScene {
     std::vector<MtsgNode> nodes;
     std::vector<MtsgTri> tris;
@@ -28,6 +42,9 @@ struct HostScene {
     MtsgEnv env;
     std::vector<uint16_t> env_texels;
     std::vector<float> env_cdf_rows, env_cdf_cols, env_row_weights;
+    // roughplastic tables (MtsgBsdf::rt_ext / rt_int offsets) and per-vertex UVs
+    std::vector<float> rtrans, texcoords;
+    bool ext = false;   // roughplastic or textured BSDFs: the MTSG_FEAT_EXT kernel variant
 };
 
 // Returns MTSGPU_OK or an error code; `err` receives the message.

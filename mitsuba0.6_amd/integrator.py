@@ -27,7 +27,7 @@ class MtsgpuError(RuntimeError):
 
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
-           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device']
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene']
 
 _lib = None
 
@@ -52,13 +52,25 @@ def load_library(path=None):
     L.mtsgpu_destroy.argtypes = [C.c_void_p]
     L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
+    L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
     L.mtsgpu_develop_device.argtypes = [C.c_void_p, P(abi.DevelopParams), C.c_void_p, C.c_void_p, C.c_void_p]
-    if L.mtsgpu_abi_version() != 1:
+    if L.mtsgpu_abi_version() != abi.ABI_VERSION:
         raise NativeUnavailable('ABI version mismatch')
     if path is None:
         _lib = L
     return L
+
+
+def check_scene(scene):
+    """Host-only configure of `scene` (mtsgpu_check_scene): raises MtsgpuError with
+    the reference's configure() error message, or returns None."""
+    L = load_library()
+    d = scene.desc()
+    buf = C.create_string_buffer(1024)
+    rc = L.mtsgpu_check_scene(C.byref(d), buf, 1024)
+    if rc != 0:
+        raise MtsgpuError(rc, buf.value.decode())
 
 
 class Context:

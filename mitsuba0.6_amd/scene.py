@@ -9,6 +9,7 @@ film and the sampler.  `Scene.desc()` packs it into the C-ABI structs of
 include/mtsgpu.h; everything the reference derives in configure() is derived
 behind the ABI by libmtsgpu.so.
 """
+import ctypes as C
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -28,12 +29,44 @@ def lookup_ior(v):
 
 
 @dataclass
+class Checkerboard:
+    """`checkerboard` texture (src/textures/checkerboard.cpp) with Texture2D's
+    uv transform (src/librender/texture.cpp:81-121): uv' = uv * scale + offset,
+    color0 where (2 (floor-mod of int(2u')) - 1) (2 (.. v') - 1) == 1."""
+    color0: tuple = (0.4, 0.4, 0.4)
+    color1: tuple = (0.2, 0.2, 0.2)
+    uoffset: float = 0.0
+    voffset: float = 0.0
+    uscale: float = 1.0
+    vscale: float = 1.0
+
+    def fill(self, t):
+        t.type = abi.TEX_CHECKERBOARD
+        t.color0[:] = _spec(self.color0)
+        t.color1[:] = _spec(self.color1)
+        t.uoffset, t.voffset, t.uscale, t.vscale = self.uoffset, self.voffset, self.uscale, self.vscale
+
+    def average(self):
+        c0, c1 = np.asarray(_spec(self.color0), np.float32), np.asarray(_spec(self.color1), np.float32)
+        return tuple(float(x) for x in ((c0 + c1) * np.float32(0.5)))
+
+
+def _spec(v):
+    """A Spectrum property: a float is Spectrum(value), a 3-tuple RGB."""
+    if isinstance(v, (int, float, np.floating)):
+        return (float(v),) * 3
+    return tuple(float(x) for x in v)
+
+
+@dataclass
 class BSDF:
-    """One of diffuse / roughconductor / roughdielectric with Mitsuba property names."""
+    """One of diffuse / roughconductor / roughdielectric / roughplastic with
+    Mitsuba property names.  `reflectance` (diffuse), `diffuseReflectance`
+    (roughplastic) and `alpha` (rough BSDFs, isotropic) may be a Checkerboard."""
     type: str = 'diffuse'
-    reflectance: tuple = (0.5, 0.5, 0.5)
+    reflectance: object = (0.5, 0.5, 0.5)
     distribution: str = 'beckmann'
-    alpha: Optional[float] = None
+    alpha: object = None
     alphaU: Optional[float] = None
     alphaV: Optional[float] = None
     sampleVisible: bool = True
@@ -43,20 +76,33 @@ class BSDF:
     k: Optional[tuple] = None
     material: Optional[str] = 'Cu'     # roughconductor.cpp:174 default
     extEta: object = 'air'
-    intIOR: object = 'bk7'
+    intIOR: object = None              # roughdielectric: bk7 (roughdielectric.cpp:186); roughplastic: polypropylene
     extIOR: object = 'air'
+    diffuseReflectance: object = (0.5, 0.5, 0.5)   # roughplastic.cpp:201
+    nonlinear: bool = False
+    rtransDir: Optional[str] = None    # where data/microfacet/<distribution>.dat is looked up first (rtrans.py)
     ensureEnergyConservation: bool = True
+
+    def int_ior(self):
+        if self.intIOR is not None:
+            return self.intIOR
+        return 'polypropylene' if self.type == 'roughplastic' else 'bk7'
 
     def to_desc(self):
         d = abi.BsdfDesc()
         d.type = {'diffuse': abi.BSDF_DIFFUSE, 'roughconductor': abi.BSDF_ROUGHCONDUCTOR,
-                  'roughdielectric': abi.BSDF_ROUGHDIELECTRIC}[self.type]
+                  'roughdielectric': abi.BSDF_ROUGHDIELECTRIC, 'roughplastic': abi.BSDF_ROUGHPLASTIC}[self.type]
         d.distribution = {'beckmann': abi.DISTR_BECKMANN, 'ggx': abi.DISTR_GGX,
                           'phong': abi.DISTR_PHONG, 'as': abi.DISTR_PHONG}[self.distribution.lower()]
         d.sample_visible = int(self.sampleVisible)
         d.ensure_energy_conservation = int(self.ensureEnergyConservation)
         # MicrofacetDistribution(props) defaults alphaU = alphaV = 0.1 (microfacet.h:99-101,117-130)
-        if self.alpha is not None:
+        if isinstance(self.alpha, Checkerboard):
+            if self.alphaU is not None or self.alphaV is not None:
+                raise ValueError("Microfacet model: please specify either 'alpha' or 'alphaU'/'alphaV'.")
+            au = av = 0.1
+            self.alpha.fill(d.alpha_tex)
+        elif self.alpha is not None:
             au = av = float(self.alpha)
         elif self.alphaU is not None or self.alphaV is not None:
             if self.alphaU is None or self.alphaV is None:
@@ -65,17 +111,33 @@ class BSDF:
         else:
             au = av = 0.1
         d.alpha_u, d.alpha_v = au, av
-        d.reflectance[:] = self.reflectance
-        d.specular_reflectance[:] = self.specularReflectance
-        d.specular_transmittance[:] = self.specularTransmittance
+        if isinstance(self.reflectance, Checkerboard):
+            if self.type == 'diffuse':
+                self.reflectance.fill(d.reflectance_tex)
+        else:
+            d.reflectance[:] = _spec(self.reflectance)
+        d.specular_reflectance[:] = _spec(self.specularReflectance)
+        d.specular_transmittance[:] = _spec(self.specularTransmittance)
         if self.type == 'roughconductor':
             # intEta/intK from the material, overridden by explicit 'eta'/'k' (roughconductor.cpp:172-190)
             from .conductors import conductor_rgb
             eta, k = conductor_rgb(self.material or 'Cu')
             d.eta[:] = self.eta if self.eta is not None else eta
             d.k[:] = self.k if self.k is not None else k
+        if self.type == 'roughplastic':
+            if isinstance(self.diffuseReflectance, Checkerboard):
+                self.diffuseReflectance.fill(d.reflectance_tex)
+            else:
+                d.diffuse_reflectance[:] = _spec(self.diffuseReflectance)
+            d.nonlinear = int(self.nonlinear)
+            from .rtrans import table_bytes
+            data = table_bytes(self.distribution, [self.rtransDir])
+            buf = C.create_string_buffer(data, len(data))
+            d.rtrans_data = C.cast(buf, C.c_void_p)
+            d.rtrans_bytes = len(data)
+            d._keep = buf                  # the buffer lives as long as the descriptor
         d.ext_eta = lookup_ior(self.extEta)
-        d.int_ior = lookup_ior(self.intIOR)
+        d.int_ior = lookup_ior(self.int_ior())
         d.ext_ior = lookup_ior(self.extIOR)
         return d
 
@@ -186,7 +248,9 @@ class Scene:
             md[i].face_normals, md[i].flip_normals = int(m.faceNormals), int(m.flipNormals)
         bd = (abi.BsdfDesc * max(1, len(self.bsdfs)))()
         for i, b in enumerate(self.bsdfs):
-            bd[i] = b.to_desc()
+            bdi = b.to_desc()
+            keep.append(getattr(bdi, '_keep', None))
+            bd[i] = bdi
         ed = (abi.EmitterDesc * max(1, len(self.emitters)))()
         for i, e in enumerate(self.emitters):
             ed[i] = e.to_desc()

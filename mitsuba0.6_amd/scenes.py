@@ -6,7 +6,7 @@ scene a user would write: per-shape meshes with BSDFs and area emitters.
 """
 import numpy as np
 
-from .scene import BSDF, Emitter, Mesh, PathIntegrator, Scene, Sensor, look_at
+from .scene import BSDF, Checkerboard, Emitter, Mesh, PathIntegrator, Scene, Sensor, look_at
 from .transform import Transform
 
 S = 0.01  # classic Cornell box data is in millimetres; scene units are 10 cm
@@ -77,6 +77,25 @@ def rough_materials():
     ]
 
 
+def plastic_materials():
+    """roughplastic (with the rough-transmittance tables) and checkerboard-textured
+    BSDFs: constant and textured roughness, the three distributions, nonlinear,
+    a textured diffuse reflectance."""
+    chk_alpha = Checkerboard(color0=0.05, color1=0.4, uscale=3.0, vscale=3.0)
+    return [
+        BSDF('roughplastic', distribution='ggx', alpha=0.15, diffuseReflectance=(0.1, 0.3, 0.7)),
+        BSDF('roughplastic', distribution='beckmann', alpha=chk_alpha, diffuseReflectance=(0.6, 0.2, 0.1),
+             intIOR=1.6),
+        BSDF('roughplastic', distribution='phong', alpha=0.3, nonlinear=True, diffuseReflectance=(0.7, 0.7, 0.2)),
+        BSDF('roughplastic', distribution='ggx', alpha=chk_alpha, sampleVisible=False,
+             diffuseReflectance=Checkerboard(color0=(0.8, 0.1, 0.1), color1=(0.1, 0.1, 0.8), uscale=4, vscale=4)),
+        BSDF('diffuse', reflectance=Checkerboard(color0=(0.75, 0.75, 0.7), color1=(0.2, 0.25, 0.3), uscale=6,
+                                                 vscale=6, uoffset=0.1)),
+        BSDF('roughconductor', distribution='ggx', alpha=Checkerboard(color0=0.02, color1=0.3, uscale=2,
+                                                                      vscale=2), material='Au'),
+    ]
+
+
 def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, materials='diffuse'):
     """Config C1 (512x512, 64 spp) / C2 (1280x720, 512 spp): diffuse Cornell box
     with a rectangular area light.  materials='rough' swaps the
@@ -88,13 +107,18 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
     meshes = []
     # room surfaces: vertex normals left to TriMesh::computeNormals (trimesh.cpp:608-681)
     floor_b, short_b, tall_b = 0, 0, 0
+    back_b = 0
     if materials == 'rough':
         rough = rough_materials()
         base = len(bsdfs)
         bsdfs += rough
         floor_b, short_b, tall_b = base + 7, base + 0, base + 1
-    uv = materials == 'rough'    # UV tangents on every rough surface (anisotropic ones require them)
-    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, 0), (_GREEN, 2), (_RED, 1)):
+    elif materials == 'plastic':
+        base = len(bsdfs)
+        bsdfs += plastic_materials()
+        floor_b, short_b, tall_b, back_b = base + 4, base + 1, base + 0, base + 5
+    uv = materials in ('rough', 'plastic')   # UV tangents (anisotropic BSDFs) and texture coordinates
+    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, back_b), (_GREEN, 2), (_RED, 1)):
         m = _quads_mesh([quad], inward=True, uv=uv)
         meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b))
     for quads, b in ((_SHORT, short_b), (_TALL, tall_b)):
@@ -143,9 +167,10 @@ def procedural_envmap(width=1024, height=512, seed=0x5EED):
     return sky.astype(np.float32)
 
 
-def blob_mesh(nu=236, nv=148, radius=1.0, center=(0.0, 1.0, 0.0)):
+def blob_mesh(nu=236, nv=148, radius=1.0, center=(0.0, 1.0, 0.0), uv=False):
     """Procedural stand-in for data/tests/bunny.ply (~69k triangles, closed,
-    smooth vertex normals left to computeNormals): a displaced UV sphere."""
+    smooth vertex normals left to computeNormals): a displaced UV sphere.
+    uv=True also returns spherical texture coordinates (u = phi / 2pi, v = theta / pi)."""
     th = np.linspace(0, np.pi, nv)
     ph = np.linspace(0, 2 * np.pi, nu, endpoint=False)
     T, P = np.meshgrid(th, ph, indexing='ij')
@@ -161,20 +186,34 @@ def blob_mesh(nu=236, nv=148, radius=1.0, center=(0.0, 1.0, 0.0)):
                 idx.append((a, b, d))
             if i < nv - 2:
                 idx.append((a, d, c))
+    if uv:
+        tc = np.stack([(P / (2 * np.pi)), T / np.pi], -1).reshape(-1, 2).astype(np.float32)
+        return pos, np.asarray(idx, np.uint32), tc
     return pos, np.asarray(idx, np.uint32)
 
 
 def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env_size=(1024, 512),
-               blob=(236, 148), area_light=False, env_weight=1.0):
+               blob=(236, 148), area_light=False, env_weight=1.0, plastic=False):
     """Config C3: a ~69k-triangle object in roughconductor GGX alpha=0.1 (copper) on a
-    diffuse checker ground, lit only by a 1024x512 environment map."""
-    cu = BSDF('roughconductor', distribution='ggx', alpha=0.1, material='Cu')
+    diffuse checker ground, lit only by a 1024x512 environment map.
+    plastic=True is config C5: the object in roughplastic GGX whose roughness is a
+    checkerboard texture over spherical UVs (alpha 0.05 / 0.3), so every shading
+    point interpolates the 2D (alpha x theta) rough-transmittance slice."""
+    if plastic:
+        obj = BSDF('roughplastic', distribution='ggx', diffuseReflectance=(0.2, 0.35, 0.6),
+                   alpha=Checkerboard(color0=0.05, color1=0.3, uscale=8.0, vscale=4.0))
+    else:
+        obj = BSDF('roughconductor', distribution='ggx', alpha=0.1, material='Cu')
     g0 = BSDF('diffuse', reflectance=(0.4, 0.4, 0.4))
     g1 = BSDF('diffuse', reflectance=(0.15, 0.15, 0.15))
-    bsdfs = [cu, g0, g1]
+    bsdfs = [obj, g0, g1]
     meshes = []
-    p, i = blob_mesh(*blob)
-    meshes.append(Mesh(p, i, bsdf=0, name='object'))
+    if plastic:
+        p, i, tc = blob_mesh(*blob, uv=True)
+        meshes.append(Mesh(p, i, texcoords=tc, bsdf=0, name='object'))
+    else:
+        p, i = blob_mesh(*blob)
+        meshes.append(Mesh(p, i, bsdf=0, name='object'))
     # 12x12 checker of quads, y = 0 (two meshes, one per colour)
     n, half = 12, 6.0
     for col in (0, 1):
@@ -312,6 +351,7 @@ CONFIGS = {
     'C2': dict(builder='cornell_box', width=1280, height=720, spp=512),
     'C3': dict(builder='matpreview', width=1280, height=720, spp=512),
     'C4': dict(builder='atrium', width=1280, height=720, spp=256),
+    'C5': dict(builder='matpreview', width=1280, height=720, spp=1024, plastic=True),
 }
 
 

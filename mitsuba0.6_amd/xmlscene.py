@@ -35,7 +35,7 @@ import numpy as np
 from .film import HDRFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
 from .obj import load_obj, srgb_to_linear, strtof
 from .ply import load_ply
-from .scene import BSDF, Emitter, Mesh, PathIntegrator, Scene, Sensor
+from .scene import BSDF, Checkerboard, Emitter, Mesh, PathIntegrator, Scene, Sensor
 from .serialized import load_serialized
 from .transform import Transform, _cross, _normalize, normalize_rows
 
@@ -243,20 +243,38 @@ class XMLSceneLoader:
         return props
 
     # -- plugins ------------------------------------------------------------------
+    def make_texture(self, p):
+        """checkerboard (textures/checkerboard.cpp) with the Texture2D uv transform (texture.cpp:81-95)."""
+        if p.plugin != 'checkerboard':
+            raise NotImplementedError('texture "%s" (checkerboard is on the GPU path)' % p.plugin)
+        if p.get('coordinates', 'uv') != 'uv':
+            raise SceneError('Only UV coordinates are supported at the moment!')
+        uvscale = float(p.get('uvscale', 1.0))
+        return Checkerboard(color0=p.get('color0', 0.4), color1=p.get('color1', 0.2),
+                            uoffset=float(p.get('uoffset', 0.0)), voffset=float(p.get('voffset', 0.0)),
+                            uscale=float(p.get('uscale', uvscale)), vscale=float(p.get('vscale', uvscale)))
+
+    def _tex_params(self, p, allowed):
+        """Texture children (nested or <ref>) by parameter name; BSDF::addChild semantics."""
+        out = {}
+        for name, ch in p.children:
+            if ch.tag != 'texture':
+                continue
+            if name not in allowed:
+                raise SceneError('%s: unsupported texture parameter "%s"' % (p.plugin, name))
+            out[name] = self.make_texture(ch)
+        return out
+
     def make_bsdf(self, p):
         if p.tag != 'bsdf':
             raise SceneError('expected a BSDF')
         t = p.plugin
         if t == 'diffuse':
-            for _, ch in p.children:
-                if ch.tag == 'texture':
-                    raise NotImplementedError('textured diffuse reflectance')
-            return BSDF('diffuse', reflectance=p.get('reflectance', (0.5, 0.5, 0.5)),
+            tex = self._tex_params(p, ('reflectance',))
+            return BSDF('diffuse', reflectance=tex.get('reflectance', p.get('reflectance', (0.5, 0.5, 0.5))),
                         ensureEnergyConservation=p.get('ensureEnergyConservation', True))
-        if t in ('roughconductor', 'roughdielectric'):
-            for _, ch in p.children:
-                if ch.tag == 'texture':
-                    raise NotImplementedError('textured %s parameters' % t)
+        if t in ('roughconductor', 'roughdielectric', 'roughplastic'):
+            tex = self._tex_params(p, ('alpha', 'diffuseReflectance') if t == 'roughplastic' else ('alpha',))
             kw = dict(distribution=p.get('distribution', 'beckmann'), sampleVisible=p.get('sampleVisible', True),
                       specularReflectance=p.get('specularReflectance', (1.0, 1.0, 1.0)),
                       ensureEnergyConservation=p.get('ensureEnergyConservation', True))
@@ -264,15 +282,21 @@ class XMLSceneLoader:
                 kw['alpha'] = float(p['alpha'])
             if 'alphaU' in p or 'alphaV' in p:
                 kw['alphaU'], kw['alphaV'] = p.get('alphaU'), p.get('alphaV')
+            if 'alpha' in tex:
+                kw['alpha'] = tex['alpha']
             if t == 'roughconductor':
                 kw.update(material=p.get('material', 'Cu'), eta=p.get('eta'), k=p.get('k'),
                           extEta=p.get('extEta', 'air'))
-            else:
+            elif t == 'roughdielectric':
                 kw.update(intIOR=p.get('intIOR', 'bk7'), extIOR=p.get('extIOR', 'air'),
                           specularTransmittance=p.get('specularTransmittance', (1.0, 1.0, 1.0)))
+            else:
+                kw.update(intIOR=p.get('intIOR', 'polypropylene'), extIOR=p.get('extIOR', 'air'),
+                          diffuseReflectance=tex.get('diffuseReflectance', p.get('diffuseReflectance', (0.5, 0.5, 0.5))),
+                          nonlinear=p.get('nonlinear', False), rtransDir=os.path.dirname(os.path.abspath(self.path)))
             return BSDF(t, **kw)
         raise NotImplementedError('BSDF plugin "%s" is not on the GPU path (diffuse, roughconductor, '
-                                  'roughdielectric)' % t)
+                                  'roughdielectric, roughplastic)' % t)
 
     def make_area(self, p):
         if p.plugin != 'area':
@@ -524,6 +548,21 @@ def _rgb(name, c):
     return '<rgb name="%s" value="%s"/>' % (name, ', '.join(_fmt(x) for x in c))
 
 
+def _checker_xml(name, t):
+    return ('<texture type="checkerboard" name="%s">%s%s<float name="uoffset" value="%s"/>'
+            '<float name="voffset" value="%s"/><float name="uscale" value="%s"/><float name="vscale" value="%s"/>'
+            '</texture>' % (name, _rgb('color0', _spec3(t.color0)), _rgb('color1', _spec3(t.color1)), _fmt(t.uoffset),
+                            _fmt(t.voffset), _fmt(t.uscale), _fmt(t.vscale)))
+
+
+def _spec3(v):
+    return (v,) * 3 if isinstance(v, (int, float, np.floating)) else v
+
+
+def _spec_xml(name, v):
+    return _checker_xml(name, v) if isinstance(v, Checkerboard) else _rgb(name, _spec3(v))
+
+
 def _matrix(m):
     return '<matrix value="%s"/>' % ' '.join(_fmt(x) for x in np.asarray(m, f32).reshape(-1))
 
@@ -582,10 +621,12 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     for i, b in enumerate(scene.bsdfs):
         L.append('  <bsdf type="%s" id="bsdf%d">' % (b.type, i))
         if b.type == 'diffuse':
-            L.append('    ' + _rgb('reflectance', b.reflectance))
+            L.append('    ' + _spec_xml('reflectance', b.reflectance))
         else:
             L.append('    <string name="distribution" value="%s"/>' % b.distribution)
-            if b.alpha is not None:
+            if isinstance(b.alpha, Checkerboard):
+                L.append('    ' + _checker_xml('alpha', b.alpha))
+            elif b.alpha is not None:
                 L.append('    <float name="alpha" value="%s"/>' % _fmt(b.alpha))
             elif b.alphaU is not None:
                 L.append('    <float name="alphaU" value="%s"/><float name="alphaV" value="%s"/>'
@@ -602,11 +643,14 @@ def save_scene(scene, integ, directory, name='scene.xml'):
                 L.append('    <%s name="extEta" value="%s"/>' % (('string', b.extEta) if isinstance(b.extEta, str)
                                                                  else ('float', _fmt(b.extEta))))
             else:
-                for nm in ('intIOR', 'extIOR'):
-                    v = getattr(b, nm)
+                for nm, v in (('intIOR', b.int_ior()), ('extIOR', b.extIOR)):
                     L.append('    <%s name="%s" value="%s"/>' % (('string', nm, v) if isinstance(v, str)
                                                                   else ('float', nm, _fmt(v))))
-                L.append('    ' + _rgb('specularTransmittance', b.specularTransmittance))
+                if b.type == 'roughdielectric':
+                    L.append('    ' + _rgb('specularTransmittance', b.specularTransmittance))
+                else:
+                    L.append('    ' + _spec_xml('diffuseReflectance', b.diffuseReflectance))
+                    L.append('    <boolean name="nonlinear" value="%s"/>' % str(bool(b.nonlinear)).lower())
         L.append('  </bsdf>')
     for i, m in enumerate(scene.meshes):
         fn = 'mesh%03d.ply' % i

@@ -48,6 +48,7 @@ def lib():
         L.oracle_camera.argtypes = [C.POINTER(abi.SensorDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 6 + [C.c_int]
         L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 4 + [C.c_int]
+        L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]
         rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
@@ -55,6 +56,12 @@ def lib():
             raise RuntimeError('oracle_sobol_init failed: %d' % rc)
         _lib = L
     return _lib
+
+
+def configure_rc(scene):
+    """The oracle's configure() status for `scene` (0 = accepted)."""
+    d = scene.desc()
+    return lib().oracle_configure(C.byref(d))
 
 
 def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0)):

@@ -30,6 +30,7 @@
 #include "mts_oracle.h"
 
 #include <float.h>
+#include <limits.h>
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -832,13 +833,182 @@ enum { /* BSDF::EBSDFType (include/mitsuba/render/bsdf.h) */
 #define E_TRANSMISSION (E_DIFF_TRANS | E_GLOSSY_TRANS | E_DELTA_TRANS | E_NULL)
 #define E_DELTA (E_NULL | E_DELTA_REFL | E_DELTA_TRANS)
 
+/* Texture2D + checkerboard (librender/texture.cpp:81-121, textures/checkerboard.cpp) */
+typedef struct { int type; V3 c0, c1; float uoff, voff, us, vs; } Tex;
+
+/* RoughTransmittance (bsdfs/rtrans.h:46-448) */
+typedef struct {
+    size_t eta, alpha, theta;
+    float etaMin, etaMax, alphaMin, alphaMax;
+    int etaFixed, alphaFixed;
+    float *trans, *diff;
+} RTab;
+
 typedef struct {
     int type, distr, sampleVisible, flags;
     float alpha; /* texture average, isotropic */
     float alphaU, alphaV;
     V3 refl, specR, specT, eta3, k3;
     float eta, invEta;
+    /* roughplastic (roughplastic.cpp:197-300); refl = diffuseReflectance */
+    float specWeight, invEta2;
+    int nonlinear;
+    RTab ext, in;
+    Tex reflTex, alphaTex;
 } Bsdf;
+
+/* (int) of a float the way x86-64 cvttss2si converts it: out of range / NaN -> INT_MIN */
+static inline int x86_f2i(float f) { return (f > -2147483648.0f && f < 2147483648.0f) ? (int)f : INT_MIN; }
+static inline int imodulo(int a, int b) { int r = a % b; return (r < 0) ? r + b : r; } /* math.h:42 */
+
+static V3 tex_eval(const Tex *t, float u, float v) { /* Texture2D::eval + Checkerboard::eval */
+    float uu = u * t->us + t->uoff, vv = v * t->vs + t->voff;
+    int x = 2 * imodulo(x86_f2i(uu * 2), 2) - 1, y = 2 * imodulo(x86_f2i(vv * 2), 2) - 1;
+    return (x * y == 1) ? t->c0 : t->c1;
+}
+
+/* spline.cpp:23-60 */
+static float o_cubic1d(float x, const float *values, size_t size, float min, float max) {
+    if (!(x >= min && x <= max)) return 0.0f;
+    float t = ((x - min) * (float)(size - 1)) / (max - min);
+    size_t k = (size_t)t;
+    if (k > size - 2) k = size - 2;
+    float f0 = values[k], f1 = values[k + 1], d0, d1;
+    if (k > 0) d0 = 0.5f * (values[k + 1] - values[k - 1]);
+    else d0 = values[k + 1] - values[k];
+    if (k + 2 < size) d1 = 0.5f * (values[k + 2] - values[k]);
+    else d1 = values[k + 1] - values[k];
+    t = t - (float)k;
+    float t2 = t * t, t3 = t2 * t;
+    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+}
+/* per-dimension knot weights of evalCubicInterp2D/3D (spline.cpp:241-283) */
+static int o_cubic_w(float p, size_t size, size_t *knot, float w[4]) {
+    if (!(p >= 0.0f && p <= 1.0f)) return 0;
+    float t = ((p - 0.0f) * (float)(size - 1)) / (1.0f - 0.0f);
+    size_t k = (size_t)t;
+    if (k > size - 2) k = size - 2;
+    *knot = k;
+    t = t - (float)k;
+    float t2 = t * t, t3 = t2 * t;
+    w[0] = 0.0f; w[1] = 2 * t3 - 3 * t2 + 1; w[2] = -2 * t3 + 3 * t2; w[3] = 0.0f;
+    float d0 = t3 - 2 * t2 + t, d1 = t3 - t2;
+    if (k > 0) { w[2] += 0.5f * d0; w[0] -= 0.5f * d0; } else { w[2] += d0; w[1] -= d0; }
+    if (k + 2 < size) { w[3] += 0.5f * d1; w[1] -= 0.5f * d1; } else { w[2] += d1; w[1] -= d1; }
+    return 1;
+}
+static float o_cubic2d(float px, float py, const float *values, size_t sx, size_t sy) { /* spline.cpp:236-304 */
+    size_t kx, ky; float wx[4], wy[4];
+    if (!o_cubic_w(px, sx, &kx, wx) || !o_cubic_w(py, sy, &ky, wy)) return 0.0f;
+    float result = 0.0f;
+    for (int y = -1; y <= 2; ++y) {
+        float w = wy[y + 1];
+        for (int x = -1; x <= 2; ++x) {
+            float wxy = wx[x + 1] * w;
+            if (wxy == 0) continue;
+            result += values[(ky + y) * sx + kx + x] * wxy;
+        }
+    }
+    return result;
+}
+static float o_cubic3d(float px, float py, float pz, const float *values, size_t sx, size_t sy, size_t sz) {
+    size_t kx, ky, kz; float wx[4], wy[4], wz[4]; /* spline.cpp:379-451 */
+    if (!o_cubic_w(px, sx, &kx, wx) || !o_cubic_w(py, sy, &ky, wy) || !o_cubic_w(pz, sz, &kz, wz)) return 0.0f;
+    float result = 0.0f;
+    for (int z = -1; z <= 2; ++z) {
+        float w = wz[z + 1];
+        for (int y = -1; y <= 2; ++y) {
+            float wyz = wy[y + 1] * w;
+            for (int x = -1; x <= 2; ++x) {
+                float wxyz = wx[x + 1] * wyz;
+                if (wxyz == 0) continue;
+                result += values[((kz + z) * sy + (ky + y)) * sx + kx + x] * wxyz;
+            }
+        }
+    }
+    return result;
+}
+
+static void rtab_free(RTab *t) { free(t->trans); free(t->diff); t->trans = t->diff = NULL; }
+
+static int rtab_load(const void *data, size_t bytes, RTab *t) { /* rtrans.h:46-150 */
+    const size_t hl = 17, fixed = hl + 24 + 16;
+    const unsigned char *p = (const unsigned char *)data;
+    memset(t, 0, sizeof *t);
+    if (!data || bytes < fixed || memcmp(p, "MTS_TRANSMITTANCE", hl) != 0) return MTSGPU_EINVAL;
+    uint64_t sz[3]; float r[4];
+    memcpy(sz, p + hl, 24); memcpy(r, p + hl + 24, 16);
+    t->eta = (size_t)sz[0]; t->alpha = (size_t)sz[1]; t->theta = (size_t)sz[2];
+    t->etaMin = r[0]; t->etaMax = r[1]; t->alphaMin = r[2]; t->alphaMax = r[3];
+    if (t->eta < 2 || t->alpha < 2 || t->theta < 2 || t->eta > 4096 || t->alpha > 4096 || t->theta > 4096)
+        return MTSGPU_EINVAL;
+    size_t ts = 2 * t->eta * t->alpha * t->theta, ds = 2 * t->eta * t->alpha;
+    if (bytes != fixed + (ts + ds) * 4) return MTSGPU_EINVAL;
+    t->trans = (float *)malloc(ts * 4); t->diff = (float *)malloc(ds * 4);
+    const unsigned char *f = p + fixed;
+    size_t a = 0, b = 0;
+    for (size_t i = 0; i < 2 * t->eta; ++i)
+        for (size_t j = 0; j < t->alpha; ++j) {
+            for (size_t k = 0; k < t->theta; ++k) { memcpy(&t->trans[a++], f, 4); f += 4; }
+            memcpy(&t->diff[b++], f, 4); f += 4;
+        }
+    return MTSGPU_OK;
+}
+static void rtab_clone(const RTab *s, RTab *d) {
+    *d = *s;
+    size_t ts = 2 * s->eta * s->alpha * s->theta, ds = 2 * s->eta * s->alpha;
+    d->trans = (float *)malloc(ts * 4); memcpy(d->trans, s->trans, ts * 4);
+    d->diff = (float *)malloc(ds * 4); memcpy(d->diff, s->diff, ds * 4);
+}
+/* setEta / setAlpha (rtrans.h:262-360): configure-time, glibc powf as the reference */
+static void rtab_set_eta(RTab *t, float eta) {
+    if (t->etaFixed) return;
+    const float *trans = t->trans, *diffTrans = t->diff;
+    if (eta < 1) { trans += t->eta * t->alpha * t->theta; diffTrans += t->eta * t->alpha; eta = 1.0f / eta; }
+    if (eta < t->etaMin) eta = t->etaMin;
+    float warpedEta = powf((eta - t->etaMin) / (t->etaMax - t->etaMin), 0.25f);
+    float *nt = (float *)malloc(t->alpha * t->theta * 4), *nd = (float *)malloc(t->alpha * 4);
+    float dAlpha = 1.0f / (t->alpha - 1), dTheta = 1.0f / (t->theta - 1);
+    for (size_t i = 0; i < t->alpha; ++i) {
+        for (size_t j = 0; j < t->theta; ++j)
+            nt[i * t->theta + j] = o_cubic3d(j * dTheta, i * dAlpha, warpedEta, trans, t->theta, t->alpha, t->eta);
+        nd[i] = o_cubic2d(i * dAlpha, warpedEta, diffTrans, t->alpha, t->eta);
+    }
+    free(t->trans); free(t->diff);
+    t->trans = nt; t->diff = nd; t->etaFixed = 1;
+}
+static void rtab_set_alpha(RTab *t, float alpha) {
+    if (t->alphaFixed) return;
+    float warpedAlpha = powf((alpha - t->alphaMin) / (t->alphaMax - t->alphaMin), 0.25f);
+    float *nt = (float *)malloc(t->theta * 4), *nd = (float *)malloc(4);
+    float dTheta = 1.0f / (t->theta - 1);
+    for (size_t i = 0; i < t->theta; ++i) nt[i] = o_cubic2d(i * dTheta, warpedAlpha, t->trans, t->theta, t->alpha);
+    nd[0] = o_cubic1d(warpedAlpha, t->diff, t->alpha, 0.0f, 1.0f);
+    free(t->trans); free(t->diff);
+    t->trans = nt; t->diff = nd; t->alphaFixed = 1;
+}
+/* eval / evalDiffuse on an eta-reduced table (rtrans.h:179-247); render-time pow */
+static float rtab_eval(const RTab *t, float cosTheta, float alpha) {
+    float warpedCosTheta = o_pow(fabsf(cosTheta), 0.25f), result;
+    if (!(cosTheta >= 0)) return 0.f;
+    if (t->alphaFixed) {
+        result = o_cubic1d(warpedCosTheta, t->trans, t->theta, 0.0f, 1.0f);
+    } else {
+        float warpedAlpha = o_pow((alpha - t->alphaMin) / (t->alphaMax - t->alphaMin), 0.25f);
+        result = o_cubic2d(warpedCosTheta, warpedAlpha, t->trans, t->theta, t->alpha);
+    }
+    return smin(1.0f, smax(0.0f, result));
+}
+static float rtab_eval_diffuse(const RTab *t, float alpha) {
+    float result;
+    if (t->alphaFixed) {
+        result = t->diff[0];
+    } else {
+        float warpedAlpha = o_pow((alpha - t->alphaMin) / (t->alphaMax - t->alphaMin), 0.25f);
+        result = o_cubic1d(warpedAlpha, t->diff, t->alpha, 0.0f, 1.0f);
+    }
+    return smin(1.0f, smax(0.0f, result));
+}
 
 static float tex_scale_for_energy(V3 v, int ensure) { /* bsdf.cpp:88-112 */
     if (!ensure) return 1.0f;
@@ -847,18 +1017,92 @@ static float tex_scale_for_energy(V3 v, int ensure) { /* bsdf.cpp:88-112 */
     return 1.0f;
 }
 
+static V3 d3(const float *f) { return v3(f[0], f[1], f[2]); }
+/* getMaximum / getMinimum / getAverage of a constant or checkerboard texture */
+static V3 tdesc_max(const mtsgpu_texture_desc *t, V3 c) {
+    return t->type ? v3(smax(t->color0[0], t->color1[0]), smax(t->color0[1], t->color1[1]), smax(t->color0[2], t->color1[2])) : c;
+}
+static V3 tdesc_min(const mtsgpu_texture_desc *t, V3 c) {
+    return t->type ? v3(smin(t->color0[0], t->color1[0]), smin(t->color0[1], t->color1[1]), smin(t->color0[2], t->color1[2])) : c;
+}
+static V3 tdesc_avg(const mtsgpu_texture_desc *t, V3 c) {
+    return t->type ? vmul(vadd(d3(t->color0), d3(t->color1)), 0.5f) : c;
+}
+static float luminance3(V3 s) { return s.x * 0.212671f + s.y * 0.715160f + s.z * 0.072169f; } /* spectrum.h:725 */
+/* the texture as configured, ScaleTexture (scale.cpp:85-87) folded into its colours */
+static int tex_configure(const mtsgpu_texture_desc *t, float scale, Tex *o) {
+    memset(o, 0, sizeof *o);
+    if (t->type == MTSGPU_TEX_NONE) return MTSGPU_OK;
+    if (t->type != MTSGPU_TEX_CHECKERBOARD) return MTSGPU_EINVAL;
+    o->type = t->type;
+    o->c0 = d3(t->color0); o->c1 = d3(t->color1);
+    if (scale != 1.0f) { o->c0 = vmul(o->c0, scale); o->c1 = vmul(o->c1, scale); }
+    o->uoff = t->uoffset; o->voff = t->voffset; o->us = t->uscale; o->vs = t->vscale;
+    return MTSGPU_OK;
+}
+
+static void bsdf_free(Bsdf *b) { rtab_free(&b->ext); rtab_free(&b->in); }
+
+/* RoughPlastic ctor + configure (roughplastic.cpp:197-300) */
+static int roughplastic_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
+    if (d->int_ior < 0 || d->ext_ior < 0 || d->int_ior == d->ext_ior) return MTSGPU_EINVAL;
+    b->eta = d->int_ior / d->ext_ior;
+    b->nonlinear = d->nonlinear != 0;
+    if (d->distribution < 0 || d->distribution > 2) return MTSGPU_EINVAL;
+    b->distr = d->distribution;
+    b->sampleVisible = d->distribution == MTSGPU_DISTR_PHONG ? 0 : d->sample_visible;
+    float au = smax(d->alpha_u, 1e-4f), av = smax(d->alpha_v, 1e-4f);
+    if (d->alpha_tex.type == MTSGPU_TEX_NONE && au != av) return MTSGPU_EINVAL; /* anisotropic */
+    b->alphaU = b->alphaV = savg(v3(au, au, au));
+    V3 dr = d3(d->diffuse_reflectance), sr = d3(d->specular_reflectance);
+    float sd = tex_scale_for_energy(tdesc_max(&d->reflectance_tex, dr), d->ensure_energy_conservation);
+    float ss = tex_scale_for_energy(sr, d->ensure_energy_conservation);
+    b->refl = sd != 1.0f ? vmul(dr, sd) : dr;
+    b->specR = ss != 1.0f ? vmul(sr, ss) : sr;
+    int rc;
+    if ((rc = tex_configure(&d->reflectance_tex, sd, &b->reflTex))) return rc;
+    if ((rc = tex_configure(&d->alpha_tex, 1.0f, &b->alphaTex))) return rc;
+    V3 davg = tdesc_avg(&d->reflectance_tex, dr);
+    if (sd != 1.0f) davg = vmul(davg, sd);
+    float dAvg = luminance3(davg), sAvg = luminance3(b->specR);
+    b->specWeight = sAvg / (dAvg + sAvg);
+    b->invEta2 = 1.0f / (b->eta * b->eta);
+    b->flags = E_GLOSSY_REFL | E_DIFF_REFL | E_FRONT;
+    if ((rc = rtab_load(d->rtrans_data, (size_t)d->rtrans_bytes, &b->ext))) return rc;
+    /* checkEta / checkAlpha (rtrans.h:371-388) */
+    float e = b->eta < 1 ? 1 / b->eta : b->eta;
+    V3 a3 = v3(au, au, au);
+    float amin = savg(tdesc_min(&d->alpha_tex, a3)), amax = savg(tdesc_max(&d->alpha_tex, a3));
+    if (e < b->ext.etaMin || e > b->ext.etaMax || amin < b->ext.alphaMin || amin > b->ext.alphaMax ||
+        amax < b->ext.alphaMin || amax > b->ext.alphaMax) { bsdf_free(b); return MTSGPU_EINVAL; }
+    rtab_clone(&b->ext, &b->in);
+    rtab_set_eta(&b->ext, b->eta);
+    rtab_set_eta(&b->in, 1 / b->eta);
+    if (d->alpha_tex.type == MTSGPU_TEX_NONE) rtab_set_alpha(&b->ext, b->alphaU);
+    return MTSGPU_OK;
+}
+
 static int bsdf_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
     memset(b, 0, sizeof *b);
     b->type = d->type;
     if (d->type == MTSGPU_BSDF_DIFFUSE) {
-        V3 r = v3(d->reflectance[0], d->reflectance[1], d->reflectance[2]);
-        float sc = tex_scale_for_energy(r, d->ensure_energy_conservation);
+        V3 r = d3(d->reflectance);
+        float sc = tex_scale_for_energy(tdesc_max(&d->reflectance_tex, r), d->ensure_energy_conservation);
         if (sc != 1.0f) r = vmul(r, sc);
         b->refl = r;
-        b->flags = (smaxc(r) > 0) ? (E_DIFF_REFL | E_FRONT) : 0; /* diffuse.cpp:93-101 */
+        int rc = tex_configure(&d->reflectance_tex, sc, &b->reflTex);
+        if (rc) return rc;
+        V3 mx = b->reflTex.type ? v3(smax(b->reflTex.c0.x, b->reflTex.c1.x), smax(b->reflTex.c0.y, b->reflTex.c1.y),
+                                     smax(b->reflTex.c0.z, b->reflTex.c1.z)) : r;
+        b->flags = (smaxc(mx) > 0) ? (E_DIFF_REFL | E_FRONT) : 0; /* diffuse.cpp:93-101 */
         return MTSGPU_OK;
     }
+    if (d->type == MTSGPU_BSDF_ROUGHPLASTIC) return roughplastic_configure(d, b);
     if (d->type != MTSGPU_BSDF_ROUGHCONDUCTOR && d->type != MTSGPU_BSDF_ROUGHDIELECTRIC) return MTSGPU_EINVAL;
+    if (d->alpha_tex.type != MTSGPU_TEX_NONE) {
+        int rc = tex_configure(&d->alpha_tex, 1.0f, &b->alphaTex);
+        if (rc) return rc;
+    }
     if (d->distribution < 0 || d->distribution > 2) return MTSGPU_EINVAL;
     b->distr = d->distribution;
     /* MicrofacetDistribution(props) (microfacet.h:105-150) */
@@ -890,20 +1134,71 @@ static int bsdf_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
     return MTSGPU_OK;
 }
 
-typedef struct { V3 wi, wo; float eta; int sampledType; } BRec;
+typedef struct { V3 wi, wo; float eta; int sampledType; float u, v; /* its.uv */ } BRec;
+
+static V3 bsdf_refl(const Bsdf *b, const BRec *r) { /* m_reflectance->eval(bRec.its) */
+    return b->reflTex.type ? tex_eval(&b->reflTex, r->u, r->v) : b->refl;
+}
+/* MicrofacetDistribution at the hit: m_alpha->eval(its).average() for a texture */
+static void bsdf_distr(const Bsdf *b, const BRec *r, Distr *d) {
+    if (b->alphaTex.type) {
+        float a = savg(tex_eval(&b->alphaTex, r->u, r->v));
+        distr_init(d, b->distr, a, a, b->sampleVisible);
+    } else {
+        distr_init(d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    }
+}
+
+static float rp_prob_specular(const Bsdf *b, float cosThetaI, float alpha) { /* roughplastic.cpp:371-378 */
+    float probSpecular = 1 - rtab_eval(&b->ext, cosThetaI, alpha);
+    probSpecular = (probSpecular * b->specWeight) /
+                   (probSpecular * b->specWeight + (1 - probSpecular) * (1 - b->specWeight));
+    return probSpecular;
+}
+static V3 rp_eval(const Bsdf *b, const BRec *r) { /* RoughPlastic::eval (roughplastic.cpp:300-345) */
+    if (r->wi.z <= 0 || r->wo.z <= 0) return v3(0, 0, 0);
+    Distr d; bsdf_distr(b, r, &d);
+    V3 result = v3(0, 0, 0);
+    V3 H = vnormalize(vadd(r->wo, r->wi));
+    float D = distr_eval(&d, H);
+    float ct;
+    float F = fresnel_dielectric_ext(vdot(r->wi, H), &ct, b->eta);
+    float G = distr_G(&d, r->wi, r->wo, H);
+    float value = F * D * G / (4.0f * r->wi.z);
+    result = vadd(result, vmul(b->specR, value));
+    V3 diff = bsdf_refl(b, r);
+    float T12 = rtab_eval(&b->ext, r->wi.z, d.alphaU);
+    float T21 = rtab_eval(&b->ext, r->wo.z, d.alphaU);
+    float Fdr = 1 - rtab_eval_diffuse(&b->in, d.alphaU);
+    if (b->nonlinear) diff = vdivv(diff, vsub(v3(1.0f, 1.0f, 1.0f), vmul(diff, Fdr)));
+    else diff = vdiv(diff, 1 - Fdr);
+    return vadd(result, vmul(diff, INV_PI_F * r->wo.z * T12 * T21 * b->invEta2));
+}
+static float rp_pdf(const Bsdf *b, const BRec *r) { /* RoughPlastic::pdf (roughplastic.cpp:347-393) */
+    if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
+    Distr d; bsdf_distr(b, r, &d);
+    V3 H = vnormalize(vadd(r->wo, r->wi));
+    float probSpecular = rp_prob_specular(b, r->wi.z, d.alphaU), probDiffuse = 1 - probSpecular;
+    float dwh_dwo = 1.0f / (4.0f * vdot(r->wo, H));
+    float prob = distr_pdf(&d, r->wi, H);
+    float result = prob * dwh_dwo * probSpecular;
+    result += probDiffuse * cosine_hemisphere_pdf(r->wo);
+    return result;
+}
 
 static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
     V3 zero = v3(0, 0, 0);
     if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:110-117 */
         /* bRec.typeMask = EAll, so only the cosine tests can reject */
         if (r->wi.z <= 0 || r->wo.z <= 0) return zero;
-        return vmul(b->refl, INV_PI_F * r->wo.z);
+        return vmul(bsdf_refl(b, r), INV_PI_F * r->wo.z);
     }
+    if (b->type == MTSGPU_BSDF_ROUGHPLASTIC) return rp_eval(b, r);
     Distr d;
     if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:257-292 */
         if (r->wi.z <= 0 || r->wo.z <= 0) return zero;
         V3 H = vnormalize(vadd(r->wo, r->wi));
-        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        bsdf_distr(b, r, &d);
         float D = distr_eval(&d, H);
         if (D == 0) return zero;
         V3 F = vmulv(fresnel_conductor_exact(vdot(r->wi, H), b->eta3, b->k3), b->specR);
@@ -922,7 +1217,7 @@ static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
         H = vnormalize(vadd(r->wi, vmul(r->wo, eta)));
     }
     H = vmul(H, signumf(H.z));
-    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    bsdf_distr(b, r, &d);
     float D = distr_eval(&d, H);
     if (D == 0) return zero;
     float ct;
@@ -945,11 +1240,12 @@ static float bsdf_pdf(const Bsdf *b, const BRec *r) {
         if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
         return cosine_hemisphere_pdf(r->wo);
     }
+    if (b->type == MTSGPU_BSDF_ROUGHPLASTIC) return rp_pdf(b, r);
     Distr d;
     if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:294-319 */
         if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
         V3 H = vnormalize(vadd(r->wo, r->wi));
-        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        bsdf_distr(b, r, &d);
         if (b->sampleVisible)
             return distr_eval(&d, H) * distr_smithG1(&d, r->wi, H) / (4.0f * r->wi.z);
         return distr_pdf(&d, r->wi, H) / (4 * vabsdot(r->wo, H));
@@ -968,7 +1264,7 @@ static float bsdf_pdf(const Bsdf *b, const BRec *r) {
         dwh_dwo = (eta * eta * vdot(r->wo, H)) / (sqrtDenom * sqrtDenom);
     }
     H = vmul(H, signumf(H.z));
-    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    bsdf_distr(b, r, &d);
     if (!b->sampleVisible) distr_scale_alpha(&d, 1.2f - 0.2f * sqrtf(fabsf(r->wi.z)));
     float prob = distr_pdf(&d, vmul(r->wi, signumf(r->wi.z)), H);
     float ct;
@@ -987,12 +1283,38 @@ static V3 bsdf_sample(const Bsdf *b, BRec *r, float *pdf, float sx, float sy, Sa
         r->eta = 1.0f;
         r->sampledType = E_DIFF_REFL;
         *pdf = cosine_hemisphere_pdf(r->wo);
-        return b->refl;
+        return bsdf_refl(b, r);
+    }
+    if (b->type == MTSGPU_BSDF_ROUGHPLASTIC) { /* RoughPlastic::sample (roughplastic.cpp:395-458) */
+        if (r->wi.z <= 0) return zero;
+        int choseSpecular = 1;
+        Distr dd; bsdf_distr(b, r, &dd);
+        float probSpecular = rp_prob_specular(b, r->wi.z, dd.alphaU);
+        if (sy < probSpecular) {
+            sy /= probSpecular;
+        } else {
+            sy = (sy - probSpecular) / (1 - probSpecular);
+            choseSpecular = 0;
+        }
+        if (choseSpecular) {
+            float mpdf;
+            V3 m = distr_sample(&dd, r->wi, sx, sy, &mpdf);
+            r->wo = reflect_v(r->wi, m);
+            r->sampledType = E_GLOSSY_REFL;
+            if (r->wo.z <= 0) return zero;
+        } else {
+            r->sampledType = E_DIFF_REFL;
+            r->wo = square_to_cosine_hemisphere(sx, sy);
+        }
+        r->eta = 1.0f;
+        *pdf = rp_pdf(b, r);
+        if (*pdf == 0) return zero;
+        return vdiv(rp_eval(b, r), *pdf);
     }
     Distr d;
     if (b->type == MTSGPU_BSDF_ROUGHCONDUCTOR) { /* roughconductor.cpp:357-406 */
         if (r->wi.z < 0) return zero;
-        distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+        bsdf_distr(b, r, &d);
         V3 m = distr_sample(&d, r->wi, sx, sy, pdf);
         if (*pdf == 0) return zero;
         r->wo = reflect_v(r->wi, m);
@@ -1007,7 +1329,7 @@ static V3 bsdf_sample(const Bsdf *b, BRec *r, float *pdf, float sx, float sy, Sa
         return vmul(F, weight);
     }
     /* roughdielectric.cpp:525-615 */
-    distr_init(&d, b->distr, b->alphaU, b->alphaV, b->sampleVisible);
+    bsdf_distr(b, r, &d);
     Distr sd = d;
     if (!b->sampleVisible) distr_scale_alpha(&sd, 1.2f - 0.2f * sqrtf(fabsf(r->wi.z)));
     float microfacetPDF;
@@ -1625,6 +1947,7 @@ static void scene_free(Scene *S) {
         Mesh *m = &S->meshes[i];
         free(m->pos); free(m->nrm); free(m->uv); free(m->idx); free(m->dpdu); free(m->areaCdf);
     }
+    if (S->bsdfs) for (uint32_t i = 0; i < S->nbsdfs + 2; ++i) bsdf_free(&S->bsdfs[i]);
     free(S->meshes); free(S->bsdfs); free(S->emitters); free(S->emCdf);
     free(S->ta); free(S->taMesh); free(S->taTri); free(S->nodes); free(S->order);
     if (S->env) { env_free(S->env); free(S->env); }
@@ -1856,6 +2179,7 @@ typedef struct {
     V3 p, geoN, wi;
     Frame sh;
     int mesh; uint32_t tri;
+    float u, v;   /* its.uv */
 } Its;
 
 /* ShapeKDTree::rayIntersect(ray, its) (skdtree.cpp:112-142) + fillIntersectionRecord<true>
@@ -1896,6 +2220,12 @@ static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *
     its->geoN = faceNormal;
     compute_shading_frame(shN, dpdu, &its->sh);
     its->wi = to_local(&its->sh, vneg(ray->d));
+    if (m->uv) { /* skdtree.h:398-405 */
+        its->u = m->uv[2 * i0] * bx + m->uv[2 * i1] * by + m->uv[2 * i2] * bz;
+        its->v = m->uv[2 * i0 + 1] * bx + m->uv[2 * i1 + 1] * by + m->uv[2 * i2 + 1] * bz;
+    } else {
+        its->u = by; its->v = bz;
+    }
 }
 
 /* ShapeKDTree::rayIntersect(ray) shadow variant (skdtree.cpp:207-226) */
@@ -2097,6 +2427,7 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
                 BRec bRec;
                 bRec.wi = its.wi;
                 bRec.wo = to_local(&its.sh, dRec.d);
+                bRec.u = its.u; bRec.v = its.v;
                 V3 bsdfVal = bsdf_eval(bsdf, &bRec);
                 if (!vzero(bsdfVal) && (!P->strict || vdot(its.geoN, dRec.d) * bRec.wo.z > 0)) {
                     float bsdfPdf = dRec.measureSolidAngle ? bsdf_pdf(bsdf, &bRec) : 0;
@@ -2108,7 +2439,7 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
 
         float bsdfPdf;
         BRec bRec;
-        bRec.wi = its.wi; bRec.eta = 1.0f; bRec.sampledType = 0;
+        bRec.wi = its.wi; bRec.eta = 1.0f; bRec.sampledType = 0; bRec.u = its.u; bRec.v = its.v;
         float bx, by;
         next2d(smp, &bx, &by);
         V3 bsdfWeight = bsdf_sample(bsdf, &bRec, &bsdfPdf, bx, by, smp);
@@ -2370,16 +2701,34 @@ int oracle_camera(const mtsgpu_sensor_desc *s, float *m16, float *dxdy6) {
 
 /* one BSDF::sample(bRec, pdf, sample) with a replayable 1D sample u3[2]
  * (the FakeSampler of test_chisquare.cpp:58-88) */
+/* the probes configure a BSDF once per distinct description (roughplastic
+ * reduces its transmittance tables in configure) */
+static mtsgpu_bsdf_desc g_probe_desc;
+static Bsdf g_probe_bsdf;
+static int g_probe_valid = 0;
+static int probe_bsdf(const mtsgpu_bsdf_desc *bd, Bsdf *out) {
+    if (!g_probe_valid || memcmp(bd, &g_probe_desc, sizeof *bd) != 0) {
+        if (g_probe_valid) bsdf_free(&g_probe_bsdf);
+        g_probe_valid = 0;
+        int rc = bsdf_configure(bd, &g_probe_bsdf);
+        if (rc) return rc;
+        g_probe_desc = *bd;
+        g_probe_valid = 1;
+    }
+    *out = g_probe_bsdf;
+    return MTSGPU_OK;
+}
+
 int oracle_bsdf_sample(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *u3,
                        float *wo3, float *weight3, float *pdf, float *eta, int libm_mode) {
     g_cr = libm_mode;
     Bsdf b;
-    int rc = bsdf_configure(bd, &b);
+    int rc = probe_bsdf(bd, &b);
     if (rc) return rc;
     /* replay: a one-dimension Sobol index that returns u3[2] is not available,
      * so next1D is served from a tiny stub sampler */
     Sampler s; memset(&s, 0, sizeof s);
-    BRec r; r.wi = v3(wi3[0], wi3[1], wi3[2]); r.eta = 1.0f; r.sampledType = 0;
+    BRec r; r.wi = v3(wi3[0], wi3[1], wi3[2]); r.eta = 1.0f; r.sampledType = 0; r.u = r.v = 0;
     V3 w;
     if (b.type == MTSGPU_BSDF_ROUGHDIELECTRIC) {
         /* emulate next1D() = u3[2] by sampling dimension 0 of index 0 -> 0.0 is
@@ -2403,13 +2752,21 @@ int oracle_bsdf_eval(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *
                      float *value3, float *pdf, int libm_mode) {
     g_cr = libm_mode;
     Bsdf b;
-    int rc = bsdf_configure(bd, &b);
+    int rc = probe_bsdf(bd, &b);
     if (rc) return rc;
     BRec r; r.wi = v3(wi3[0], wi3[1], wi3[2]); r.wo = v3(wo3[0], wo3[1], wo3[2]); r.eta = 1; r.sampledType = 0;
+    r.u = r.v = 0;
     V3 v = bsdf_eval(&b, &r);
     value3[0] = v.x; value3[1] = v.y; value3[2] = v.z;
     *pdf = bsdf_pdf(&b, &r);
     return MTSGPU_OK;
+}
+
+int oracle_configure(const mtsgpu_scene_desc *scene) {
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    scene_free(&S);
+    return rc;
 }
 
 int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,

@@ -37,6 +37,8 @@ int oracle_triaccel_intersect(const float *ta10, const float *o, const float *d,
  * texels with 4 halves per texel) */
 int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
                       float *rows, float *cols, float *weights);
+/* configure() only: the status the reference's plugin constructors/configure() raise */
+int oracle_configure(const mtsgpu_scene_desc *scene);
 int oracle_intersect(const mtsgpu_scene_desc *scene, const float *o, const float *d, float *out16);
 int oracle_camera(const mtsgpu_sensor_desc *s, float *sample_to_camera16, float *dxdy6);
 /* Microfacet / BSDF probes for consistency tests: see mts_oracle.c */

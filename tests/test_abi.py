@@ -27,13 +27,14 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(integrator.EXPORTS) <= set(names)
-    assert L.mtsgpu_abi_version() == 1
+    assert L.mtsgpu_abi_version() == abi.ABI_VERSION == 2
 
 
 STRUCTS = {'mtsgpu_bsdf_desc': abi.BsdfDesc, 'mtsgpu_emitter_desc': abi.EmitterDesc,
            'mtsgpu_mesh_desc': abi.MeshDesc, 'mtsgpu_sensor_desc': abi.SensorDesc,
            'mtsgpu_scene_desc': abi.SceneDesc, 'mtsgpu_render_params': abi.RenderParams,
-           'mtsgpu_stats': abi.Stats, 'mtsgpu_develop_params': abi.DevelopParams}
+           'mtsgpu_stats': abi.Stats, 'mtsgpu_develop_params': abi.DevelopParams,
+           'mtsgpu_texture_desc': abi.TextureDesc}
 
 
 def test_struct_layout_matches_python_mirror(tmp_path):

@@ -139,3 +139,25 @@ def test_xml_scene_bitexact(gpu_ctx, oracle, tmp_path):
     film_g, smp_g, _ = gpu_ctx.render(it2, samples=True)
     film_o, smp_o, _ = oracle.render(sc2, it2, samples=True, libm_mode=1)
     _compare(film_g, smp_g, film_o, smp_o)
+
+
+def test_roughplastic_and_textures_bitexact(gpu_ctx, oracle):
+    """roughplastic (GGX / Beckmann / Phong, nonlinear, visible and all-normal
+    sampling) with the rough-transmittance slices, checkerboard-textured roughness
+    (2D alpha x theta slice), textured diffuse and textured roughconductor."""
+    sc, it = scenes.build('C1', width=48, height=40, spp=16, materials='plastic')
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
+def test_c5_textured_roughplastic_bitexact(gpu_ctx, oracle):
+    """C5 at small size: the matpreview object in roughplastic GGX with a
+    checkerboard roughness over spherical UVs, under the environment map."""
+    sc, it = scenes.build('C5', width=48, height=27, spp=8, env_size=(128, 64), blob=(60, 38))
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)

@@ -4,12 +4,18 @@ eval()/pdf() (relative/absolute error 1e-2 in single precision, :33-37), and a
 chi-square goodness-of-fit of sampled directions against the integrated pdf
 (significance 0.25% per test, :27-31)."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
 from scipy import stats
 
-from mitsuba_amd.scene import BSDF
+from mitsuba_amd.scene import BSDF, Checkerboard
+
+# roughplastic reads data/microfacet/<distribution>.dat: the reference's own
+# files when this container has them, else the in-tree generated tables
+REF_MICROFACET = '/root/reference/data/microfacet'
+RT_DIR = REF_MICROFACET if os.path.isdir(REF_MICROFACET) else None
 
 ERROR_REQ = 1e-2
 CASES = {
@@ -22,6 +28,13 @@ CASES = {
     'rd_beckmann': BSDF('roughdielectric', distribution='beckmann', alpha=0.3, intIOR=1.5),
     'rd_ggx': BSDF('roughdielectric', distribution='ggx', alpha=0.2, intIOR=1.33),
     'rd_ggx_all': BSDF('roughdielectric', distribution='ggx', alpha=0.5, sampleVisible=False, intIOR=1.5),
+    # data/tests/test_bsdf.xml:131-136: roughplastic, beckmann, alpha .7
+    'rp_beckmann': BSDF('roughplastic', distribution='beckmann', alpha=0.7, rtransDir=RT_DIR),
+    'rp_ggx': BSDF('roughplastic', distribution='ggx', alpha=0.2, diffuseReflectance=(0.2, 0.5, 0.8),
+                   rtransDir=RT_DIR),
+    'rp_phong_nonlinear': BSDF('roughplastic', distribution='phong', alpha=0.3, nonlinear=True, rtransDir=RT_DIR),
+    'rp_ggx_all_tex': BSDF('roughplastic', distribution='ggx', sampleVisible=False, rtransDir=RT_DIR,
+                           alpha=Checkerboard(color0=0.25, color1=0.05)),   # uv (0,0) -> color0
 }
 
 
@@ -117,7 +130,8 @@ def _chi2(L, d, wi, n=40000, nt=16, nphi=32, seed=3, both=False, k=8):
     return stats.chi2.sf(chi2, len(po) - 1), obs.sum() / n
 
 
-@pytest.mark.parametrize('name', ['diffuse', 'rc_beckmann', 'rc_ggx', 'rc_ggx_all', 'rc_ggx_aniso', 'rd_ggx'])
+@pytest.mark.parametrize('name', ['diffuse', 'rc_beckmann', 'rc_ggx', 'rc_ggx_all', 'rc_ggx_aniso', 'rd_ggx',
+                                  'rp_beckmann', 'rp_ggx', 'rp_phong_nonlinear', 'rp_ggx_all_tex'])
 def test_chi_square_goodness_of_fit(oracle, name):
     L = oracle.lib()
     d = CASES[name].to_desc()
