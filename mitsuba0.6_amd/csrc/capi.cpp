@@ -65,7 +65,7 @@ struct mtsgpu_ctx {
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights;
     DevBuf rtrans, texcoords;
-    DevBuf film_own, film_spill, samples, counters, contrib, trav_spill;
+    DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
 };
 
@@ -293,14 +293,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.nibbles = indexBits <= 32 ? 8 : MTSG_NIBBLES;
     L.lds_dims = 32;
     L.sobol_nib = (const uint32_t *)ctx->sobol.p;
-    // traversal stack: an LDS ring of stack_depth entries per lane (power of two)
-    // whose overflow spills to trav_spill; a BVH4 level pushes at most 3 entries
-    L.spill_cap = 3 * H.bvh_depth + 4;
-    L.stack_depth = L.spill_cap <= 8 ? 8u : 16u;
-    if (const char *env = std::getenv("MTSGPU_STACK_RING")) {
-        const long v = std::strtol(env, nullptr, 10);
-        L.stack_depth = v >= 32 ? 32u : (v >= 16 ? 16u : (v >= 8 ? 8u : 4u));
-    }
+    L.stack_depth = H.bvh_depth + 2;
     L.num_nodes = (uint32_t)H.nodes.size();
     // small scenes: stage the whole BVH + TriAccel array in LDS (<= 32 KiB)
     const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri);
@@ -350,11 +343,6 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     int bpc = 0;
     mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
-    {
-        const size_t lanes = (size_t)ctx->num_cus * bpc * BLOCK_THREADS;
-        if ((e = ctx->trav_spill.ensure(lanes * L.spill_cap * 8)) != hipSuccess) return hip_fail(ctx, e, "stack spill buffer");
-        L.trav_spill = (int32_t *)ctx->trav_spill.p;
-    }
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
     if ((e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
     for (uint32_t j0 = 0; j0 < P->spp; j0 += chunk) {
@@ -463,7 +451,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
-                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib, &ctx->trav_spill,
+                      &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights,
                       &ctx->rtrans, &ctx->texcoords,
                       &ctx->dev_in, &ctx->dev_out};

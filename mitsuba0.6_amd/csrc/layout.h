@@ -2,11 +2,8 @@
 // (scene_build.cpp) and the gfx950 kernels (path_kernel.hip).
 //
 // Everything is flat SoA/AoS arrays addressed by 32-bit indices:
-//   nodes     BVH4, 48 B per node (one node fetch = 3 x 16 B loads, tests four
-//             boxes): full-precision node origin, per-axis power-of-two scale,
-//             children's boxes quantised outward to 8 bits (CWBVH-style);
-//             inner children stored consecutively from child_base, the leaf
-//             children's triangles consecutively from tri_base
+//   nodes     BVH2, 64 B per node, both children's boxes in one node (one
+//             node fetch = 4 x 16 B loads, tests two boxes)
 //   tris      48 B per primitive in BVH leaf order: the reference's TriAccel
 //             (triaccel.h:36-51) with {shapeIndex, primIndex} replaced by the
 //             global primitive id (tie-break key) and the shape id
@@ -17,7 +14,7 @@
 #include <stdint.h>
 
 #define MTSG_MAX_STACK 64     // BVH builder keeps depth < MTSG_MAX_STACK
-#define MTSG_LEAF_MAX 7       // primitives per leaf (3-bit count in MtsgNode::meta)
+#define MTSG_LEAF_MAX 8       // primitives per leaf
 #define MTSG_SOBOL_DIMS 1024
 #define MTSG_SOBOL_SIZE 52
 #define MTSG_FILTER_RES 31
@@ -28,15 +25,11 @@ static inline int32_t mtsg_leaf_ref(uint32_t first, uint32_t count) {
     return ~(int32_t)((first << 4) | count);
 }
 
-struct MtsgNode {            // 48 B BVH4 node
-    float px, py, pz;        // origin: lower corner of the union of the children's boxes
-    // bits 0-14: per-axis exponents e (scale 2^(e-16)); 15-18: inner-child mask;
-    // 19-30: 3-bit triangle count per leaf child (0 with a clear mask bit: empty slot)
-    uint32_t meta;
-    uint32_t child_base;     // node index of the first inner child
-    uint32_t tri_base;       // TriAccel slot of the first leaf child's first triangle
-    // byte c of each word: child c's box, lo = origin + q * scale (rounded outward)
-    uint32_t qlox, qhix, qloy, qhiy, qloz, qhiz;
+struct MtsgNode {            // 64 B (Aila-Laine layout)
+    float c0lox, c0hix, c0loy, c0hiy;
+    float c1lox, c1hix, c1loy, c1hiy;
+    float c0loz, c0hiz, c1loz, c1hiz;
+    int32_t c0, c1, pad0, pad1;
 };
 
 struct MtsgTri {             // 48 B
@@ -187,9 +180,7 @@ struct MtsgLaunch {
     const uint32_t *sobol_nib;        // MTSG_SOBOL_DIMS * MTSG_NIBBLES * 16 words
     uint32_t lds_dims;                // dims [0, lds_dims) staged in LDS
     uint32_t nibbles;                 // 8 (index < 2^32) or MTSG_NIBBLES
-    uint32_t stack_depth;             // LDS traversal stack entries per lane (power of two: a ring)
-    int32_t *trav_spill;              // per lane spill_cap x {ref, dist16}: the ring's overflow (global)
-    uint32_t spill_cap;               // >= the deepest possible stack (3 per BVH4 level)
+    uint32_t stack_depth;             // LDS traversal stack entries per lane
     uint32_t num_nodes;               // BVH2 inner nodes
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)

@@ -46,9 +46,6 @@ typedef __attribute__((address_space(3))) const vf4 lds_f4;
 typedef __attribute__((address_space(1))) const vf4 glb_f4;
 typedef __attribute__((address_space(3))) const vi4 lds_i4;
 typedef __attribute__((address_space(1))) const vi4 glb_i4;
-typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) const vu4 lds_u4;
-typedef __attribute__((address_space(1))) const vu4 glb_u4;
 
 template <int NIB, typename T>
 __device__ __forceinline__ uint32_t sobol_bits(T *tab, uint64_t index) {
@@ -121,47 +118,27 @@ struct Hit {
 };
 
 // ---------------------------------------------------------------------------
-// BVH4 traversal (quantised nodes, layout.h)
+// BVH2 traversal
 // ---------------------------------------------------------------------------
-// Per-lane traversal stack: a ring of stack_depth entries in LDS (lane-strided)
-// whose oldest entries spill to global memory when it is full (rare; the
-// tree's depth bounds the total at 3 entries per level).  An entry is the
-// child reference (4 B) and its entry distance as the top 16 bits of the
-// (non-negative) float, i.e. bfloat16 rounded toward zero: a lower bound of
-// the true entry distance, so culling on pop stays conservative.
+// LDS traversal stack, lane-strided: node index (4 B) + entry distance as the
+// top 16 bits of the (non-negative) float, i.e. bfloat16 rounded toward zero:
+// a lower bound of the true entry distance, so culling on pop stays
+// conservative (6 B/entry keeps 3 blocks per CU on large scenes)
 typedef __attribute__((address_space(3))) int lds_stk_n;
 typedef __attribute__((address_space(3))) uint16_t lds_stk_d;
-typedef __attribute__((address_space(1))) int glb_stk;   // {ref, dist16} pairs
 __device__ __forceinline__ uint16_t dist_down16(float t) { return (uint16_t)(__float_as_uint(fmaxf(t, 0.0f)) >> 16); }
 __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-
-struct TravStack {
-    lds_stk_n *n;          // this lane's ring (entry i at n[(i & mask) * BLOCK])
-    lds_stk_d *d;
-    glb_stk *g;            // this lane's spill area (cap entries of 2 ints)
-    uint32_t mask, cap;
-};
-
-__device__ __forceinline__ int leaf_ref(uint32_t first, uint32_t count) {   // = mtsg_leaf_ref (layout.h)
-    return ~(int)((first << 4) | count);
-}
-
-// byte c of a quantised word as a float (v_cvt_f32_ubyte<c>)
-__device__ __forceinline__ float qbyte(uint32_t w, int c) { return (float)((w >> (8 * c)) & 0xffu); }
-
-// Speculative while-while traversal (Aila & Laine 2009) over BVH4 nodes: a
-// lane that reaches a leaf parks it and keeps descending until every lane of
-// the wave holds a leaf; then all lanes test their parked leaves together.
-// Children are visited nearest first.  Same closest hit (tie rule included)
-// as any complete traversal: the boxes only ever over-approximate.
+#ifndef MTSG_TRAV_IFIF
+// Speculative while-while traversal (Aila & Laine 2009): a lane that reaches a
+// leaf parks it and keeps descending until every lane of the wave holds a
+// leaf; then all lanes test their parked leaves together.  Same closest hit
+// (tie rule included) as a plain depth-first traversal.
 template <bool ANY, bool STATS, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
-                                         const TravStack &stk, uint32_t &bestSlot, float &bu, float &bv, float &bt,
-                                         unsigned long long &nodes, unsigned long long &tests) {
+                                         lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
-    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_u4, glb_u4>::type U4;
-    // reciprocal direction for the (conservative) node tests; exact zeros use
-    // +-1e30 so that 0 * inf never produces NaN (TriAccel uses the exact ray)
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
     const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
     const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
@@ -170,86 +147,51 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     bool found = false;
     uint32_t bestPrim = 0;
     bt = maxt;
-    uint32_t sp = 0, lo = 0;   // entries [0, lo) live in the spill area, [lo, sp) in the ring
-    auto push = [&](int ref, float t) {
-        if (sp - lo > stk.mask) {                    // ring full: spill its oldest entry
-            const uint32_t s = (lo & stk.mask) * BLOCK;
-            if (lo < stk.cap) {
-                stk.g[2 * lo] = stk.n[s];
-                stk.g[2 * lo + 1] = (int)stk.d[s];
-            }
-            ++lo;
-        }
-        const uint32_t s = (sp & stk.mask) * BLOCK;
-        stk.n[s] = ref;
-        stk.d[s] = dist_down16(t);
-        ++sp;
-    };
+    int sp = 0;
+    int node = 0, leaf = 0;
     auto pop = [&]() -> int {
         while (sp > 0) {
             --sp;
-            int ref;
-            uint16_t dd;
-            if (sp >= lo) {
-                const uint32_t s = (sp & stk.mask) * BLOCK;
-                ref = stk.n[s];
-                dd = stk.d[s];
-            } else {
-                lo = sp;
-                ref = stk.g[2 * sp];
-                dd = (uint16_t)stk.g[2 * sp + 1];
-            }
-            if (ANY || dist_up16(dd) <= bt) return ref;
+            if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
         }
         return DONE;
     };
-    int node = 0, leaf = 0;
     while (node != DONE) {
         // inner nodes
         while ((uint32_t)node < (uint32_t)DONE) {
             if (STATS) nodes++;
-            NodeT *nd = nodesArr + node;
-            const vf4 w0 = *reinterpret_cast<F4 *>(&nd->px);
-            const vu4 w1 = *reinterpret_cast<U4 *>(&nd->child_base);
-            const vu4 w2 = *reinterpret_cast<U4 *>(&nd->qloy);
-            const uint32_t meta = __float_as_uint(w0.w);
-            const float sx = __uint_as_float(((meta & 31u) + 111u) << 23);        // 2^(e - 16)
-            const float sy = __uint_as_float((((meta >> 5) & 31u) + 111u) << 23);
-            const float sz = __uint_as_float((((meta >> 10) & 31u) + 111u) << 23);
-            const uint32_t imask = (meta >> 15) & 15u, counts = meta >> 19;
-            // decode folded into the slab: t = q * (scale * inv) + (origin * inv - o * inv);
-            // scale is a power of two, so scale * inv is exact
-            const float ax = sx * ix, ay = sy * iy, az = sz * iz;
-            const float bx = __builtin_fmaf(w0.x, ix, -ox), by = __builtin_fmaf(w0.y, iy, -oy),
-                        bz = __builtin_fmaf(w0.z, iz, -oz);
-            uint32_t innerIdx = w1.x, triIdx = w1.y;
-            float dist[4];
-            int ref[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                // w1 = {child_base, tri_base, qlox, qhix}, w2 = {qloy, qhiy, qloz, qhiz}
-                const float t0x = __builtin_fmaf(qbyte(w1.z, c), ax, bx), t1x = __builtin_fmaf(qbyte(w1.w, c), ax, bx);
-                const float t0y = __builtin_fmaf(qbyte(w2.x, c), ay, by), t1y = __builtin_fmaf(qbyte(w2.y, c), ay, by);
-                const float t0z = __builtin_fmaf(qbyte(w2.z, c), az, bz), t1z = __builtin_fmaf(qbyte(w2.w, c), az, bz);
-                const float nn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
-                const float ff = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
-                const uint32_t cnt = (counts >> (3 * c)) & 7u;
-                const bool inner = (imask >> c) & 1u;
-                dist[c] = ((inner || cnt != 0) && nn <= ff) ? nn : INFINITY;
-                ref[c] = inner ? (int)innerIdx : leaf_ref(triIdx, cnt);
-                innerIdx += inner ? 1u : 0u;
-                triIdx += cnt;
+            NodeT *n = nodesArr + node;
+            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
+            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
+            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
+            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+            // slab tests; node boxes are conservatively inflated on the host
+            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
+            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
+            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
+            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
+            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
+            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
+            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
+            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
+            const bool h0 = n0 <= f0, h1 = n1 <= f1;
+            if (h0 && h1) {
+                int nearC = e.x, farC = e.y;
+                float farT = n1;
+                if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
+                stkN[sp * BLOCK] = farC;
+                stkD[sp * BLOCK] = dist_down16(farT);
+                ++sp;
+                node = nearC;
+            } else if (h0) {
+                node = e.x;
+            } else if (h1) {
+                node = e.y;
+            } else {
+                node = pop();
             }
-            // nearest first: sorting network on (distance, reference)
-#define MTSG_CSWAP(i, j) \
-    if (dist[j] < dist[i]) { const float td = dist[i]; dist[i] = dist[j]; dist[j] = td; \
-                             const int tr = ref[i]; ref[i] = ref[j]; ref[j] = tr; }
-            MTSG_CSWAP(0, 1) MTSG_CSWAP(2, 3) MTSG_CSWAP(0, 2) MTSG_CSWAP(1, 3) MTSG_CSWAP(1, 2)
-#undef MTSG_CSWAP
-            if (dist[3] < INFINITY) push(ref[3], dist[3]);
-            if (dist[2] < INFINITY) push(ref[2], dist[2]);
-            if (dist[1] < INFINITY) push(ref[1], dist[1]);
-            node = dist[0] < INFINITY ? ref[0] : pop();
             // park the first leaf reached and keep descending
             if (node < 0 && leaf == 0) {
                 leaf = node;
@@ -259,8 +201,8 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         }
         // leaves
         while (leaf < 0) {
-            const uint32_t lref = (uint32_t)(~leaf);
-            const uint32_t first = lref >> 4, count = lref & 15u;
+            const uint32_t ref = (uint32_t)(~leaf);
+            const uint32_t first = ref >> 4, count = ref & 15u;
             for (uint32_t i = first; i < first + count; ++i) {
                 if (STATS) tests++;
                 TriT *tr = trisArr + i;
@@ -301,6 +243,108 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     }
     return found;
 }
+#else
+template <bool ANY, bool STATS, typename NodeT, typename TriT>
+__device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
+                                         lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
+    // reciprocal direction for the (conservative) node tests; exact zeros use
+    // +-1e30 so that 0 * inf never produces NaN (TriAccel uses the exact ray)
+    const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
+    const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
+    const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
+    const float ox = o.x * ix, oy = o.y * iy, oz = o.z * iz;
+    bool found = false;
+    uint32_t bestPrim = 0;
+    bt = maxt;
+    int sp = 0;
+    int node = 0;
+    while (true) {
+        if (node >= 0) {
+            if (STATS) nodes++;
+            NodeT *n = nodesArr + node;
+            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
+            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
+            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
+            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+            // slab tests; node boxes are conservatively inflated on the host, so the
+            // fused (o*inv precomputed) form needs no bit-exactness
+            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
+            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
+            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
+            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
+            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
+            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
+            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
+            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
+            const bool h0 = n0 <= f0, h1 = n1 <= f1;
+            if (h0 && h1) {
+                int nearC = e.x, farC = e.y;
+                float farT = n1;
+                if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
+                stkN[sp * BLOCK] = farC;
+                stkD[sp * BLOCK] = dist_down16(farT);
+                ++sp;
+                node = nearC;
+                continue;
+            } else if (h0) {
+                node = e.x;
+                continue;
+            } else if (h1) {
+                node = e.y;
+                continue;
+            }
+        } else {
+            const uint32_t ref = (uint32_t)(~node);
+            const uint32_t first = ref >> 4, count = ref & 15u;
+            for (uint32_t i = first; i < first + count; ++i) {
+                if (STATS) tests++;
+                TriT *tr = trisArr + i;
+                const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
+                const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
+                const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
+                const uint32_t k = __float_as_uint(q0.x);
+                // TriAccel::rayIntersect (triaccel.h:92-160)
+                float o_u, o_v, o_k, d_u, d_v, d_k;
+                if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+                else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+                else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+                else continue;
+                const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
+                const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
+                const float c_nu = q2.x, c_nv = q2.y;
+                const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+                if (t < mint || t > bt) continue;
+                const float hu = o_u + t * d_u - a_u;
+                const float hv = o_v + t * d_v - a_v;
+                const float u = hv * b_nu + hu * b_nv;
+                const float v = hu * c_nu + hv * c_nv;
+                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                    if (ANY) return true;
+                    const uint32_t prim = __float_as_uint(q2.z);
+                    // ties (t == bt): the larger primitive index wins
+                    if (!found || t < bt || prim > bestPrim) {
+                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+                    }
+                }
+            }
+        }
+        // pop, skipping subtrees that start beyond the closest hit found so far
+        bool popped = false;
+        while (sp > 0) {
+            --sp;
+            if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) { node = stkN[sp * BLOCK]; popped = true; break; }
+        }
+        if (!popped) break;
+    }
+    return found;
+}
+
+#endif
 
 // AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
 __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, float &nearT, float &farT) {
@@ -573,7 +617,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     const uint32_t base2 = tabWords + 16 * 16;
     uint32_t sceneWords = 0;
     if (SCENE_LDS) {
-        const uint32_t nodeWords = L.num_nodes * 12, triWords = S.num_prims * 12;
+        const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
         const uint32_t *gn = reinterpret_cast<const uint32_t *>(S.nodes);
         const uint32_t *gt = reinterpret_cast<const uint32_t *>(S.tris);
         for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[base2 + i] = gn[i];
@@ -584,19 +628,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
     // base2 and the node array size are multiples of 4 words: 16-byte aligned (ds_read_b128)
     lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
-    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 12), 16);
+    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
     SobolCtx SC;
     SC.lds = (lds_u32 *)lds;
     SC.glob = (glb_u32 *)L.sobol_nib;
     SC.lds_dims = L.lds_dims;
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
-    TravStack stk;
-    stk.n = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
-    stk.d = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
-    stk.g = (glb_stk *)L.trav_spill + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * L.spill_cap * 2;
-    stk.mask = L.stack_depth - 1;
-    stk.cap = L.spill_cap;
+    lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
 
     unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
     unsigned long long cHits = 0, cNee = 0, cSobol = 0;
@@ -676,9 +716,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 #endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS)
-                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
                 else
-                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stk, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
             }
         }
         bool hit = false;
@@ -689,9 +729,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             float mint, maxt;
             if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
-                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
                 else
-                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stk, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
             }
         }
 
@@ -984,7 +1024,7 @@ __global__ void arith_probe(const float *a, const float *b, float *out, int n) {
 // host-side launchers (called by capi.cpp)
 // ---------------------------------------------------------------------------
 size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
-    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 12 + (size_t)L.scene.num_prims * 12) : 0;
+    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
     return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2) * 4;
 }
 

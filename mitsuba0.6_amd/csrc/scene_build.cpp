@@ -364,21 +364,15 @@ struct BBox {
 
 struct BuildPrim { BBox box; float c[3]; uint32_t id; };
 
-// binary node of the SAH build (collapsed into MtsgNode BVH4 nodes afterwards)
-struct Node2 {
-    BBox b0, b1;              // children's (inflated) boxes
-    int32_t c0, c1;           // >= 0: Node2 index, < 0: leaf ref (mtsg_leaf_ref)
-};
-
 const uint32_t kMaxDepth = 28;   // traversal stack (LDS) holds < 32 entries
 
 struct Builder {
     std::vector<BuildPrim> &prims;
-    std::vector<Node2> &nodes;
+    std::vector<MtsgNode> &nodes;
     std::vector<uint32_t> order;
     float absEps;
     uint32_t maxDepth = 0;
-    explicit Builder(std::vector<BuildPrim> &p, std::vector<Node2> &n) : prims(p), nodes(n) {}
+    explicit Builder(std::vector<BuildPrim> &p, std::vector<MtsgNode> &n) : prims(p), nodes(n) {}
 
     void inflate(BBox &b) const {
         for (int a = 0; a < 3; ++a) {
@@ -452,130 +446,17 @@ struct Builder {
                              [&](uint32_t x, uint32_t y) { return prims[x].c[axis] < prims[y].c[axis]; });
         }
         const uint32_t id = (uint32_t)nodes.size();
-        nodes.push_back(Node2());
+        nodes.push_back(MtsgNode());
         BBox b0 = bounds(first, mid - first), b1 = bounds(mid, first + count - mid);
         inflate(b0); inflate(b1);
         const int32_t c0 = build(first, mid - first, depth + 1);
         const int32_t c1 = build(mid, first + count - mid, depth + 1);
-        Node2 &n = nodes[id];
-        n.b0 = b0; n.b1 = b1; n.c0 = c0; n.c1 = c1;
+        MtsgNode &n = nodes[id];
+        n.c0lox = b0.lo[0]; n.c0hix = b0.hi[0]; n.c0loy = b0.lo[1]; n.c0hiy = b0.hi[1];
+        n.c1lox = b1.lo[0]; n.c1hix = b1.hi[0]; n.c1loy = b1.lo[1]; n.c1hiy = b1.hi[1];
+        n.c0loz = b0.lo[2]; n.c0hiz = b0.hi[2]; n.c1loz = b1.lo[2]; n.c1hiz = b1.hi[2];
+        n.c0 = c0; n.c1 = c1; n.pad0 = n.pad1 = 0;
         return (int32_t)id;
-    }
-};
-
-// ---- BVH2 -> BVH4 with 8-bit quantised child boxes ---------------------------
-// Each BVH4 node takes a BVH2 node's two children and repeatedly opens the
-// inner child of largest surface area until it has four (leaves stay leaves).
-// Breadth-first layout: a node's inner children get consecutive indices, its
-// leaf children's triangles consecutive TriAccel slots.  Child boxes are
-// quantised outward against the union's lower corner with a per-axis scale
-// 2^(e-16), e in [0, 31]; every decoded bound is checked in the device's own
-// arithmetic (fmaf(q, scale, origin)) to contain the inflated float box, so a
-// quantised node can only report more hits than the float box, never fewer.
-struct Collapse {
-    const std::vector<Node2> &n2;
-    const std::vector<uint32_t> &order;
-    std::vector<MtsgNode> &out;
-    std::vector<uint32_t> triOrder;
-    uint32_t depth = 0;
-    std::string err;
-
-    struct Kid { int32_t ref; BBox box; };
-
-    void kids_of(int32_t id, std::vector<Kid> &k) const {
-        k.clear();
-        k.push_back({n2[id].c0, n2[id].b0});
-        k.push_back({n2[id].c1, n2[id].b1});
-        while (k.size() < 4) {
-            int best = -1;
-            float ba = -1.0f;
-            for (int i = 0; i < (int)k.size(); ++i)
-                if (k[i].ref >= 0 && k[i].box.area() > ba) { ba = k[i].box.area(); best = i; }
-            if (best < 0) break;
-            const Node2 &c = n2[k[best].ref];
-            k[best] = {c.c0, c.b0};
-            k.insert(k.begin() + best + 1, Kid{c.c1, c.b1});
-        }
-    }
-
-    static int axis_exponent(float ext) {   // smallest e with ext <= 255 * 2^(e-16)
-        for (int e = 0; e < 32; ++e)
-            if (ext <= 255.0f * std::ldexp(1.0f, e - 16)) return e;
-        return -1;
-    }
-
-    bool quantise(const BBox &u, const std::vector<Kid> &k, MtsgNode &n, int ex[3]) {
-        for (int a = 0; a < 3; ++a) {
-            ex[a] = axis_exponent(u.hi[a] - u.lo[a]);
-            if (ex[a] < 0) { err = "scene extent exceeds the compressed BVH range (8.4e6 units per node axis)"; return false; }
-        }
-        uint32_t q[6] = {0, 0, 0, 0, 0, 0};
-        const float org[3] = {u.lo[0], u.lo[1], u.lo[2]};
-        for (int c = 0; c < 4; ++c) {
-            uint32_t lo[3] = {255, 255, 255}, hi[3] = {0, 0, 0};   // empty slot: lo > hi
-            if (c < (int)k.size()) {
-                for (int a = 0; a < 3; ++a) {
-                    const float sc = std::ldexp(1.0f, ex[a] - 16);
-                    long ql = (long)std::floor((double)(k[c].box.lo[a] - org[a]) / sc);
-                    long qh = (long)std::ceil((double)(k[c].box.hi[a] - org[a]) / sc);
-                    ql = std::max(0l, std::min(255l, ql));
-                    qh = std::max(0l, std::min(255l, qh));
-                    while (ql > 0 && std::fmaf((float)ql, sc, org[a]) > k[c].box.lo[a]) --ql;
-                    while (qh < 255 && std::fmaf((float)qh, sc, org[a]) < k[c].box.hi[a]) ++qh;
-                    if (std::fmaf((float)ql, sc, org[a]) > k[c].box.lo[a] ||
-                        std::fmaf((float)qh, sc, org[a]) < k[c].box.hi[a]) {
-                        err = "BVH quantisation cannot bound a child box";
-                        return false;
-                    }
-                    lo[a] = (uint32_t)ql; hi[a] = (uint32_t)qh;
-                }
-            }
-            for (int a = 0; a < 3; ++a) {
-                q[2 * a] |= lo[a] << (8 * c);
-                q[2 * a + 1] |= hi[a] << (8 * c);
-            }
-        }
-        n.px = org[0]; n.py = org[1]; n.pz = org[2];
-        n.qlox = q[0]; n.qhix = q[1]; n.qloy = q[2]; n.qhiy = q[3]; n.qloz = q[4]; n.qhiz = q[5];
-        return true;
-    }
-
-    bool run(int32_t root) {
-        struct Item { int32_t id; uint32_t idx, level; };
-        std::vector<Item> queue;
-        out.assign(1, MtsgNode());
-        queue.push_back({root, 0, 1});
-        std::vector<Kid> k;
-        for (size_t qi = 0; qi < queue.size(); ++qi) {
-            const Item it = queue[qi];
-            depth = std::max(depth, it.level);
-            kids_of(it.id, k);
-            BBox u; u.reset();
-            for (const Kid &c : k)
-                if (c.ref >= 0 || (((uint32_t)~c.ref) & 15u)) u.grow(c.box);
-            MtsgNode n;
-            std::memset(&n, 0, sizeof n);
-            int ex[3];
-            if (!quantise(u, k, n, ex)) return false;
-            uint32_t imask = 0, counts = 0;
-            n.child_base = (uint32_t)out.size();
-            n.tri_base = (uint32_t)triOrder.size();
-            for (int c = 0; c < (int)k.size(); ++c) {
-                if (k[c].ref >= 0) {
-                    imask |= 1u << c;
-                    queue.push_back({k[c].ref, (uint32_t)out.size(), it.level + 1});
-                    out.push_back(MtsgNode());
-                } else {
-                    const uint32_t ref = (uint32_t)~k[c].ref, first = ref >> 4, cnt = ref & 15u;
-                    if (cnt > MTSG_LEAF_MAX) { err = "BVH leaf too large"; return false; }
-                    counts |= cnt << (3 * c);
-                    for (uint32_t i = first; i < first + cnt; ++i) triOrder.push_back(order[i]);
-                }
-            }
-            n.meta = (uint32_t)ex[0] | ((uint32_t)ex[1] << 5) | ((uint32_t)ex[2] << 10) | (imask << 15) | (counts << 19);
-            out[it.idx] = n;
-        }
-        return true;
     }
 };
 
@@ -1164,61 +1045,29 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         S.aabb_min[a] = amin[a]; S.aabb_max[a] = amax[a];
     }
     if (S.env.emitter >= 0) envmap_bsphere(S, D->sensor);
-    // BVH: binned-SAH BVH2, collapsed to the quantised BVH4 of layout.h
-    std::vector<Node2> n2;
-    Builder B(bp, n2);
+    // BVH
+    Builder B(bp, S.nodes);
     B.order.resize(prims);
     for (uint32_t i = 0; i < prims; ++i) B.order[i] = i;
     float diag = 0;
     for (int a = 0; a < 3; ++a) diag += (amax[a] - amin[a]) * (amax[a] - amin[a]);
     B.absEps = 1e-7f * std::sqrt(diag) + 1e-30f;
-    n2.reserve(prims + 2);
+    S.nodes.reserve(prims + 2);
     const int32_t rootRef = B.build(0, prims, 0);   // the first inner node created is node 0
     if (rootRef < 0) {
-        // whole scene in one leaf: a root holding that leaf and an empty one
-        Node2 n;
-        n.b0 = B.bounds(0, prims);
-        B.inflate(n.b0);
-        n.b1 = n.b0;
-        n.c0 = rootRef; n.c1 = mtsg_leaf_ref(0, 0);
-        n2.push_back(n);
+        // whole scene in one leaf: a root node holding that leaf and an empty one
+        BBox b = B.bounds(0, prims);
+        B.inflate(b);
+        MtsgNode n;
+        n.c0lox = b.lo[0]; n.c0hix = b.hi[0]; n.c0loy = b.lo[1]; n.c0hiy = b.hi[1]; n.c0loz = b.lo[2]; n.c0hiz = b.hi[2];
+        n.c1lox = n.c1hix = n.c1loy = n.c1hiy = n.c1loz = n.c1hiz = 0;
+        n.c0 = rootRef; n.c1 = mtsg_leaf_ref(0, 0); n.pad0 = n.pad1 = 0;
+        S.nodes.push_back(n);
     }
-    Collapse Cl{n2, B.order, S.nodes};
-    if (!Cl.run(0)) { err = Cl.err; return MTSGPU_EINVAL; }
-    if (Cl.triOrder.size() != prims) { err = "BVH collapse lost primitives"; return MTSGPU_EINVAL; }
-    S.bvh_depth = Cl.depth;
-    {   // structural check of the BVH4 (child and triangle ranges; each triangle's box
-        // inside its decoded leaf box) before any device traversal sees it
-        std::vector<uint8_t> seen(prims, 0);
-        for (const MtsgNode &n : S.nodes) {
-            const uint32_t imask = (n.meta >> 15) & 15u, counts = n.meta >> 19;
-            const uint32_t inner = (uint32_t)__builtin_popcount(imask);
-            if (inner && (size_t)n.child_base + inner > S.nodes.size()) { err = "BVH4: child index out of range"; return MTSGPU_EINVAL; }
-            uint32_t t = n.tri_base;
-            for (int c = 0; c < 4; ++c) {
-                if ((imask >> c) & 1u) continue;
-                const uint32_t cnt = (counts >> (3 * c)) & 7u;
-                const float org[3] = {n.px, n.py, n.pz};
-                const uint32_t ql[3] = {n.qlox, n.qloy, n.qloz}, qh[3] = {n.qhix, n.qhiy, n.qhiz};
-                for (uint32_t i = t; i < t + cnt; ++i) {
-                    if (i >= prims || seen[i]) { err = "BVH4: triangle range out of range"; return MTSGPU_EINVAL; }
-                    seen[i] = 1;
-                    const BBox &pb = bp[Cl.triOrder[i]].box;
-                    for (int a = 0; a < 3; ++a) {
-                        const float sc = std::ldexp(1.0f, (int)((n.meta >> (5 * a)) & 31u) - 16);
-                        const float lo = std::fmaf((float)((ql[a] >> (8 * c)) & 0xffu), sc, org[a]);
-                        const float hi = std::fmaf((float)((qh[a] >> (8 * c)) & 0xffu), sc, org[a]);
-                        if (lo > pb.lo[a] || hi < pb.hi[a]) { err = "BVH4: leaf box does not bound its triangle"; return MTSGPU_EINVAL; }
-                    }
-                }
-                t += cnt;
-            }
-        }
-        for (uint32_t i = 0; i < prims; ++i)
-            if (!seen[i]) { err = "BVH4: triangle not referenced"; return MTSGPU_EINVAL; }
-    }
-    // triangles in BVH4 leaf order
+    S.bvh_depth = B.maxDepth;
+    if (B.maxDepth + 1 >= 32) { err = "BVH too deep for the traversal stack"; return MTSGPU_EINVAL; }
+    // triangles in leaf order
     S.tris.resize(prims);
-    for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[Cl.triOrder[i]];
+    for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];
     return MTSGPU_OK;
 }

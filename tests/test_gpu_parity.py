@@ -161,15 +161,3 @@ def test_c5_textured_roughplastic_bitexact(gpu_ctx, oracle):
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
     film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
     _compare(film_g, smp_g, film_o, smp_o)
-
-
-def test_traversal_stack_spill_bitexact(gpu_ctx, oracle, monkeypatch):
-    """A 4-entry LDS ring forces the BVH4 traversal stack to spill to global
-    memory on most paths through the 69k-triangle object: same hits, same film."""
-    sc, it = _c3_small()
-    gpu_ctx.upload(sc)
-    monkeypatch.setenv('MTSGPU_STACK_RING', '4')
-    film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
-    monkeypatch.delenv('MTSGPU_STACK_RING')
-    film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
-    _compare(film_g, smp_g, film_o, smp_o)
