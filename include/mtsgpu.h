@@ -239,6 +239,16 @@ int mtsgpu_develop_device(mtsgpu_ctx *ctx, const mtsgpu_develop_params *params, 
                           void *out_device, void *stream);
 /* Same from and to host memory (stages both through the context's buffers). */
 int mtsgpu_develop(mtsgpu_ctx *ctx, const mtsgpu_develop_params *params, const float *film, void *out);
+/* Batch ray queries on the uploaded scene, one GPU lane per ray:
+ * Scene::rayIntersect (closest hit, shadow = 0) or the occlusion test
+ * (shadow = 1) of ShapeKDTree::rayIntersect (src/librender/skdtree.cpp:
+ * 112-142, 207-226), including the scene-bounds clip and the adaptive ray
+ * epsilon.  rays: n x 8 floats {o.xyz, mint, d.xyz, maxt}; hits: n x 4
+ * floats {t, u, v, prim} where prim is the global triangle index (mesh order,
+ * then triangle order) as uint32 bits, 0xffffffff and t = inf on a miss;
+ * shadow queries write t = 1 (occluded) or 0.  Host buffers; the kernel's
+ * device time goes to *kernel_ms if non-NULL. */
+int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow, float *hits, double *kernel_ms);
 /* Diagnostics (tests): device arithmetic probe -- for each i, out[8i..8i+7] =
  * {a/b, sqrt|a|, sin a, cos a, acos(clamp a), atan2(a,b), exp(-|a|), a*b+a}
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */

@@ -24,6 +24,8 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
+hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32_t n, float *out, bool shadow,
+                             uint32_t stackDepth, int numCUs, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
 hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
                                hipStream_t s);
@@ -65,6 +67,7 @@ struct mtsgpu_ctx {
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights;
     DevBuf rtrans, texcoords;
+    DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
 };
@@ -453,13 +456,39 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights,
-                      &ctx->rtrans, &ctx->texcoords,
+                      &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out};
     for (DevBuf *b : bufs) b->release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow, float *hits, double *kernel_ms) {
+    if (!ctx) return MTSGPU_EINVAL;
+    if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "trace_rays before upload_scene");
+    if (!rays || !hits) return fail(ctx, MTSGPU_EINVAL, "trace_rays: NULL buffer");
+    if (n == 0) return MTSGPU_OK;
+    (void)hipSetDevice(ctx->device);
+    hipError_t e;
+    if ((e = ctx->qrays.ensure((size_t)n * 32)) != hipSuccess || (e = ctx->qhits.ensure((size_t)n * 16)) != hipSuccess)
+        return hip_fail(ctx, e, "trace buffers");
+    hipStream_t s = ctx->stream;
+    if ((e = hipMemcpyAsync(ctx->qrays.p, rays, (size_t)n * 32, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipEventRecord(ctx->ev0, s)) != hipSuccess ||
+        (e = mtsg_launch_trace(ctx->dscene, (const float *)ctx->qrays.p, n, (float *)ctx->qhits.p, shadow != 0,
+                               ctx->host.bvh_depth + 2, ctx->num_cus, s)) != hipSuccess ||
+        (e = hipEventRecord(ctx->ev1, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(hits, ctx->qhits.p, (size_t)n * 16, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(ctx, e, "trace_rays");
+    if (kernel_ms) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+        *kernel_ms = ms;
+    }
+    return MTSGPU_OK;
 }
 
 // diagnostics: device arithmetic probe (tests/test_gpu_arith.py)

@@ -20,6 +20,7 @@
 //    dependent ones) and the lane-strided traversal stacks.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "dbsdf.h"
@@ -973,6 +974,36 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     if (cErr) atomicAdd(L.counters + 6, cErr);
 }
 
+// Scene::rayIntersect / Scene::isOccluded on a batch of rays (one ray per lane):
+// rays[2i] = {o, mint}, rays[2i+1] = {d, maxt}; out[i] = {t, u, v, prim bits}
+// (prim 0xffffffff and t = inf: no hit; the shadow query writes t = 1 / 0)
+template <bool ANY, int WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(MtsgDeviceScene S, const float4 *__restrict__ rays,
+                                                              uint32_t n, float4 *__restrict__ out,
+                                                              uint32_t stackDepth) {
+    extern __shared__ uint32_t lds[];
+    lds_stk_n *stkN = (lds_stk_n *)lds + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + stackDepth * BLOCK) + threadIdx.x;
+    unsigned long long cn = 0, ct = 0;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
+        const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
+        float4 r = make_float4(INFINITY, 0.0f, 0.0f, __uint_as_float(0xffffffffu));
+        float mint, maxt;
+        if (ray_interval(S, o, d, a.w, b.w, ANY, mint, maxt)) {
+            uint32_t slot = 0;
+            float u = 0, v = 0, t = 0;
+            const bool hit = traverse<ANY, false>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
+                                                  slot, u, v, t, cn, ct);
+            if (ANY) r.x = hit ? 1.0f : 0.0f;
+            else if (hit) r = make_float4(t, u, v, __uint_as_float(S.tris[slot].prim));
+        } else if (ANY) {
+            r.x = 0.0f;
+        }
+        out[i] = r;
+    }
+}
+
 // per-pixel ordered sum of the own-pixel splats: film_own[p] (+)= c[0] + c[1] + ...
 // in sample order -- the reference's `*dest++ += weight * value[k]` sequence
 __global__ void film_reduce(MtsgLaunch L) {
@@ -1071,6 +1102,23 @@ hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStr
     const int threads = 256;
     const int blocks = (int)((n + threads - 1) / threads);
     if (blocks > 0) hipLaunchKernelGGL(film_finalize, dim3(blocks), dim3(threads), 0, stream, own, spill, n);
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32_t n, float *out, bool shadow,
+                             uint32_t stackDepth, int numCUs, hipStream_t stream) {
+    const size_t lds = (size_t)stackDepth * 3 * BLOCK / 2 * 4 + 16;
+    int bpc = 1;
+    if (shadow) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<true, 8>, BLOCK, lds);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<false, 8>, BLOCK, lds);
+    const uint32_t want = (n + BLOCK - 1) / BLOCK;
+    const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(want, (uint32_t)(std::max(bpc, 1) * numCUs)));
+    if (shadow)
+        hipLaunchKernelGGL((trace_kernel<true, 8>), dim3(grid), dim3(BLOCK), lds, stream, S, (const float4 *)rays, n,
+                           (float4 *)out, stackDepth);
+    else
+        hipLaunchKernelGGL((trace_kernel<false, 8>), dim3(grid), dim3(BLOCK), lds, stream, S, (const float4 *)rays, n,
+                           (float4 *)out, stackDepth);
     return hipGetLastError();
 }
 

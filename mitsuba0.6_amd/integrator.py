@@ -27,7 +27,8 @@ class MtsgpuError(RuntimeError):
 
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
-           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene']
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
+           'mtsgpu_trace_rays']
 
 _lib = None
 
@@ -52,6 +53,7 @@ def load_library(path=None):
     L.mtsgpu_destroy.argtypes = [C.c_void_p]
     L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
+    L.mtsgpu_trace_rays.argtypes = [C.c_void_p, P(C.c_float), C.c_uint32, C.c_int, P(C.c_float), P(C.c_double)]
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
     L.mtsgpu_develop_device.argtypes = [C.c_void_p, P(abi.DevelopParams), C.c_void_p, C.c_void_p, C.c_void_p]
@@ -143,6 +145,20 @@ class Context:
         p = hdrfilm.develop_params(film_shape, border)
         self._check(self.L.mtsgpu_develop_device(self.h, C.byref(p), C.c_void_p(film_ptr), C.c_void_p(out_ptr),
                                                   C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def trace_rays(self, o, d, mint=1e-4, maxt=np.inf, shadow=False):
+        """Scene::rayIntersect (shadow=False) / occlusion (shadow=True) for a batch of
+        rays: o, d (n, 3); mint, maxt scalars or (n,).  Returns (hits (n, 4) float32
+        {t, u, v, prim bits}, kernel ms)."""
+        o = np.asarray(o, np.float32).reshape(-1, 3)
+        d = np.asarray(d, np.float32).reshape(-1, 3)
+        n = o.shape[0]
+        rays = np.empty((n, 8), np.float32)
+        rays[:, 0:3], rays[:, 3], rays[:, 4:7], rays[:, 7] = o, mint, d, maxt
+        hits = np.empty((n, 4), np.float32)
+        ms = C.c_double()
+        self._check(self.L.mtsgpu_trace_rays(self.h, abi.fptr(rays), n, int(shadow), abi.fptr(hits), C.byref(ms)))
+        return hits, ms.value
 
     def debug_arith(self, a, b):
         a = np.ascontiguousarray(a, np.float32)

@@ -49,6 +49,8 @@ def lib():
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 6 + [C.c_int]
         L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 4 + [C.c_int]
         L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
+        L.oracle_trace_rays.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.c_uint32, C.c_int,
+                                        C.POINTER(C.c_float)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]
         rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
@@ -56,6 +58,22 @@ def lib():
             raise RuntimeError('oracle_sobol_init failed: %d' % rc)
         _lib = L
     return _lib
+
+
+def trace_rays(scene, o, d, mint=1e-4, maxt=np.inf, shadow=False):
+    """The oracle's Scene::rayIntersect / occlusion for a batch (same layout as Context.trace_rays)."""
+    o = np.asarray(o, np.float32).reshape(-1, 3)
+    d = np.asarray(d, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    rays = np.empty((n, 8), np.float32)
+    rays[:, 0:3], rays[:, 3], rays[:, 4:7], rays[:, 7] = o, mint, d, maxt
+    hits = np.empty((n, 4), np.float32)
+    desc = scene.desc()
+    fp = C.POINTER(C.c_float)
+    rc = lib().oracle_trace_rays(C.byref(desc), rays.ctypes.data_as(fp), n, int(shadow), hits.ctypes.data_as(fp))
+    if rc != 0:
+        raise RuntimeError('oracle_trace_rays failed: %d' % rc)
+    return hits
 
 
 def configure_rc(scene):

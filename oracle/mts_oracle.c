@@ -2180,6 +2180,7 @@ typedef struct {
     Frame sh;
     int mesh; uint32_t tri;
     float u, v;   /* its.uv */
+    float bu, bv; /* TriAccel barycentrics of the hit */
 } Its;
 
 /* ShapeKDTree::rayIntersect(ray, its) (skdtree.cpp:112-142) + fillIntersectionRecord<true>
@@ -2201,6 +2202,7 @@ static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *
     const Mesh *m = &S->meshes[S->taMesh[prim]];
     uint32_t tri = S->taTri[prim];
     its->valid = 1; its->t = t; its->mesh = (int)S->taMesh[prim]; its->tri = tri;
+    its->bu = u; its->bv = v;
     const float bx = 1 - u - v, by = u, bz = v;
     const uint32_t i0 = m->idx[3 * tri], i1 = m->idx[3 * tri + 1], i2 = m->idx[3 * tri + 2];
     V3 p0 = m->pos[i0], p1 = m->pos[i1], p2 = m->pos[i2];
@@ -2802,6 +2804,41 @@ int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *t
 
 /* ShapeKDTree::rayIntersect(ray, its) probe (tests/test_oracle_kat.py, after
  * src/tests/test_dgeom.cpp:35-176): out16 = {valid, t, p[3], geoN[3], shN[3], shS[3], mesh, tri} */
+/* the batch query of mtsgpu_trace_rays: rays n x {o, mint, d, maxt} -> n x {t, u, v, prim bits} */
+int oracle_trace_rays(const mtsgpu_scene_desc *scene, const float *rays, uint32_t n, int shadow, float *hits) {
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    if (rc) { scene_free(&S); return rc; }
+    #pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        const float *r = rays + 8 * i;
+        Ray ray;
+        memset(&ray, 0, sizeof ray);
+        ray.o = v3(r[0], r[1], r[2]);
+        ray_set_dir(&ray, v3(r[4], r[5], r[6]));
+        ray.mint = r[3]; ray.maxt = r[7];
+        Counters C = {0, 0, 0, 0};
+        float *h = hits + 4 * i;
+        if (shadow) {
+            h[0] = scene_occluded(&S, &ray, &C) ? 1.0f : 0.0f; h[1] = h[2] = 0.0f; h[3] = 0.0f;
+            uint32_t none = 0xffffffffu; memcpy(&h[3], &none, 4);
+            continue;
+        }
+        Its its;
+        scene_intersect(&S, &ray, &its, &C);
+        uint32_t prim = 0xffffffffu;
+        if (its.valid) {
+            prim = S.meshes[its.mesh].primOffset + its.tri;
+            h[0] = its.t; h[1] = its.bu; h[2] = its.bv;
+        } else {
+            h[0] = INFINITY; h[1] = h[2] = 0.0f;
+        }
+        memcpy(&h[3], &prim, 4);
+    }
+    scene_free(&S);
+    return MTSGPU_OK;
+}
+
 int oracle_intersect(const mtsgpu_scene_desc *scene, const float *o, const float *d, float *out16) {
     Scene S;
     int rc = scene_configure(scene, &S);

@@ -161,3 +161,27 @@ def test_c5_textured_roughplastic_bitexact(gpu_ctx, oracle):
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
     film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
     _compare(film_g, smp_g, film_o, smp_o)
+
+
+def _random_rays(sc, n, seed):
+    rng = np.random.default_rng(seed)
+    lo = np.min([m.positions.min(0) for m in sc.meshes], 0)
+    hi = np.max([m.positions.max(0) for m in sc.meshes], 0)
+    o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d
+
+
+@pytest.mark.parametrize('cfg', ['C3', 'C4'])
+def test_trace_rays_bitexact(gpu_ctx, oracle, cfg):
+    """mtsgpu_trace_rays (Scene::rayIntersect / occlusion in batch) == the oracle's
+    kd-tree-semantics query: same t, barycentrics and primitive, bit for bit."""
+    sc, _ = scenes.build(cfg)
+    gpu_ctx.upload(sc)
+    o, d = _random_rays(sc, 100000, 5)
+    for shadow, maxt in ((False, np.inf), (True, 3.0)):
+        hg, _ = gpu_ctx.trace_rays(o, d, maxt=maxt, shadow=shadow)
+        ho = oracle.trace_rays(sc, o, d, maxt=maxt, shadow=shadow)
+        assert np.array_equal(_bits(hg), _bits(ho)), (cfg, shadow, np.argwhere(_bits(hg) != _bits(ho))[:5])
+        assert 0.05 < np.mean(hg[:, 3].view(np.uint32) != 0xffffffff if not shadow else hg[:, 0] > 0) < 1.0
