@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 2
+#define MTSGPU_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -53,7 +53,11 @@ enum { /* BSDF plugins on the path (src/bsdfs) */
     MTSGPU_BSDF_DIFFUSE = 0,         /* diffuse.cpp         */
     MTSGPU_BSDF_ROUGHCONDUCTOR = 1,  /* roughconductor.cpp  */
     MTSGPU_BSDF_ROUGHDIELECTRIC = 2, /* roughdielectric.cpp */
-    MTSGPU_BSDF_ROUGHPLASTIC = 3     /* roughplastic.cpp + rtrans.h */
+    MTSGPU_BSDF_ROUGHPLASTIC = 3,    /* roughplastic.cpp + rtrans.h */
+    MTSGPU_BSDF_CONDUCTOR = 4,       /* conductor.cpp  (smooth, delta reflection)        */
+    MTSGPU_BSDF_DIELECTRIC = 5,      /* dielectric.cpp (smooth, delta refl. + transm.)   */
+    MTSGPU_BSDF_PLASTIC = 6,         /* plastic.cpp    (delta coating + diffuse base)    */
+    MTSGPU_BSDF_TWOSIDED = 7         /* twosided.cpp   (wraps nested[0], nested[1])      */
 };
 
 enum { /* MicrofacetDistribution::EType (src/bsdfs/microfacet.h:48-57) */
@@ -81,13 +85,13 @@ typedef struct {
     int32_t ensure_energy_conservation; /* 'ensureEnergyConservation' (default 1)   */
     float alpha_u, alpha_v;         /* 'alpha' / 'alphaU','alphaV' as given        */
     float reflectance[3];           /* diffuse 'reflectance'                       */
-    float specular_reflectance[3];  /* rough*: 'specularReflectance' (default 1)   */
+    float specular_reflectance[3];  /* all but diffuse: 'specularReflectance' (1)  */
     float specular_transmittance[3];/* roughdielectric (default 1)                 */
-    float eta[3], k[3];             /* roughconductor: RGB eta/k, before /extEta   */
+    float eta[3], k[3];             /* (rough)conductor: RGB eta/k, before /extEta */
     float ext_eta;                  /* roughconductor 'extEta' (air = 1.000277)    */
-    float int_ior, ext_ior;         /* roughdielectric (bk7 = 1.5046, air);        */
-                                    /* roughplastic (polypropylene = 1.49, air)    */
-    /* roughplastic (roughplastic.cpp:197-300) */
+    float int_ior, ext_ior;         /* (rough)dielectric (bk7 = 1.5046, air);      */
+                                    /* (rough)plastic (polypropylene = 1.49, air)  */
+    /* (rough)plastic (roughplastic.cpp:197-300, plastic.cpp:144-216) */
     float diffuse_reflectance[3];   /* 'diffuseReflectance' (default 0.5)          */
     int32_t nonlinear;              /* 'nonlinear' (default 0)                     */
     const void *rtrans_data;        /* the bytes of data/microfacet/<distr>.dat    */
@@ -95,6 +99,11 @@ typedef struct {
     /* textured parameters; type NONE -> the constant field above is used */
     mtsgpu_texture_desc reflectance_tex;   /* diffuse 'reflectance' / roughplastic 'diffuseReflectance' */
     mtsgpu_texture_desc alpha_tex;         /* rough*: isotropic 'alpha' (value = texture average)       */
+    /* twosided (twosided.cpp:63-110): indices into the scene's bsdfs of the
+       front-side BSDF and of the back-side one (-1: the front one is reused);
+       nested BSDFs must be one-sided reflectors (diffuse, roughconductor,
+       roughplastic, conductor, plastic): TwoSidedBRDF::configure raises otherwise */
+    int32_t nested[2];
 } mtsgpu_bsdf_desc;
 
 enum { MTSGPU_EMITTER_AREA = 0, MTSGPU_EMITTER_ENVMAP = 1 };

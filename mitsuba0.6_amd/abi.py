@@ -12,8 +12,9 @@ STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTA
                 EDIM: 'EDIM', ECANCEL: 'ECANCEL', ENODEV: 'ENODEV'}
 
 BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC, BSDF_ROUGHPLASTIC = 0, 1, 2, 3
+BSDF_CONDUCTOR, BSDF_DIELECTRIC, BSDF_PLASTIC, BSDF_TWOSIDED = 4, 5, 6, 7
 TEX_NONE, TEX_CHECKERBOARD = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP = 0, 1
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
@@ -40,7 +41,8 @@ class BsdfDesc(C.Structure):
                 ('int_ior', C.c_float), ('ext_ior', C.c_float),
                 ('diffuse_reflectance', _f3), ('nonlinear', C.c_int32),
                 ('rtrans_data', C.c_void_p), ('rtrans_bytes', C.c_uint64),
-                ('reflectance_tex', TextureDesc), ('alpha_tex', TextureDesc)]
+                ('reflectance_tex', TextureDesc), ('alpha_tex', TextureDesc),
+                ('nested', C.c_int32 * 2)]
 
 
 class EmitterDesc(C.Structure):

@@ -5,6 +5,8 @@
 //   src/bsdfs/diffuse.cpp:110-150        src/bsdfs/microfacet.h:67-670
 //   src/bsdfs/roughconductor.cpp:257-410 src/bsdfs/roughdielectric.cpp:270-615
 //   src/bsdfs/roughplastic.cpp:300-470   src/bsdfs/rtrans.h:179-260
+//   src/bsdfs/conductor.cpp:216-283      src/bsdfs/dielectric.cpp:218-333
+//   src/bsdfs/plastic.cpp:240-440        src/bsdfs/twosided.cpp:105-175
 //   src/libcore/spline.cpp:23-60,236-304 src/textures/checkerboard.cpp
 //   src/librender/texture.cpp:112-121
 //   src/libcore/util.cpp:651-771 (Fresnel, reflect, refract)
@@ -20,7 +22,8 @@ enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
 #else
 #define BSDF_CALL __device__ __noinline__
 #endif
-enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2, BSDF_ROUGHPLASTIC = 3 };
+enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2, BSDF_ROUGHPLASTIC = 3,
+       BSDF_CONDUCTOR = 4, BSDF_DIELECTRIC = 5, BSDF_PLASTIC = 6, BSDF_TWOSIDED = 7 };   // = MTSGPU_BSDF_*
 
 __device__ __forceinline__ float tan_theta(f3 v) {           // frame.h:117-122
     float temp = 1 - v.z * v.z;
@@ -529,6 +532,91 @@ __device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float 
     return result;
 }
 
+// ---- smooth (delta) BSDFs: conductor, dielectric, plastic ------------------
+// eval()/pdf() are only queried by the path's emitter sampling, i.e. with
+// measure = ESolidAngle, where the delta lobes contribute nothing
+// (conductor.cpp:216-245, dielectric.cpp:228-275): only plastic's diffuse base
+// remains (plastic.cpp:245-310).
+__device__ __forceinline__ float fresnel_dielectric_ext2(float cosThetaI, float eta) {   // util.cpp:680-683
+    float ct;
+    return fresnel_dielectric_ext(cosThetaI, ct, eta);
+}
+__device__ __forceinline__ f3 sp_diffuse(GBsdf &b, float u, float v) {   // diff /= ... (plastic.cpp:276-280)
+    f3 diff = bsdf_refl<true>(b, u, v);
+    if (b.nonlinear) diff = divv(diff, sub(mk(1.0f, 1.0f, 1.0f), mul(diff, b.fdr_int)));
+    else diff = divs(diff, 1 - b.fdr_int);
+    return diff;
+}
+__device__ __forceinline__ float sp_prob_specular(GBsdf &b, float Fi) {   // plastic.cpp:296-299
+    return (Fi * b.spec_weight) / (Fi * b.spec_weight + (1 - Fi) * (1 - b.spec_weight));
+}
+__device__ __noinline__ f3 sm_eval(GBsdf &b, f3 wi, f3 wo, float u, float v) {
+    if (b.type != BSDF_PLASTIC) return mk(0, 0, 0);
+    if (wo.z <= 0 || wi.z <= 0) return mk(0, 0, 0);
+    const float Fi = fresnel_dielectric_ext2(wi.z, b.eta);
+    const float Fo = fresnel_dielectric_ext2(wo.z, b.eta);
+    return mul(sp_diffuse(b, u, v), D_INV_PI * wo.z * b.inv_eta2 * (1 - Fi) * (1 - Fo));
+}
+__device__ __noinline__ float sm_pdf(GBsdf &b, f3 wi, f3 wo) {
+    if (b.type != BSDF_PLASTIC) return 0.0f;
+    if (wo.z <= 0 || wi.z <= 0) return 0.0f;
+    const float probSpecular = sp_prob_specular(b, fresnel_dielectric_ext2(wi.z, b.eta));
+    return (D_INV_PI * wo.z) * (1 - probSpecular);
+}
+// sample(bRec, pdf, sample) (conductor.cpp:269-283, dielectric.cpp:277-333, plastic.cpp:356-420)
+__device__ __noinline__ BSample sm_sample(GBsdf &b, f3 wi, float sx, float sy, float u, float v) {
+    BSample r;
+    r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
+    if (b.type == BSDF_CONDUCTOR) {
+        if (wi.z <= 0) return r;
+        r.sampledType = MTSG_F_DELTA_REFL;
+        r.wo = mk(-wi.x, -wi.y, wi.z);
+        r.eta = 1.0f;
+        r.pdf = 1;
+        r.weight = mulv(ld3(b.spec_r), fresnel_conductor_exact(wi.z, ld3(b.eta3), ld3(b.k3)));
+        return r;
+    }
+    if (b.type == BSDF_DIELECTRIC) {
+        float cosThetaT;
+        const float F = fresnel_dielectric_ext(wi.z, cosThetaT, b.eta);
+        if (sx <= F) {
+            r.sampledType = MTSG_F_DELTA_REFL;
+            r.wo = mk(-wi.x, -wi.y, wi.z);
+            r.eta = 1.0f;
+            r.pdf = F;
+            r.weight = ld3(b.spec_r);
+        } else {
+            const float scale = -(cosThetaT < 0 ? b.inv_eta : b.eta);
+            r.sampledType = MTSG_F_DELTA_TRANS;
+            r.wo = mk(scale * wi.x, scale * wi.y, cosThetaT);
+            r.eta = cosThetaT < 0 ? b.eta : b.inv_eta;
+            r.pdf = 1 - F;
+            const float factor = cosThetaT < 0 ? b.inv_eta : b.eta;
+            r.weight = mul(ld3(b.spec_t), factor * factor);
+        }
+        return r;
+    }
+    // plastic
+    if (wi.z <= 0) return r;
+    const float Fi = fresnel_dielectric_ext2(wi.z, b.eta);
+    r.eta = 1.0f;
+    const float probSpecular = sp_prob_specular(b, Fi);
+    if (sx < probSpecular) {
+        r.sampledType = MTSG_F_DELTA_REFL;
+        r.wo = mk(-wi.x, -wi.y, wi.z);
+        r.pdf = probSpecular;
+        r.weight = divs(mul(ld3(b.spec_r), Fi), probSpecular);
+    } else {
+        r.sampledType = MTSG_F_DIFF_REFL;
+        r.wo = square_to_cosine_hemisphere((sx - probSpecular) / (1 - probSpecular), sy);
+        const float Fo = fresnel_dielectric_ext2(r.wo.z, b.eta);
+        const f3 diff = sp_diffuse(b, u, v);
+        r.pdf = (1 - probSpecular) * (D_INV_PI * r.wo.z);
+        r.weight = mul(diff, b.inv_eta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+    }
+    return r;
+}
+
 // ---- BSDF::eval / pdf / sample --------------------------------------------
 template <bool EXT>
 BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
@@ -537,7 +625,10 @@ BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
         if (wi.z <= 0 || wo.z <= 0) return zero;
         return mul(bsdf_refl<EXT>(b, u, v), D_INV_PI * wo.z);
     }
-    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_eval(b, rt, wi, wo, u, v); }
+    if constexpr (EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval(b, rt, wi, wo, u, v);
+        if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
+    }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:257-292
         if (wi.z <= 0 || wo.z <= 0) return zero;
         f3 H = normalize(add(wo, wi));
@@ -582,7 +673,10 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) 
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
     }
-    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf(b, rt, wi, wo, u, v); }
+    if constexpr (EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf(b, rt, wi, wo, u, v);
+        if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
+    }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:294-319
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         f3 H = normalize(add(wo, wi));
@@ -660,7 +754,10 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         r.weight = bsdf_refl<EXT>(b, u, v);
         return r;
     }
-    if constexpr (EXT) { if (b.type == BSDF_ROUGHPLASTIC) return rp_sample(b, rt, wi, sx, sy, u, v); }
+    if constexpr (EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample(b, rt, wi, sx, sy, u, v);
+        if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
+    }
     if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:357-406
         if (wi.z < 0) return r;
         Distr d = bsdf_distr<EXT>(b, u, v);

@@ -70,6 +70,10 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
     int32_t rt_alpha_fixed;          // external table reduced to 1D (constant alpha)
     float rt_alpha_min, rt_alpha_max;
     MtsgTex refl_tex, alpha_tex;     // textured reflectance / alpha (type 0: constant)
+    // plastic (plastic.cpp:186-216): m_fdrInt, m_fdrExt (fresnelDiffuseReflectance)
+    float fdr_int, fdr_ext;
+    // twosided (twosided.cpp): record indices of the front / back nested BSDFs
+    int32_t nested[2];
 };
 
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };

@@ -892,9 +892,19 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                 f3 c = mk(0, 0, 0);
                                 if (!is_zero(value)) {
                                     const f3 wo = to_local(P.its.sh, dd);
-                                    const f3 bsdfVal = bsdf_eval<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, wo, P.its.u, P.its.v);
+                                    // twosided (twosided.cpp:105-131): the nested BSDF of the side wi is on
+                                    f3 qwi = P.its.wi, qwo = wo;
+                                    GBsdf *qb = &bsdf;
+                                    if constexpr (EXT) {
+                                        if (bsdf.type == BSDF_TWOSIDED) {
+                                            const bool flip = !(qwi.z > 0);
+                                            qb = &((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
+                                            if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
+                                        }
+                                    }
+                                    const f3 bsdfVal = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
                                     if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                        const float bsdfPdf = bsdf_pdf<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, wo, P.its.u, P.its.v);
+                                        const float bsdfPdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
                                         const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
                                         const float weight = pa / (pa + pb);
                                         c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
@@ -912,7 +922,18 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                         next2d(SC, L.resolution, smp, px, py, bx2, by2);
                         float u1d = 0.0f;
                         if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
-                        const BSample bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                        BSample bs;
+                        if (EXT && bsdf.type == BSDF_TWOSIDED) {
+                            // TwoSidedBRDF::sample(bRec, pdf, sample) (twosided.cpp:151-172)
+                            const bool flip = P.its.wi.z < 0;
+                            f3 qwi = P.its.wi;
+                            if (flip) qwi.z = -qwi.z;
+                            bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
+                                                  bx2, by2, u1d, P.its.u, P.its.v);
+                            if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
+                        } else {
+                            bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                        }
                         if (!is_zero(bs.weight) && !smp.err) {
                             P.scattered |= bs.sampledType != MTSG_F_NULL;
                             const f3 wo = to_world(P.its.sh, bs.wo);

@@ -277,9 +277,137 @@ int configure_roughplastic(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::vector<f
     return MTSGPU_OK;
 }
 
+// fresnelDielectricExt(cosThetaI, eta) (util.cpp:651-677)
+float fresnel_dielectric_ext_h(float cosThetaI_, float eta) {
+    if (eta == 1) return 0.0f;
+    const float scale = (cosThetaI_ > 0) ? 1 / eta : eta,
+                cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) return 1.0f;
+    const float cosThetaI = std::fabs(cosThetaI_), cosThetaT = std::sqrt(cosThetaTSqr);
+    const float Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    const float Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+// GaussLobattoIntegrator(1024, 0, 1e-5f) with the convergence estimate
+// (quad.cpp:287-409) over fresnelDiffuseIntegrand (util.cpp:808-811): the
+// accurate branch of fresnelDiffuseReflectance(eta, false) (util.cpp:814-860).
+// The six sub-steps are summed (and their evaluations counted) left to right.
+struct FdrQuad {
+    float eta;
+    size_t evals = 0;
+    static constexpr size_t kMaxEvals = 1024;
+    static constexpr float kRelError = 1e-5f;
+    const float alpha = (float)std::sqrt(2.0 / 3.0), beta = (float)(1.0 / std::sqrt(5.0));
+    const float x1 = (float)0.94288241569547971906, x2 = (float)0.64185334234578130578,
+                x3 = (float)0.23638319966214988028;
+    float f(float xi) const { return fresnel_dielectric_ext_h(std::sqrt(xi), eta); }
+    float abs_tolerance(float a, float b) {
+        const float m = (a + b) / 2, h = (b - a) / 2;
+        const float y1 = f(a), y3 = f(m - alpha * h), y5 = f(m - beta * h), y7 = f(m), y9 = f(m + beta * h),
+                    y11 = f(m + alpha * h), y13 = f(b);
+        const float acc = h * ((float)0.0158271919734801831 * (y1 + y13)
+                             + (float)0.0942738402188500455 * (f(m - x1 * h) + f(m + x1 * h))
+                             + (float)0.1550719873365853963 * (y3 + y11)
+                             + (float)0.1888215739601824544 * (f(m - x2 * h) + f(m + x2 * h))
+                             + (float)0.1997734052268585268 * (y5 + y9)
+                             + (float)0.2249264653333395270 * (f(m - x3 * h) + f(m + x3 * h))
+                             + (float)0.2426110719014077338 * y7);
+        evals += 13;
+        float r = 1.0f;
+        const float integral2 = (h / 6) * (y1 + y13 + 5 * (y5 + y9));
+        const float integral1 = (h / 1470) * (77 * (y1 + y13) + 432 * (y3 + y11) + 625 * (y5 + y9) + 672 * y7);
+        if (std::fabs(integral2 - acc) != 0.0f) r = std::fabs(integral1 - acc) / std::fabs(integral2 - acc);
+        if (r == 0.0f || r > 1.0f) r = 1.0f;
+        float result = INFINITY;
+        if (acc != 0) result = acc * fmax_std(kRelError, FLT_EPSILON) / (r * FLT_EPSILON);
+        return result;
+    }
+    float step(float a, float b, float fa, float fb, float acc) {
+        const float h = (b - a) / 2, m = (a + b) / 2;
+        const float mll = m - alpha * h, ml = m - beta * h, mr = m + beta * h, mrr = m + alpha * h;
+        const float fmll = f(mll), fml = f(ml), fm = f(m), fmr = f(mr), fmrr = f(mrr);
+        const float integral2 = (h / 6) * (fa + fb + 5 * (fml + fmr));
+        const float integral1 = (h / 1470) * (77 * (fa + fb) + 432 * (fmll + fmrr) + 625 * (fml + fmr) + 672 * fm);
+        evals += 5;
+        if (evals >= kMaxEvals) return integral1;
+        const float dist = acc + (integral1 - integral2);
+        if (dist == acc || mll <= a || b <= mrr) return integral1;
+        float r = step(a, mll, fa, fmll, acc);
+        r = r + step(mll, ml, fmll, fml, acc);
+        r = r + step(ml, m, fml, fm, acc);
+        r = r + step(m, mr, fm, fmr, acc);
+        r = r + step(mr, mrr, fmr, fmrr, acc);
+        r = r + step(mrr, b, fmrr, fb, acc);
+        return r;
+    }
+    float integrate() {   // over [0, 1]
+        const float tol = abs_tolerance(0.0f, 1.0f);
+        evals += 2;
+        return step(0.0f, 1.0f, f(0.0f), f(1.0f), tol);
+    }
+};
+
+float fresnel_diffuse_reflectance(float eta) {
+    FdrQuad q;
+    q.eta = eta;
+    return q.integrate();
+}
+
+// SmoothConductor / SmoothDielectric / SmoothPlastic ctor + configure
+// (conductor.cpp:164-212, dielectric.cpp:146-201, plastic.cpp:144-216)
+int configure_smooth(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::string &err) {
+    const float ss = energy_scale(d.specular_reflectance, d.ensure_energy_conservation);
+    for (int i = 0; i < 3; ++i) b.spec_r[i] = ss != 1.0f ? d.specular_reflectance[i] * ss : d.specular_reflectance[i];
+    if (d.type == MTSGPU_BSDF_CONDUCTOR) {
+        const float r = 1.0f / d.ext_eta;   // m_eta = eta / extEta (Spectrum / Float: reciprocal multiply)
+        for (int i = 0; i < 3; ++i) { b.eta3[i] = d.eta[i] * r; b.k3[i] = d.k[i] * r; }
+        b.flags = MTSG_F_DELTA_REFL | MTSG_F_FRONT;
+        return MTSGPU_OK;
+    }
+    if (d.int_ior < 0 || d.ext_ior < 0) {
+        err = "The interior and exterior indices of refraction must be positive!";
+        return MTSGPU_EINVAL;
+    }
+    b.eta = d.int_ior / d.ext_ior;
+    if (d.type == MTSGPU_BSDF_DIELECTRIC) {
+        b.inv_eta = 1 / b.eta;
+        const float st = energy_scale(d.specular_transmittance, d.ensure_energy_conservation);
+        for (int i = 0; i < 3; ++i)
+            b.spec_t[i] = st != 1.0f ? d.specular_transmittance[i] * st : d.specular_transmittance[i];
+        b.flags = MTSG_F_DELTA_REFL | MTSG_F_DELTA_TRANS | MTSG_F_FRONT | MTSG_F_BACK;
+        return MTSGPU_OK;
+    }
+    // plastic
+    b.nonlinear = d.nonlinear ? 1 : 0;
+    float mx[3];
+    tex_max(d.reflectance_tex, d.diffuse_reflectance, mx);
+    const float sd = energy_scale(mx, d.ensure_energy_conservation);
+    for (int i = 0; i < 3; ++i) b.refl[i] = sd != 1.0f ? d.diffuse_reflectance[i] * sd : d.diffuse_reflectance[i];
+    int rc;
+    if ((rc = set_tex(d.reflectance_tex, sd, b.refl_tex, err))) return rc;
+    b.fdr_int = fresnel_diffuse_reflectance(1 / b.eta);
+    b.fdr_ext = fresnel_diffuse_reflectance(b.eta);
+    float davg[3], savg[3];
+    tex_avg(d.reflectance_tex, d.diffuse_reflectance, davg);
+    for (int i = 0; i < 3; ++i) {
+        if (sd != 1.0f) davg[i] = davg[i] * sd;
+        savg[i] = b.spec_r[i];
+    }
+    const float dAvg = luminance(davg), sAvg = luminance(savg);
+    b.spec_weight = sAvg / (dAvg + sAvg);
+    b.inv_eta2 = 1 / (b.eta * b.eta);
+    b.flags = MTSG_F_DELTA_REFL | MTSG_F_DIFF_REFL | MTSG_F_FRONT;
+    return MTSGPU_OK;
+}
+
 int configure_bsdf(const mtsgpu_bsdf_desc &d, MtsgBsdf &b, std::vector<float> &rt, std::string &err) {
     std::memset(&b, 0, sizeof b);
     b.type = d.type;
+    b.nested[0] = b.nested[1] = -1;
+    if (d.type == MTSGPU_BSDF_TWOSIDED) return MTSGPU_OK;   // resolved by configure_twosided
+    if (d.type == MTSGPU_BSDF_CONDUCTOR || d.type == MTSGPU_BSDF_DIELECTRIC || d.type == MTSGPU_BSDF_PLASTIC)
+        return configure_smooth(d, b, err);
     if (d.type == MTSGPU_BSDF_DIFFUSE) {
         float mx[3];
         tex_max(d.reflectance_tex, d.reflectance, mx);
@@ -808,10 +936,33 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     S.film_h = D->sensor.film_height;
     const uint32_t nb = D->num_bsdfs;
     S.bsdfs.resize(nb + 2);
-    for (uint32_t i = 0; i < nb; ++i) {
+    for (uint32_t i = 0; i < nb; ++i)
         if ((rc = configure_bsdf(D->bsdfs[i], S.bsdfs[i], S.rtrans, err))) return rc;
+    // TwoSidedBRDF::configure (twosided.cpp:82-103): nested[1] defaults to
+    // nested[0]; components = front ones | back ones; no transmission allowed
+    for (uint32_t i = 0; i < nb; ++i) {
+        const mtsgpu_bsdf_desc &d = D->bsdfs[i];
+        if (d.type != MTSGPU_BSDF_TWOSIDED) continue;
+        MtsgBsdf &b = S.bsdfs[i];
+        if (d.nested[0] < 0 || d.nested[0] >= (int)nb) { err = "A nested one-sided material is required!"; return MTSGPU_EINVAL; }
+        const int n1 = d.nested[1] < 0 ? d.nested[0] : d.nested[1];
+        if (n1 >= (int)nb) { err = "twosided: nested BSDF index out of range"; return MTSGPU_EINVAL; }
+        const int n[2] = {d.nested[0], n1};
+        uint32_t flags = 0;
+        for (int k = 0; k < 2; ++k) {
+            const MtsgBsdf &c = S.bsdfs[n[k]];
+            if (c.type == MTSGPU_BSDF_TWOSIDED) { err = "twosided: nesting a twosided BSDF is not supported"; return MTSGPU_EINVAL; }
+            const uint32_t lobes = (uint32_t)c.flags & ~(uint32_t)(MTSG_F_FRONT | MTSG_F_BACK);
+            if (lobes) flags |= lobes | (k == 0 ? MTSG_F_FRONT : MTSG_F_BACK);
+        }
+        if (flags & MTSG_F_TRANSMISSION) { err = "Only materials without a transmission component can be nested!"; return MTSGPU_EINVAL; }
+        b.flags = (int32_t)flags;
+        b.nested[0] = n[0];
+        b.nested[1] = n[1];
+    }
+    for (uint32_t i = 0; i < nb; ++i) {
         const MtsgBsdf &b = S.bsdfs[i];
-        if (b.type == MTSGPU_BSDF_ROUGHPLASTIC || b.refl_tex.type || b.alpha_tex.type) S.ext = true;
+        if (b.type >= MTSGPU_BSDF_ROUGHPLASTIC || b.refl_tex.type || b.alpha_tex.type) S.ext = true;
     }
     {   // Shape::configure defaults (shape.cpp:48-70): black for emitters, 0.5 otherwise
         mtsgpu_bsdf_desc dd; std::memset(&dd, 0, sizeof dd);
@@ -871,9 +1022,20 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         if (m.bsdf >= (int)nb) { err = "bsdf index out of range"; return MTSGPU_EINVAL; }
         sh.bsdf = m.bsdf >= 0 ? m.bsdf : (m.emitter >= 0 ? (int)nb : (int)nb + 1);
         {   // EAnisotropic (roughconductor.cpp:229-231) without texcoords: computeUVTangents error (trimesh.cpp:685-691)
-            const mtsgpu_bsdf_desc *ub = m.bsdf >= 0 ? &D->bsdfs[m.bsdf] : nullptr;
-            if (!m.texcoords && ub && ub->type != MTSGPU_BSDF_DIFFUSE &&
-                fmax_std(ub->alpha_u, 1e-4f) != fmax_std(ub->alpha_v, 1e-4f)) {
+            // (through twosided: its combined type carries the nested EAnisotropic)
+            bool aniso = false;
+            if (m.bsdf >= 0) {
+                const mtsgpu_bsdf_desc *ub = &D->bsdfs[m.bsdf];
+                const int cand[2] = {ub->type == MTSGPU_BSDF_TWOSIDED ? S.bsdfs[m.bsdf].nested[0] : m.bsdf,
+                                     ub->type == MTSGPU_BSDF_TWOSIDED ? S.bsdfs[m.bsdf].nested[1] : m.bsdf};
+                for (int c : cand) {
+                    const mtsgpu_bsdf_desc &cb = D->bsdfs[c];
+                    if ((cb.type == MTSGPU_BSDF_ROUGHCONDUCTOR || cb.type == MTSGPU_BSDF_ROUGHDIELECTRIC) &&
+                        fmax_std(cb.alpha_u, 1e-4f) != fmax_std(cb.alpha_v, 1e-4f))
+                        aniso = true;
+                }
+            }
+            if (!m.texcoords && aniso) {
                 err = "computeUVTangents(): texture coordinates are required to generate tangent vectors. If you "
                       "want to render with an anisotropic material, please make sure that all associated shapes "
                       "have valid texture coordinates.";

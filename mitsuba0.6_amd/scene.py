@@ -58,11 +58,19 @@ def _spec(v):
     return tuple(float(x) for x in v)
 
 
+BSDF_TYPES = {'diffuse': abi.BSDF_DIFFUSE, 'roughconductor': abi.BSDF_ROUGHCONDUCTOR,
+              'roughdielectric': abi.BSDF_ROUGHDIELECTRIC, 'roughplastic': abi.BSDF_ROUGHPLASTIC,
+              'conductor': abi.BSDF_CONDUCTOR, 'dielectric': abi.BSDF_DIELECTRIC,
+              'plastic': abi.BSDF_PLASTIC, 'twosided': abi.BSDF_TWOSIDED}
+
+
 @dataclass
 class BSDF:
-    """One of diffuse / roughconductor / roughdielectric / roughplastic with
-    Mitsuba property names.  `reflectance` (diffuse), `diffuseReflectance`
-    (roughplastic) and `alpha` (rough BSDFs, isotropic) may be a Checkerboard."""
+    """One of diffuse / roughconductor / roughdielectric / roughplastic /
+    conductor / dielectric / plastic / twosided with Mitsuba property names.
+    `reflectance` (diffuse), `diffuseReflectance` ((rough)plastic) and `alpha`
+    (rough BSDFs, isotropic) may be a Checkerboard.  A twosided BSDF holds its
+    one or two nested BSDFs in `nested` (twosided.cpp:63-103)."""
     type: str = 'diffuse'
     reflectance: object = (0.5, 0.5, 0.5)
     distribution: str = 'beckmann'
@@ -82,16 +90,19 @@ class BSDF:
     nonlinear: bool = False
     rtransDir: Optional[str] = None    # where data/microfacet/<distribution>.dat is looked up first (rtrans.py)
     ensureEnergyConservation: bool = True
+    nested: list = field(default_factory=list)   # twosided: [front] or [front, back]
 
     def int_ior(self):
         if self.intIOR is not None:
             return self.intIOR
-        return 'polypropylene' if self.type == 'roughplastic' else 'bk7'
+        return 'polypropylene' if self.type in ('roughplastic', 'plastic') else 'bk7'
 
     def to_desc(self):
         d = abi.BsdfDesc()
-        d.type = {'diffuse': abi.BSDF_DIFFUSE, 'roughconductor': abi.BSDF_ROUGHCONDUCTOR,
-                  'roughdielectric': abi.BSDF_ROUGHDIELECTRIC, 'roughplastic': abi.BSDF_ROUGHPLASTIC}[self.type]
+        if self.type not in BSDF_TYPES:
+            raise NotImplementedError('BSDF plugin "%s" is not on the GPU path' % self.type)
+        d.type = BSDF_TYPES[self.type]
+        d.nested[0] = d.nested[1] = -1
         d.distribution = {'beckmann': abi.DISTR_BECKMANN, 'ggx': abi.DISTR_GGX,
                           'phong': abi.DISTR_PHONG, 'as': abi.DISTR_PHONG}[self.distribution.lower()]
         d.sample_visible = int(self.sampleVisible)
@@ -118,18 +129,19 @@ class BSDF:
             d.reflectance[:] = _spec(self.reflectance)
         d.specular_reflectance[:] = _spec(self.specularReflectance)
         d.specular_transmittance[:] = _spec(self.specularTransmittance)
-        if self.type == 'roughconductor':
+        if self.type in ('roughconductor', 'conductor'):
             # intEta/intK from the material, overridden by explicit 'eta'/'k' (roughconductor.cpp:172-190)
             from .conductors import conductor_rgb
             eta, k = conductor_rgb(self.material or 'Cu')
             d.eta[:] = self.eta if self.eta is not None else eta
             d.k[:] = self.k if self.k is not None else k
-        if self.type == 'roughplastic':
+        if self.type in ('roughplastic', 'plastic'):
             if isinstance(self.diffuseReflectance, Checkerboard):
                 self.diffuseReflectance.fill(d.reflectance_tex)
             else:
                 d.diffuse_reflectance[:] = _spec(self.diffuseReflectance)
             d.nonlinear = int(self.nonlinear)
+        if self.type == 'roughplastic':
             from .rtrans import table_bytes
             data = table_bytes(self.distribution, [self.rtransDir])
             buf = C.create_string_buffer(data, len(data))
@@ -246,10 +258,24 @@ class Scene:
             md[i].num_triangles = idx.shape[0]
             md[i].bsdf, md[i].emitter = m.bsdf, m.emitter
             md[i].face_normals, md[i].flip_normals = int(m.faceNormals), int(m.flipNormals)
-        bd = (abi.BsdfDesc * max(1, len(self.bsdfs)))()
+        # twosided's nested BSDFs go after the scene's own (mesh indices stay valid)
+        flat = list(self.bsdfs)
+        nested_idx = {}
         for i, b in enumerate(self.bsdfs):
+            if b.type == 'twosided':
+                if not 1 <= len(b.nested) <= 2:
+                    raise ValueError('twosided: one or two nested BSDFs (twosided.cpp:82-87, 161-170)')
+                nested_idx[i] = []
+                for nb in b.nested:
+                    nested_idx[i].append(len(flat))
+                    flat.append(nb)
+        bd = (abi.BsdfDesc * max(1, len(flat)))()
+        for i, b in enumerate(flat):
             bdi = b.to_desc()
             keep.append(getattr(bdi, '_keep', None))
+            if i in nested_idx:
+                for k, j in enumerate(nested_idx[i]):
+                    bdi.nested[k] = j
             bd[i] = bdi
         ed = (abi.EmitterDesc * max(1, len(self.emitters)))()
         for i, e in enumerate(self.emitters):
@@ -263,7 +289,7 @@ class Scene:
                 ed[i].env_height, ed[i].env_width = img.shape[0], img.shape[1]
         d = abi.SceneDesc()
         d.meshes, d.num_meshes = md, len(self.meshes)
-        d.bsdfs, d.num_bsdfs = bd, len(self.bsdfs)
+        d.bsdfs, d.num_bsdfs = bd, len(flat)
         d.emitters, d.num_emitters = ed, len(self.emitters)
         s = self.sensor
         d.sensor.fov = s.fov

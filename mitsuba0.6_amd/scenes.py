@@ -96,6 +96,25 @@ def plastic_materials():
     ]
 
 
+def smooth_materials():
+    """Delta BSDFs and twosided: conductor (named and 'none'), dielectric
+    (glass, water-like with a tinted transmittance), plastic (linear, and
+    nonlinear with a textured diffuse base), twosided with one and with two
+    nested BSDFs."""
+    return [
+        BSDF('conductor', material='Cu'),
+        BSDF('dielectric', intIOR=1.5, extIOR='air'),
+        BSDF('plastic', diffuseReflectance=(0.1, 0.3, 0.7)),
+        BSDF('plastic', intIOR=1.6, nonlinear=True,
+             diffuseReflectance=Checkerboard(color0=(0.8, 0.1, 0.1), color1=(0.1, 0.1, 0.8), uscale=4, vscale=4)),
+        BSDF('twosided', nested=[BSDF('diffuse', reflectance=(0.14, 0.45, 0.091))]),
+        BSDF('twosided', nested=[BSDF('plastic', diffuseReflectance=(0.7, 0.6, 0.2)),
+                                 BSDF('roughconductor', distribution='ggx', alpha=0.2, material='Au')]),
+        BSDF('conductor', material='none', specularReflectance=0.8),
+        BSDF('dielectric', intIOR=1.33, extIOR=1.0, specularTransmittance=(0.9, 0.8, 0.7)),
+    ]
+
+
 def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, materials='diffuse'):
     """Config C1 (512x512, 64 spp) / C2 (1280x720, 512 spp): diffuse Cornell box
     with a rectangular area light.  materials='rough' swaps the
@@ -117,10 +136,17 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
         base = len(bsdfs)
         bsdfs += plastic_materials()
         floor_b, short_b, tall_b, back_b = base + 4, base + 1, base + 0, base + 5
-    uv = materials in ('rough', 'plastic')   # UV tangents (anisotropic BSDFs) and texture coordinates
-    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, back_b), (_GREEN, 2), (_RED, 1)):
+    green_b, flip_back = 2, False
+    if materials == 'smooth':
+        # the back wall shows its back side (flipped normals) through twosided
+        base = len(bsdfs)
+        bsdfs += smooth_materials()
+        floor_b, short_b, tall_b, back_b, green_b, flip_back = base + 3, base + 0, base + 1, base + 5, base + 4, True
+    uv = materials in ('rough', 'plastic', 'smooth')   # UV tangents (anisotropic BSDFs) and texture coordinates
+    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, back_b), (_GREEN, green_b), (_RED, 1)):
         m = _quads_mesh([quad], inward=True, uv=uv)
-        meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b))
+        meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b,
+                           flipNormals=flip_back and quad is _BACK))
     for quads, b in ((_SHORT, short_b), (_TALL, tall_b)):
         m = _quads_mesh(quads, inward=False, center=np.mean(np.asarray(quads, np.float64).reshape(-1, 3), 0), uv=uv)
         meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b, faceNormals=True))

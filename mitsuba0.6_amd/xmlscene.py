@@ -295,8 +295,38 @@ class XMLSceneLoader:
                           diffuseReflectance=tex.get('diffuseReflectance', p.get('diffuseReflectance', (0.5, 0.5, 0.5))),
                           nonlinear=p.get('nonlinear', False), rtransDir=os.path.dirname(os.path.abspath(self.path)))
             return BSDF(t, **kw)
+        if t == 'conductor':                       # conductor.cpp:164-181
+            self._tex_params(p, ())
+            return BSDF('conductor', material=p.get('material', 'Cu'), eta=p.get('eta'), k=p.get('k'),
+                        extEta=p.get('extEta', 'air'),
+                        specularReflectance=p.get('specularReflectance', (1.0, 1.0, 1.0)),
+                        ensureEnergyConservation=p.get('ensureEnergyConservation', True))
+        if t == 'dielectric':                      # dielectric.cpp:146-165
+            self._tex_params(p, ())
+            return BSDF('dielectric', intIOR=p.get('intIOR', 'bk7'), extIOR=p.get('extIOR', 'air'),
+                        specularReflectance=p.get('specularReflectance', (1.0, 1.0, 1.0)),
+                        specularTransmittance=p.get('specularTransmittance', (1.0, 1.0, 1.0)),
+                        ensureEnergyConservation=p.get('ensureEnergyConservation', True))
+        if t == 'plastic':                         # plastic.cpp:144-165
+            tex = self._tex_params(p, ('diffuseReflectance',))
+            return BSDF('plastic', intIOR=p.get('intIOR', 'polypropylene'), extIOR=p.get('extIOR', 'air'),
+                        specularReflectance=p.get('specularReflectance', (1.0, 1.0, 1.0)),
+                        diffuseReflectance=tex.get('diffuseReflectance', p.get('diffuseReflectance', (0.5, 0.5, 0.5))),
+                        nonlinear=p.get('nonlinear', False),
+                        ensureEnergyConservation=p.get('ensureEnergyConservation', True))
+        if t == 'twosided':                        # twosided.cpp:63-103, 193-205 (addChild)
+            nested = [self.make_bsdf(c) for _, c in p.children if c.tag == 'bsdf']
+            for _, c in p.children:
+                if c.tag != 'bsdf':
+                    raise SceneError('twosided: unexpected <%s> child' % c.tag)
+            if not nested:
+                raise SceneError('A nested one-sided material is required!')
+            if len(nested) > 2:
+                raise SceneError('No more than two nested BRDFs can be added!')
+            return BSDF('twosided', nested=nested)
         raise NotImplementedError('BSDF plugin "%s" is not on the GPU path (diffuse, roughconductor, '
-                                  'roughdielectric, roughplastic)' % t)
+                                  'roughdielectric, roughplastic, conductor, dielectric, plastic, '
+                                  'twosided)' % t)
 
     def make_area(self, p):
         if p.plugin != 'area':
@@ -545,7 +575,7 @@ def _fmt(x):
 
 
 def _rgb(name, c):
-    return '<rgb name="%s" value="%s"/>' % (name, ', '.join(_fmt(x) for x in c))
+    return '<rgb name="%s" value="%s"/>' % (name, ', '.join(_fmt(x) for x in _spec3(c)))
 
 
 def _checker_xml(name, t):
@@ -579,6 +609,51 @@ def _transform_xml(t):
         else:
             out.append('<%s %s/>' % (tag, ' '.join('%s="%s"' % (k, _fmt(v)) for k, v in a.items())))
     return ''.join(out)
+
+
+def _ior_xml(nm, v, ind):
+    return ind + '<%s name="%s" value="%s"/>' % (('string', nm, v) if isinstance(v, str) else ('float', nm, _fmt(v)))
+
+
+def _bsdf_xml(b, ind, bid=None):
+    """One <bsdf> element (nested BSDFs of twosided inline)."""
+    L = ['%s<bsdf type="%s"%s>' % (ind, b.type, ' id="%s"' % bid if bid else '')]
+    i2 = ind + '  '
+    if b.type == 'twosided':
+        for nb in b.nested:
+            L += _bsdf_xml(nb, i2)
+    elif b.type == 'diffuse':
+        L.append(i2 + _spec_xml('reflectance', b.reflectance))
+    else:
+        if b.type.startswith('rough'):
+            L.append(i2 + '<string name="distribution" value="%s"/>' % b.distribution)
+            if isinstance(b.alpha, Checkerboard):
+                L.append(i2 + _checker_xml('alpha', b.alpha))
+            elif b.alpha is not None:
+                L.append(i2 + '<float name="alpha" value="%s"/>' % _fmt(b.alpha))
+            elif b.alphaU is not None:
+                L.append(i2 + '<float name="alphaU" value="%s"/><float name="alphaV" value="%s"/>'
+                         % (_fmt(b.alphaU), _fmt(b.alphaV)))
+            L.append(i2 + '<boolean name="sampleVisible" value="%s"/>' % str(bool(b.sampleVisible)).lower())
+        L.append(i2 + _rgb('specularReflectance', b.specularReflectance))
+        if b.type in ('roughconductor', 'conductor'):
+            if b.material:                    # None: the plugin default (Cu)
+                L.append(i2 + '<string name="material" value="%s"/>' % b.material)
+            if b.eta is not None:
+                L.append(i2 + _rgb('eta', b.eta))
+            if b.k is not None:
+                L.append(i2 + _rgb('k', b.k))
+            L.append(_ior_xml('extEta', b.extEta, i2))
+        else:
+            L.append(_ior_xml('intIOR', b.int_ior(), i2))
+            L.append(_ior_xml('extIOR', b.extIOR, i2))
+            if b.type in ('roughdielectric', 'dielectric'):
+                L.append(i2 + _rgb('specularTransmittance', b.specularTransmittance))
+            else:
+                L.append(i2 + _spec_xml('diffuseReflectance', b.diffuseReflectance))
+                L.append(i2 + '<boolean name="nonlinear" value="%s"/>' % str(bool(b.nonlinear)).lower())
+    L.append(ind + '</bsdf>')
+    return L
 
 
 def save_scene(scene, integ, directory, name='scene.xml'):
@@ -619,39 +694,7 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     L.append('    </film>')
     L.append('  </sensor>')
     for i, b in enumerate(scene.bsdfs):
-        L.append('  <bsdf type="%s" id="bsdf%d">' % (b.type, i))
-        if b.type == 'diffuse':
-            L.append('    ' + _spec_xml('reflectance', b.reflectance))
-        else:
-            L.append('    <string name="distribution" value="%s"/>' % b.distribution)
-            if isinstance(b.alpha, Checkerboard):
-                L.append('    ' + _checker_xml('alpha', b.alpha))
-            elif b.alpha is not None:
-                L.append('    <float name="alpha" value="%s"/>' % _fmt(b.alpha))
-            elif b.alphaU is not None:
-                L.append('    <float name="alphaU" value="%s"/><float name="alphaV" value="%s"/>'
-                         % (_fmt(b.alphaU), _fmt(b.alphaV)))
-            L.append('    <boolean name="sampleVisible" value="%s"/>' % str(bool(b.sampleVisible)).lower())
-            L.append('    ' + _rgb('specularReflectance', b.specularReflectance))
-            if b.type == 'roughconductor':
-                if b.material:
-                    L.append('    <string name="material" value="%s"/>' % b.material)
-                if b.eta is not None:
-                    L.append('    ' + _rgb('eta', b.eta))
-                if b.k is not None:
-                    L.append('    ' + _rgb('k', b.k))
-                L.append('    <%s name="extEta" value="%s"/>' % (('string', b.extEta) if isinstance(b.extEta, str)
-                                                                 else ('float', _fmt(b.extEta))))
-            else:
-                for nm, v in (('intIOR', b.int_ior()), ('extIOR', b.extIOR)):
-                    L.append('    <%s name="%s" value="%s"/>' % (('string', nm, v) if isinstance(v, str)
-                                                                  else ('float', nm, _fmt(v))))
-                if b.type == 'roughdielectric':
-                    L.append('    ' + _rgb('specularTransmittance', b.specularTransmittance))
-                else:
-                    L.append('    ' + _spec_xml('diffuseReflectance', b.diffuseReflectance))
-                    L.append('    <boolean name="nonlinear" value="%s"/>' % str(bool(b.nonlinear)).lower())
-        L.append('  </bsdf>')
+        L += _bsdf_xml(b, '  ', 'bsdf%d' % i)
     for i, m in enumerate(scene.meshes):
         fn = 'mesh%03d.ply' % i
         write_ply(os.path.join(directory, fn), m)

@@ -48,6 +48,8 @@ def lib():
         L.oracle_camera.argtypes = [C.POINTER(abi.SensorDesc), C.POINTER(C.c_float), C.POINTER(C.c_float)]
         L.oracle_bsdf_sample.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 6 + [C.c_int]
         L.oracle_bsdf_eval.argtypes = [C.POINTER(abi.BsdfDesc)] + [C.POINTER(C.c_float)] * 4 + [C.c_int]
+        L.oracle_fresnel_diffuse_reflectance.restype = C.c_float
+        L.oracle_fresnel_diffuse_reflectance.argtypes = [C.c_float]
         L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
         L.oracle_trace_rays.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.c_uint32, C.c_int,
                                         C.POINTER(C.c_float)]

@@ -855,6 +855,10 @@ typedef struct {
     int nonlinear;
     RTab ext, in;
     Tex reflTex, alphaTex;
+    /* plastic (plastic.cpp:186-216) */
+    float fdrInt, fdrExt;
+    /* twosided (twosided.cpp:63-103): m_nestedBRDF[2] */
+    const void *nested[2];
 } Bsdf;
 
 /* (int) of a float the way x86-64 cvttss2si converts it: out of range / NaN -> INT_MIN */
@@ -1082,9 +1086,134 @@ static int roughplastic_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
     return MTSGPU_OK;
 }
 
+/* fresnelDielectricExt(cosThetaI, eta) (util.cpp:680-683) */
+static float fresnel_dielectric_ext2(float cosThetaI, float eta) {
+    float ct;
+    return fresnel_dielectric_ext(cosThetaI, &ct, eta);
+}
+
+/* GaussLobattoIntegrator(1024, 0, 1e-5f, useConvergenceEstimate = true)
+ * (quad.cpp:287-409) on fresnelDiffuseIntegrand (util.cpp:808-811), i.e.
+ * fresnelDiffuseReflectance(eta, false) (util.cpp:814-860).  The six
+ * recursive steps are summed left to right. */
+typedef struct { float eta; size_t evals; } GLQuad;
+static float gl_alpha(void) { return (float)sqrt(2.0 / 3.0); }
+static float gl_beta(void) { return (float)(1.0 / sqrt(5.0)); }
+static float gl_f(const GLQuad *q, float xi) { return fresnel_dielectric_ext2(sqrtf(xi), q->eta); }
+static float gl_abs_tolerance(GLQuad *q, float a, float b) {
+    const float al = gl_alpha(), be = gl_beta();
+    const float x1 = (float)0.94288241569547971906, x2 = (float)0.64185334234578130578, x3 = (float)0.23638319966214988028;
+    const float m = (a + b) / 2, h = (b - a) / 2;
+    const float y1 = gl_f(q, a), y3 = gl_f(q, m - al * h), y5 = gl_f(q, m - be * h), y7 = gl_f(q, m);
+    const float y9 = gl_f(q, m + be * h), y11 = gl_f(q, m + al * h), y13 = gl_f(q, b);
+    const float acc = h * ((float)0.0158271919734801831 * (y1 + y13)
+                         + (float)0.0942738402188500455 * (gl_f(q, m - x1 * h) + gl_f(q, m + x1 * h))
+                         + (float)0.1550719873365853963 * (y3 + y11)
+                         + (float)0.1888215739601824544 * (gl_f(q, m - x2 * h) + gl_f(q, m + x2 * h))
+                         + (float)0.1997734052268585268 * (y5 + y9)
+                         + (float)0.2249264653333395270 * (gl_f(q, m - x3 * h) + gl_f(q, m + x3 * h))
+                         + (float)0.2426110719014077338 * y7);
+    q->evals += 13;
+    float r = 1.0f;
+    const float integral2 = (h / 6) * (y1 + y13 + 5 * (y5 + y9));
+    const float integral1 = (h / 1470) * (77 * (y1 + y13) + 432 * (y3 + y11) + 625 * (y5 + y9) + 672 * y7);
+    if (fabsf(integral2 - acc) != 0.0f) r = fabsf(integral1 - acc) / fabsf(integral2 - acc);
+    if (r == 0.0f || r > 1.0f) r = 1.0f;
+    float result = INFINITY;
+    if (acc != 0) result = acc * smax(1e-5f, FLT_EPSILON) / (r * FLT_EPSILON);
+    return result;
+}
+static float gl_step(GLQuad *q, float a, float b, float fa, float fb, float acc) {
+    const float al = gl_alpha(), be = gl_beta();
+    const float h = (b - a) / 2, m = (a + b) / 2;
+    const float mll = m - al * h, ml = m - be * h, mr = m + be * h, mrr = m + al * h;
+    const float fmll = gl_f(q, mll), fml = gl_f(q, ml), fm = gl_f(q, m), fmr = gl_f(q, mr), fmrr = gl_f(q, mrr);
+    const float integral2 = (h / 6) * (fa + fb + 5 * (fml + fmr));
+    const float integral1 = (h / 1470) * (77 * (fa + fb) + 432 * (fmll + fmrr) + 625 * (fml + fmr) + 672 * fm);
+    q->evals += 5;
+    if (q->evals >= 1024) return integral1;
+    const float dist = acc + (integral1 - integral2);
+    if (dist == acc || mll <= a || b <= mrr) return integral1;
+    float r = gl_step(q, a, mll, fa, fmll, acc);
+    r = r + gl_step(q, mll, ml, fmll, fml, acc);
+    r = r + gl_step(q, ml, m, fml, fm, acc);
+    r = r + gl_step(q, m, mr, fm, fmr, acc);
+    r = r + gl_step(q, mr, mrr, fmr, fmrr, acc);
+    r = r + gl_step(q, mrr, b, fmrr, fb, acc);
+    return r;
+}
+float oracle_fresnel_diffuse_reflectance(float eta) {
+    GLQuad q = {eta, 0};
+    const float tol = gl_abs_tolerance(&q, 0.0f, 1.0f);
+    q.evals += 2;
+    return gl_step(&q, 0.0f, 1.0f, gl_f(&q, 0.0f), gl_f(&q, 1.0f), tol);
+}
+
+/* SmoothConductor / SmoothDielectric / SmoothPlastic ctor + configure
+ * (conductor.cpp:164-212, dielectric.cpp:146-201, plastic.cpp:144-216) */
+static int smooth_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
+    V3 sr = d3(d->specular_reflectance);
+    float ss = tex_scale_for_energy(sr, d->ensure_energy_conservation);
+    b->specR = ss != 1.0f ? vmul(sr, ss) : sr;
+    if (d->type == MTSGPU_BSDF_CONDUCTOR) {
+        float r = 1.0f / d->ext_eta;
+        b->eta3 = vmul(d3(d->eta), r);
+        b->k3 = vmul(d3(d->k), r);
+        b->flags = E_DELTA_REFL | E_FRONT;
+        return MTSGPU_OK;
+    }
+    if (d->int_ior < 0 || d->ext_ior < 0) return MTSGPU_EINVAL;
+    b->eta = d->int_ior / d->ext_ior;
+    if (d->type == MTSGPU_BSDF_DIELECTRIC) {
+        b->invEta = 1 / b->eta;
+        V3 st = d3(d->specular_transmittance);
+        float sct = tex_scale_for_energy(st, d->ensure_energy_conservation);
+        b->specT = sct != 1.0f ? vmul(st, sct) : st;
+        b->flags = E_DELTA_REFL | E_DELTA_TRANS | E_FRONT | E_BACK;
+        return MTSGPU_OK;
+    }
+    b->nonlinear = d->nonlinear != 0;
+    V3 dr = d3(d->diffuse_reflectance);
+    float sd = tex_scale_for_energy(tdesc_max(&d->reflectance_tex, dr), d->ensure_energy_conservation);
+    b->refl = sd != 1.0f ? vmul(dr, sd) : dr;
+    int rc;
+    if ((rc = tex_configure(&d->reflectance_tex, sd, &b->reflTex))) return rc;
+    b->fdrInt = oracle_fresnel_diffuse_reflectance(1 / b->eta);
+    b->fdrExt = oracle_fresnel_diffuse_reflectance(b->eta);
+    V3 davg = tdesc_avg(&d->reflectance_tex, dr);
+    if (sd != 1.0f) davg = vmul(davg, sd);
+    float dAvg = luminance3(davg), sAvg = luminance3(b->specR);
+    b->specWeight = sAvg / (dAvg + sAvg);
+    b->invEta2 = 1 / (b->eta * b->eta);
+    b->flags = E_DELTA_REFL | E_DIFF_REFL | E_FRONT;
+    return MTSGPU_OK;
+}
+
+/* TwoSidedBRDF::configure (twosided.cpp:82-103); `all` = the scene's BSDFs */
+static int twosided_configure(const mtsgpu_bsdf_desc *d, Bsdf *b, const Bsdf *all, uint32_t n) {
+    if (d->nested[0] < 0 || d->nested[0] >= (int)n) return MTSGPU_EINVAL;
+    int n1 = d->nested[1] < 0 ? d->nested[0] : d->nested[1];
+    if (n1 >= (int)n) return MTSGPU_EINVAL;
+    b->nested[0] = &all[d->nested[0]];
+    b->nested[1] = &all[n1];
+    int flags = 0;
+    for (int k = 0; k < 2; ++k) {
+        const Bsdf *c = (const Bsdf *)b->nested[k];
+        if (c->type == MTSGPU_BSDF_TWOSIDED) return MTSGPU_EINVAL;
+        int lobes = c->flags & ~(E_FRONT | E_BACK);
+        if (lobes) flags |= lobes | (k == 0 ? E_FRONT : E_BACK);
+    }
+    if (flags & E_TRANSMISSION) return MTSGPU_EINVAL;
+    b->flags = flags;
+    return MTSGPU_OK;
+}
+
 static int bsdf_configure(const mtsgpu_bsdf_desc *d, Bsdf *b) {
     memset(b, 0, sizeof *b);
     b->type = d->type;
+    if (d->type == MTSGPU_BSDF_TWOSIDED) return MTSGPU_OK; /* twosided_configure, once all are built */
+    if (d->type == MTSGPU_BSDF_CONDUCTOR || d->type == MTSGPU_BSDF_DIELECTRIC || d->type == MTSGPU_BSDF_PLASTIC)
+        return smooth_configure(d, b);
     if (d->type == MTSGPU_BSDF_DIFFUSE) {
         V3 r = d3(d->reflectance);
         float sc = tex_scale_for_energy(tdesc_max(&d->reflectance_tex, r), d->ensure_energy_conservation);
@@ -1186,8 +1315,93 @@ static float rp_pdf(const Bsdf *b, const BRec *r) { /* RoughPlastic::pdf (roughp
     return result;
 }
 
+/* SmoothPlastic's diffuse term (plastic.cpp:270-280) */
+static V3 sp_diffuse(const Bsdf *b, const BRec *r) {
+    V3 diff = bsdf_refl(b, r);
+    if (b->nonlinear) diff = vdivv(diff, vsub(v3(1.0f, 1.0f, 1.0f), vmul(diff, b->fdrInt)));
+    else diff = vdiv(diff, 1 - b->fdrInt);
+    return diff;
+}
+static float sp_prob_specular(const Bsdf *b, float Fi) { /* plastic.cpp:296-299 */
+    return (Fi * b->specWeight) / (Fi * b->specWeight + (1 - Fi) * (1 - b->specWeight));
+}
+
+/* eval()/pdf() with measure = ESolidAngle, the only measure Li() queries
+ * (path.cpp:185,195): delta lobes contribute nothing there
+ * (conductor.cpp:216-245, dielectric.cpp:228-275, plastic.cpp:245-311) */
+static V3 sm_eval(const Bsdf *b, const BRec *r) {
+    if (b->type != MTSGPU_BSDF_PLASTIC) return v3(0, 0, 0);
+    if (r->wo.z <= 0 || r->wi.z <= 0) return v3(0, 0, 0);
+    float Fi = fresnel_dielectric_ext2(r->wi.z, b->eta);
+    float Fo = fresnel_dielectric_ext2(r->wo.z, b->eta);
+    V3 diff = sp_diffuse(b, r);
+    return vmul(diff, cosine_hemisphere_pdf(r->wo) * b->invEta2 * (1 - Fi) * (1 - Fo));
+}
+static float sm_pdf(const Bsdf *b, const BRec *r) {
+    if (b->type != MTSGPU_BSDF_PLASTIC) return 0.0f;
+    if (r->wo.z <= 0 || r->wi.z <= 0) return 0.0f;
+    float Fi = fresnel_dielectric_ext2(r->wi.z, b->eta);
+    float probSpecular = sp_prob_specular(b, Fi);
+    return cosine_hemisphere_pdf(r->wo) * (1 - probSpecular);
+}
+/* sample(bRec, pdf, sample) (conductor.cpp:269-283, dielectric.cpp:277-333, plastic.cpp:356-420) */
+static V3 sm_sample(const Bsdf *b, BRec *r, float *pdf, float sx, float sy) {
+    V3 zero = v3(0, 0, 0);
+    if (b->type == MTSGPU_BSDF_CONDUCTOR) {
+        if (r->wi.z <= 0) return zero;
+        r->sampledType = E_DELTA_REFL;
+        r->wo = v3(-r->wi.x, -r->wi.y, r->wi.z);
+        r->eta = 1.0f;
+        *pdf = 1;
+        return vmulv(b->specR, fresnel_conductor_exact(r->wi.z, b->eta3, b->k3));
+    }
+    if (b->type == MTSGPU_BSDF_DIELECTRIC) {
+        float cosThetaT;
+        float F = fresnel_dielectric_ext(r->wi.z, &cosThetaT, b->eta);
+        if (sx <= F) {
+            r->sampledType = E_DELTA_REFL;
+            r->wo = v3(-r->wi.x, -r->wi.y, r->wi.z);
+            r->eta = 1.0f;
+            *pdf = F;
+            return b->specR;
+        }
+        float scale = -(cosThetaT < 0 ? b->invEta : b->eta);
+        r->sampledType = E_DELTA_TRANS;
+        r->wo = v3(scale * r->wi.x, scale * r->wi.y, cosThetaT);
+        r->eta = cosThetaT < 0 ? b->eta : b->invEta;
+        *pdf = 1 - F;
+        float factor = cosThetaT < 0 ? b->invEta : b->eta; /* mode == ERadiance */
+        return vmul(b->specT, factor * factor);
+    }
+    /* plastic */
+    if (r->wi.z <= 0) return zero;
+    float Fi = fresnel_dielectric_ext2(r->wi.z, b->eta);
+    r->eta = 1.0f;
+    float probSpecular = sp_prob_specular(b, Fi);
+    if (sx < probSpecular) {
+        r->sampledType = E_DELTA_REFL;
+        r->wo = v3(-r->wi.x, -r->wi.y, r->wi.z);
+        *pdf = probSpecular;
+        return vdiv(vmul(b->specR, Fi), probSpecular);
+    }
+    r->sampledType = E_DIFF_REFL;
+    r->wo = square_to_cosine_hemisphere((sx - probSpecular) / (1 - probSpecular), sy);
+    float Fo = fresnel_dielectric_ext2(r->wo.z, b->eta);
+    V3 diff = sp_diffuse(b, r);
+    *pdf = (1 - probSpecular) * cosine_hemisphere_pdf(r->wo);
+    return vmul(diff, b->invEta2 * (1 - Fi) * (1 - Fo) / (1 - probSpecular));
+}
+
 static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
     V3 zero = v3(0, 0, 0);
+    if (b->type == MTSGPU_BSDF_TWOSIDED) { /* twosided.cpp:105-117 */
+        BRec q = *r;
+        if (q.wi.z > 0) return bsdf_eval((const Bsdf *)b->nested[0], &q);
+        q.wi.z *= -1;
+        q.wo.z *= -1;
+        return bsdf_eval((const Bsdf *)b->nested[1], &q);
+    }
+    if (b->type >= MTSGPU_BSDF_CONDUCTOR) return sm_eval(b, r);
     if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:110-117 */
         /* bRec.typeMask = EAll, so only the cosine tests can reject */
         if (r->wi.z <= 0 || r->wo.z <= 0) return zero;
@@ -1236,6 +1450,14 @@ static V3 bsdf_eval(const Bsdf *b, const BRec *r) {
 }
 
 static float bsdf_pdf(const Bsdf *b, const BRec *r) {
+    if (b->type == MTSGPU_BSDF_TWOSIDED) { /* twosided.cpp:119-131 */
+        BRec q = *r;
+        if (q.wi.z > 0) return bsdf_pdf((const Bsdf *)b->nested[0], &q);
+        q.wi.z *= -1;
+        q.wo.z *= -1;
+        return bsdf_pdf((const Bsdf *)b->nested[1], &q);
+    }
+    if (b->type >= MTSGPU_BSDF_CONDUCTOR) return sm_pdf(b, r);
     if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:119-126 */
         if (r->wi.z <= 0 || r->wo.z <= 0) return 0.0f;
         return cosine_hemisphere_pdf(r->wo);
@@ -1277,6 +1499,17 @@ static float bsdf_pdf(const Bsdf *b, const BRec *r) {
  * roughdielectric lobe choice (roughdielectric.cpp:554) */
 static V3 bsdf_sample(const Bsdf *b, BRec *r, float *pdf, float sx, float sy, Sampler *smp) {
     V3 zero = v3(0, 0, 0);
+    if (b->type == MTSGPU_BSDF_TWOSIDED) { /* twosided.cpp:151-172 */
+        int flipped = 0;
+        if (r->wi.z < 0) { r->wi.z *= -1; flipped = 1; }
+        V3 result = bsdf_sample((const Bsdf *)b->nested[flipped], r, pdf, sx, sy, smp);
+        if (flipped) {
+            r->wi.z *= -1;
+            if (!vzero(result) && *pdf != 0) r->wo.z *= -1;
+        }
+        return result;
+    }
+    if (b->type >= MTSGPU_BSDF_CONDUCTOR) return sm_sample(b, r, pdf, sx, sy);
     if (b->type == MTSGPU_BSDF_DIFFUSE) { /* diffuse.cpp:139-150 */
         if (r->wi.z <= 0) return zero;
         r->wo = square_to_cosine_hemisphere(sx, sy);
@@ -1963,6 +2196,9 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
     S->bsdfs = (Bsdf *)calloc(D->num_bsdfs + 2, sizeof(Bsdf));
     for (uint32_t i = 0; i < D->num_bsdfs; ++i)
         if ((rc = bsdf_configure(&D->bsdfs[i], &S->bsdfs[i]))) return rc;
+    for (uint32_t i = 0; i < D->num_bsdfs; ++i)
+        if (D->bsdfs[i].type == MTSGPU_BSDF_TWOSIDED &&
+            (rc = twosided_configure(&D->bsdfs[i], &S->bsdfs[i], S->bsdfs, D->num_bsdfs))) return rc;
     /* Shape::configure default BSDFs (shape.cpp:48-70) */
     mtsgpu_bsdf_desc dd; memset(&dd, 0, sizeof dd);
     dd.type = MTSGPU_BSDF_DIFFUSE; dd.ensure_energy_conservation = 1;
@@ -2709,6 +2945,7 @@ static mtsgpu_bsdf_desc g_probe_desc;
 static Bsdf g_probe_bsdf;
 static int g_probe_valid = 0;
 static int probe_bsdf(const mtsgpu_bsdf_desc *bd, Bsdf *out) {
+    if (bd->type == MTSGPU_BSDF_TWOSIDED) return MTSGPU_EINVAL; /* needs the scene's nested BSDFs */
     if (!g_probe_valid || memcmp(bd, &g_probe_desc, sizeof *bd) != 0) {
         if (g_probe_valid) bsdf_free(&g_probe_bsdf);
         g_probe_valid = 0;

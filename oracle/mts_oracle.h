@@ -45,6 +45,8 @@ int oracle_camera(const mtsgpu_sensor_desc *s, float *sample_to_camera16, float 
 /* Microfacet / BSDF probes for consistency tests: see mts_oracle.c */
 int oracle_bsdf_sample(const mtsgpu_bsdf_desc *b, const float *wi3, const float *u3,
                        float *wo3, float *weight3, float *pdf, float *eta, int libm_mode);
+/* fresnelDiffuseReflectance(eta, false) (util.cpp:814-860): plastic's m_fdrInt/m_fdrExt */
+float oracle_fresnel_diffuse_reflectance(float eta);
 int oracle_bsdf_eval(const mtsgpu_bsdf_desc *b, const float *wi3, const float *wo3,
                      float *value3, float *pdf, int libm_mode);
 

@@ -35,7 +35,11 @@ CASES = {
     'rp_phong_nonlinear': BSDF('roughplastic', distribution='phong', alpha=0.3, nonlinear=True, rtransDir=RT_DIR),
     'rp_ggx_all_tex': BSDF('roughplastic', distribution='ggx', sampleVisible=False, rtransDir=RT_DIR,
                            alpha=Checkerboard(color0=0.25, color1=0.05)),   # uv (0,0) -> color0
+    # smooth plastic: the diffuse lobe is checked here, its delta coating in test_oracle_smooth.py
+    'plastic': BSDF('plastic', diffuseReflectance=(0.3, 0.5, 0.7)),
+    'plastic_nonlinear': BSDF('plastic', intIOR=1.6, nonlinear=True, diffuseReflectance=(0.8, 0.4, 0.1)),
 }
+DELTA = 0x20 | 0x40   # EDeltaReflection | EDeltaTransmission: no density w.r.t. solid angle
 
 
 def _f3(v):
@@ -70,8 +74,8 @@ def test_sample_weight_matches_eval_over_pdf(oracle, name):
         wi = _wi(ct)
         for _ in range(400):
             u = rng.random(3).astype(np.float32)
-            wo, w, pdf, _ = _sample(L, d, wi, u)
-            if not np.any(w):
+            wo, w, pdf, t = _sample(L, d, wi, u)
+            if not np.any(w) or t & DELTA:
                 continue
             f, p = _eval(L, d, wi, wo)
             assert p > 0 and np.isfinite(w).all()
@@ -89,8 +93,8 @@ def _chi2(L, d, wi, n=40000, nt=16, nphi=32, seed=3, both=False, k=8):
     lo = -1.0 if both else 0.0
     obs = np.zeros((nt, nphi))
     for _ in range(n):
-        wo, w, pdf, _ = _sample(L, d, wi, rng.random(3).astype(np.float32))
-        if not np.any(w):
+        wo, w, pdf, t = _sample(L, d, wi, rng.random(3).astype(np.float32))
+        if not np.any(w) or t & DELTA:
             continue
         ct = float(np.clip(wo[2], -1, 1))
         ph = float(np.arctan2(wo[1], wo[0])) % (2 * np.pi)
@@ -131,10 +135,10 @@ def _chi2(L, d, wi, n=40000, nt=16, nphi=32, seed=3, both=False, k=8):
 
 
 @pytest.mark.parametrize('name', ['diffuse', 'rc_beckmann', 'rc_ggx', 'rc_ggx_all', 'rc_ggx_aniso', 'rd_ggx',
-                                  'rp_beckmann', 'rp_ggx', 'rp_phong_nonlinear', 'rp_ggx_all_tex'])
+                                  'rp_beckmann', 'rp_ggx', 'rp_phong_nonlinear', 'rp_ggx_all_tex', 'plastic'])
 def test_chi_square_goodness_of_fit(oracle, name):
     L = oracle.lib()
     d = CASES[name].to_desc()
     p, frac = _chi2(L, d, _wi(0.7), n=20000, both=name.startswith('rd'))
     assert p > 0.0025, (name, p)
-    assert frac > 0.5
+    assert frac > (0.3 if name == 'plastic' else 0.5)

@@ -16,6 +16,7 @@ from mitsuba_amd.xmlscene import SceneError, cube_mesh, load_scene, read_pfm, sa
 
 @pytest.mark.parametrize('cfg,kw', [('C1', dict(width=40, height=30, spp=4)),
                                     ('C1', dict(width=24, height=24, spp=4, materials='rough')),
+                                    ('C1', dict(width=24, height=24, spp=4, materials='smooth')),
                                     ('C3', dict(width=32, height=18, spp=4, env_size=(64, 32), blob=(24, 16)))])
 def test_round_trip_renders_identically(tmp_path, oracle, cfg, kw):
     sc, it = scenes.build(cfg, **kw)
