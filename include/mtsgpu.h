@@ -122,6 +122,13 @@ typedef struct {
                                     /* library inverts env_to_world (Gauss-Jordan) */
 } mtsgpu_emitter_desc;
 
+enum { /* shape plugins (src/shapes) */
+    MTSGPU_SHAPE_TRIMESH = 0,        /* obj / ply / serialized / cube: world-space triangles */
+    MTSGPU_SHAPE_RECTANGLE = 1,      /* rectangle.cpp: [-1,1]^2 x {0} under 'toWorld'        */
+    MTSGPU_SHAPE_DISK = 2,           /* disk.cpp: unit disk in z = 0 under 'toWorld'         */
+    MTSGPU_SHAPE_SPHERE = 3          /* sphere.cpp: 'center', 'radius', optional 'toWorld'   */
+};
+
 typedef struct {
     const float *positions;         /* 3*num_vertices, world space                 */
     const float *normals;           /* 3*num_vertices or NULL                      */
@@ -132,6 +139,15 @@ typedef struct {
     int32_t emitter;                /* index into emitters (area), -1: none        */
     int32_t face_normals;           /* 'faceNormals'                               */
     int32_t flip_normals;           /* 'flipNormals'                               */
+    /* analytic shapes (shape_type != TRIMESH) are one primitive each, intersected
+       exactly as the plugin's rayIntersect does; positions/indices are unused */
+    int32_t shape_type;             /* MTSGPU_SHAPE_*                              */
+    int32_t has_to_world;           /* 'toWorld' given (sphere.cpp:113-121)        */
+    float to_world[16];             /* row-major 'toWorld' (identity if absent)    */
+    float to_world_inv[16];         /* its inverse as the reference's Transform    */
+                                    /* carries it; all zero: the library inverts   */
+    float center[3];                /* sphere 'center' (default 0)                 */
+    float radius;                   /* sphere 'radius' (default 1)                 */
 } mtsgpu_mesh_desc;
 
 enum { MTSGPU_FOV_X = 0, MTSGPU_FOV_Y = 1, MTSGPU_FOV_DIAGONAL = 2,

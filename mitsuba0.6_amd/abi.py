@@ -17,6 +17,7 @@ TEX_NONE, TEX_CHECKERBOARD = 0, 1
 ABI_VERSION = 3
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP = 0, 1
+SHAPE_TRIMESH, SHAPE_RECTANGLE, SHAPE_DISK, SHAPE_SPHERE = 0, 1, 2, 3
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 SAMPLE_RECORD_FLOATS = 8
@@ -56,7 +57,9 @@ class MeshDesc(C.Structure):
                 ('texcoords', C.POINTER(C.c_float)), ('indices', C.POINTER(C.c_uint32)),
                 ('num_vertices', C.c_uint32), ('num_triangles', C.c_uint32),
                 ('bsdf', C.c_int32), ('emitter', C.c_int32),
-                ('face_normals', C.c_int32), ('flip_normals', C.c_int32)]
+                ('face_normals', C.c_int32), ('flip_normals', C.c_int32),
+                ('shape_type', C.c_int32), ('has_to_world', C.c_int32), ('to_world', _f16),
+                ('to_world_inv', _f16), ('center', _f3), ('radius', C.c_float)]
 
 
 class SensorDesc(C.Structure):

@@ -66,7 +66,7 @@ struct mtsgpu_ctx {
     MtsgDeviceScene dscene;
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights;
-    DevBuf rtrans, texcoords;
+    DevBuf rtrans, texcoords, analytic;
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
@@ -184,7 +184,8 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         denv = (const MtsgEnv *)ctx->env.p;
     }
     if ((!H.rtrans.empty() && (e = upload(ctx->rtrans, H.rtrans, s)) != hipSuccess) ||
-        (!H.texcoords.empty() && (e = upload(ctx->texcoords, H.texcoords, s)) != hipSuccess))
+        (!H.texcoords.empty() && (e = upload(ctx->texcoords, H.texcoords, s)) != hipSuccess) ||
+        (!H.analytic.empty() && (e = upload(ctx->analytic, H.analytic, s)) != hipSuccess))
         return hip_fail(ctx, e, "texture/table upload");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "scene upload sync");
     MtsgDeviceScene &D = ctx->dscene;
@@ -208,6 +209,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     D.env_emitter = H.env.emitter;
     D.rtrans = H.rtrans.empty() ? nullptr : (const float *)ctx->rtrans.p;
     D.texcoords = H.texcoords.empty() ? nullptr : (const float *)ctx->texcoords.p;
+    D.analytic = H.analytic.empty() ? nullptr : (const MtsgAnalytic *)ctx->analytic.p;
     for (int a = 0; a < 3; ++a) { D.aabb_min[a] = H.aabb_min[a]; D.aabb_max[a] = H.aabb_max[a]; }
     D.cam = H.cam;
     ctx->have_scene = true;
@@ -305,6 +307,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
     // LDS as the rest allows (the others are read through L1/L2)
     L.ext = H.ext ? 1u : 0u;
+    L.ana = H.analytic.empty() ? 0u : 1u;
     L.waves = 3;
     if (!L.scene_lds) {
         const size_t perBlock = (160u << 10) / 4;

@@ -77,10 +77,31 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
 };
 
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };
-enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2 };   // path_kernel variants   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
+enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4 };   // path_kernel variants   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
 
 struct MtsgShape {
     int32_t bsdf, emitter, has_normals, has_uv;
+    int32_t kind;            // MTSGPU_SHAPE_* (0: triangle mesh)
+    int32_t analytic;        // index into MtsgDeviceScene::analytic, -1: triangle mesh
+};
+
+// Analytic shapes (shapes/rectangle.cpp, disk.cpp, sphere.cpp): one primitive
+// each; its TriAccel slot carries k = MTSG_K_ANALYTIC and the record index in
+// the n_u bits.  Static per-shape quantities the plugins derive in their
+// constructors / configure() are precomputed on the host.
+#define MTSG_K_ANALYTIC 4u
+enum { MTSG_SHAPE_TRIMESH = 0, MTSG_SHAPE_RECTANGLE = 1, MTSG_SHAPE_DISK = 2, MTSG_SHAPE_SPHERE = 3 };   // = MTSGPU_SHAPE_*
+struct MtsgAnalytic {        // 240 B
+    int32_t type;            // MTSGPU_SHAPE_RECTANGLE / _DISK / _SPHERE
+    int32_t flip;            // sphere m_flipNormals
+    float radius;            // sphere m_radius
+    float inv_area;          // m_invSurfaceArea
+    float to_world[16];      // m_objectToWorld (row-major)
+    float to_obj[16];        // m_worldToObject = its inverse as the Transform carries it
+    float center[3];         // sphere m_center
+    float n[3];              // rectangle m_frame.n; disk normalize(trafo(Normal(0,0,1)))
+    float fs[3], ft[3];      // rectangle m_frame.s, m_frame.t
+    float dpdu[3], dpdv[3];  // rectangle m_dpdu, m_dpdv
 };
 
 struct MtsgEmitter {
@@ -147,6 +168,7 @@ struct MtsgDeviceScene {
     const MtsgEnv *env;         // device copy, or null without an environment emitter
     const float *rtrans;        // roughplastic rough-transmittance slices (rtrans.h)
     const float *texcoords;     // 2 per vertex (textured scenes), else null
+    const MtsgAnalytic *analytic;   // analytic shape records, or null
     uint32_t num_emitters, num_prims;
     float em_norm;
     int32_t env_emitter;        // index of the environment emitter, -1: none
@@ -189,6 +211,7 @@ struct MtsgLaunch {
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
+    uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

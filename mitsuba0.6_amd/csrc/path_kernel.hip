@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "danalytic.h"
 #include "dbsdf.h"
 #include "denv.h"
 #include "layout.h"
@@ -134,10 +135,11 @@ __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float(
 // leaf parks it and keeps descending until every lane of the wave holds a
 // leaf; then all lanes test their parked leaves together.  Same closest hit
 // (tie rule included) as a plain depth-first traversal.
-template <bool ANY, bool STATS, typename NodeT, typename TriT>
+template <bool ANY, bool STATS, bool ANA = false, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
-                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests,
+                                         const MtsgAnalytic *anaArr = nullptr) {
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
@@ -216,7 +218,21 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
                 else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
                 else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-                else continue;
+                else {
+                    if constexpr (ANA) {
+                        // analytic primitive (skdtree.h:280-290: Shape::rayIntersect on [mint, maxt])
+                        float at, alx, aly;
+                        if (k == MTSG_K_ANALYTIC &&
+                            ana_intersect<ANY>(((GAna *)anaArr)[__float_as_uint(q0.y)], o, d, mint, bt, at, alx, aly)) {
+                            if (ANY) return true;
+                            const uint32_t prim = __float_as_uint(q2.z);
+                            if (!found || at < bt || prim > bestPrim) {
+                                found = true; bestPrim = prim; bestSlot = i; bt = at; bu = alx; bv = aly;
+                            }
+                        }
+                    }
+                    continue;
+                }
                 const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
                 const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
                 const float c_nu = q2.x, c_nv = q2.y;
@@ -245,10 +261,12 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     return found;
 }
 #else
-template <bool ANY, bool STATS, typename NodeT, typename TriT>
+template <bool ANY, bool STATS, bool ANA = false, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
-                                         float &bt, unsigned long long &nodes, unsigned long long &tests) {
+                                         float &bt, unsigned long long &nodes, unsigned long long &tests,
+                                         const MtsgAnalytic *anaArr = nullptr) {
+    static_assert(!ANA, "the if-if traversal ablation has no analytic primitives");
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     // reciprocal direction for the (conservative) node tests; exact zeros use
@@ -314,7 +332,21 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
                 else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
                 else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-                else continue;
+                else {
+                    if constexpr (ANA) {
+                        // analytic primitive (skdtree.h:280-290: Shape::rayIntersect on [mint, maxt])
+                        float at, alx, aly;
+                        if (k == MTSG_K_ANALYTIC &&
+                            ana_intersect<ANY>(((GAna *)anaArr)[__float_as_uint(q0.y)], o, d, mint, bt, at, alx, aly)) {
+                            if (ANY) return true;
+                            const uint32_t prim = __float_as_uint(q2.z);
+                            if (!found || at < bt || prim > bestPrim) {
+                                found = true; bestPrim = prim; bestSlot = i; bt = at; bu = alx; bv = aly;
+                            }
+                        }
+                    }
+                    continue;
+                }
                 const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
                 const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
                 const float c_nu = q2.x, c_nv = q2.y;
@@ -394,9 +426,24 @@ __device__ __forceinline__ Frame shading_frame(f3 n, f3 dpdu) {
 }
 
 // fillIntersectionRecord<true> (skdtree.h:343-429); UV = TEX
-template <bool TEX>
-__device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot, float u, float v, float t, f3 d,
+template <bool TEX, bool ANA = false>
+__device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot, float u, float v, float t, f3 o, f3 d,
                                          Hit &h) {
+    if constexpr (ANA) {
+        const MtsgTri &tr = S.tris[slot];
+        if (tr.k == MTSG_K_ANALYTIC) {   // Shape::fillIntersectionRecord + skdtree.h:425-427
+            const AnaHit a = ana_fill(((GAna *)S.analytic)[__float_as_uint(tr.n_u)], o, d, t, u, v);
+            h.valid = 1;
+            h.t = t;
+            h.shape = (int)tr.shape;
+            h.p = a.p;
+            h.geoN = a.geoN;
+            h.sh = shading_frame(a.shN, a.dpdu);
+            h.wi = to_local(h.sh, neg(d));
+            if constexpr (TEX) { h.u = a.u; h.v = a.v; }
+            return;
+        }
+    }
     const uint32_t prim = S.tris[slot].prim;
     const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
     h.valid = 1;
@@ -599,7 +646,8 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     constexpr bool STATS = INSTR;
-    constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0;
+    constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
+                   ANA = (FEAT & MTSG_FEAT_ANA) != 0;
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
     // LDS: [Sobol nibble tables][look_up column tables][BVH + TriAccel (small scenes)][stacks]
@@ -717,9 +765,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 #endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS)
-                    occluded = traverse<true, STATS>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
                 else
-                    occluded = traverse<true, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests);
+                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
             }
         }
         bool hit = false;
@@ -730,9 +778,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             float mint, maxt;
             if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
-                    hit = traverse<false, STATS>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
                 else
-                    hit = traverse<false, STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests);
+                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
             }
         }
 
@@ -747,7 +795,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 endPath = true;   // the BSDF sample at the previous vertex failed
             } else {
                 // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
-                if (hit) fill_hit<EXT>(S, slot, hu, hv, ht, rd, P.its); else P.its.valid = 0;
+                if (hit) fill_hit<EXT, ANA>(S, slot, hu, hv, ht, ro, rd, P.its); else P.its.valid = 0;
                 if (STATS && hit) cHits++;
                 if (primary) {
                     P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
@@ -783,8 +831,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             const MtsgEmitter &e = S.emitters[sh.emitter];
                             const f3 dn = P.its.sh.n;
                             float pdf = 0.0f;
-                            if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0)
-                                pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
+                            if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0) {
+                                if (ANA && S.shapes[P.its.shape].analytic >= 0)   // dRec.ref = the previous vertex
+                                    pdf = ana_pdf_direct(((GAna *)S.analytic)[S.shapes[P.its.shape].analytic], ro, rd,
+                                                         dn, P.its.t);
+                                else
+                                    pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
+                            }
                             lumPdf = pdf * (e.weight * S.em_norm);
                         }
                         const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
@@ -853,6 +906,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                 const EnvSample es = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey);
                                 value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
 #endif
+                            } else if (ANA && S.shapes[e.shape].analytic >= 0) {
+                                const AnaSample as =
+                                    ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], P.its.p, ex, ey);
+                                dd = as.d; dist = as.dist; pdf = as.pdf;
+                                // AreaLight::sampleDirect (area.cpp:158-173)
+                                if (dot(dd, P.refN) >= 0 && dot(dd, as.n) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+                                else pdf = 0.0f;
                             } else {
                             // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
                             float py2 = ey;
@@ -998,7 +1058,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 // Scene::rayIntersect / Scene::isOccluded on a batch of rays (one ray per lane):
 // rays[2i] = {o, mint}, rays[2i+1] = {d, maxt}; out[i] = {t, u, v, prim bits}
 // (prim 0xffffffff and t = inf: no hit; the shadow query writes t = 1 / 0)
-template <bool ANY, int WAVES>
+template <bool ANY, int WAVES, bool ANA>
 __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(MtsgDeviceScene S, const float4 *__restrict__ rays,
                                                               uint32_t n, float4 *__restrict__ out,
                                                               uint32_t stackDepth) {
@@ -1014,8 +1074,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(MtsgDeviceScene S, 
         if (ray_interval(S, o, d, a.w, b.w, ANY, mint, maxt)) {
             uint32_t slot = 0;
             float u = 0, v = 0, t = 0;
-            const bool hit = traverse<ANY, false>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
-                                                  slot, u, v, t, cn, ct);
+            const bool hit = traverse<ANY, false, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN,
+                                                       stkD, slot, u, v, t, cn, ct, S.analytic);
             if (ANY) r.x = hit ? 1.0f : 0.0f;
             else if (hit) r = make_float4(t, u, v, __uint_as_float(S.tris[slot].prim));
         } else if (ANY) {
@@ -1098,7 +1158,8 @@ static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t s
 }
 
 int mtsg_path_features(const MtsgLaunch &L) {
-    return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | (L.ext ? MTSG_FEAT_EXT : 0);
+    return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | ((L.ext || L.ana) ? MTSG_FEAT_EXT : 0) |
+           (L.ana ? MTSG_FEAT_ANA : 0);
 }
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
@@ -1107,7 +1168,9 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
         case 0: launch_path<0>(L, grid, instr, stream); break;
         case MTSG_FEAT_ENV: launch_path<MTSG_FEAT_ENV>(L, grid, instr, stream); break;
         case MTSG_FEAT_EXT: launch_path<MTSG_FEAT_EXT>(L, grid, instr, stream); break;
-        default: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, instr, stream); break;
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, instr, stream); break;
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: launch_path<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, instr, stream); break;
+        default: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, instr, stream); break;
     }
     return hipGetLastError();
 }
@@ -1130,16 +1193,16 @@ hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32
                              uint32_t stackDepth, int numCUs, hipStream_t stream) {
     const size_t lds = (size_t)stackDepth * 3 * BLOCK / 2 * 4 + 16;
     int bpc = 1;
-    if (shadow) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<true, 8>, BLOCK, lds);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<false, 8>, BLOCK, lds);
+    if (shadow) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<true, 8, false>, BLOCK, lds);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, trace_kernel<false, 8, false>, BLOCK, lds);
     const uint32_t want = (n + BLOCK - 1) / BLOCK;
     const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(want, (uint32_t)(std::max(bpc, 1) * numCUs)));
-    if (shadow)
-        hipLaunchKernelGGL((trace_kernel<true, 8>), dim3(grid), dim3(BLOCK), lds, stream, S, (const float4 *)rays, n,
-                           (float4 *)out, stackDepth);
-    else
-        hipLaunchKernelGGL((trace_kernel<false, 8>), dim3(grid), dim3(BLOCK), lds, stream, S, (const float4 *)rays, n,
-                           (float4 *)out, stackDepth);
+    const bool ana = S.analytic != nullptr;
+#define MTSG_TRACE(A, N) hipLaunchKernelGGL((trace_kernel<A, 8, N>), dim3(grid), dim3(BLOCK), lds, stream, S, \
+                                            (const float4 *)rays, n, (float4 *)out, stackDepth)
+    if (shadow) { if (ana) MTSG_TRACE(true, true); else MTSG_TRACE(true, false); }
+    else { if (ana) MTSG_TRACE(false, true); else MTSG_TRACE(false, false); }
+#undef MTSG_TRACE
     return hipGetLastError();
 }
 
@@ -1164,6 +1227,8 @@ int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
         case 0: return occupancy_e<0>(L, blocksPerCU);
         case MTSG_FEAT_ENV: return occupancy_e<MTSG_FEAT_ENV>(L, blocksPerCU);
         case MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_EXT>(L, blocksPerCU);
-        default: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, blocksPerCU);
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, blocksPerCU);
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: return occupancy_e<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, blocksPerCU);
+        default: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, blocksPerCU);
     }
 }

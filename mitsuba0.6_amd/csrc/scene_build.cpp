@@ -115,6 +115,94 @@ V xf_point(const M4 &m, V p) {
     return vdiv(v(x, y, z), w);
 }
 
+V xf_vec(const M4 &m, V a) {          // Transform::operator()(const Vector &) (transform.h:175-183)
+    return v(m.m[0][0] * a.x + m.m[0][1] * a.y + m.m[0][2] * a.z, m.m[1][0] * a.x + m.m[1][1] * a.y + m.m[1][2] * a.z,
+             m.m[2][0] * a.x + m.m[2][1] * a.y + m.m[2][2] * a.z);
+}
+V xf_normal(const M4 &inv, V a) {     // Transform::operator()(const Normal &) (transform.h:203-211)
+    return v(inv.m[0][0] * a.x + inv.m[1][0] * a.y + inv.m[2][0] * a.z,
+             inv.m[0][1] * a.x + inv.m[1][1] * a.y + inv.m[2][1] * a.z,
+             inv.m[0][2] * a.x + inv.m[1][2] * a.y + inv.m[2][2] * a.z);
+}
+void put3(float *d, V a) { d[0] = a.x; d[1] = a.y; d[2] = a.z; }
+void put16(float *d, const M4 &m) { std::memcpy(d, &m.m[0][0], 16 * sizeof(float)); }
+
+// 'toWorld' of a shape desc as the reference's Transform (matrix + carried inverse)
+int desc_transform(const float *t16, const float *inv16, Xf &out, std::string &err) {
+    std::memcpy(&out.t.m[0][0], t16, 16 * sizeof(float));
+    bool haveInv = false;
+    for (int i = 0; i < 16; ++i) haveInv |= inv16[i] != 0.0f;
+    if (haveInv) std::memcpy(&out.inv.m[0][0], inv16, 16 * sizeof(float));
+    else if (!invert(out.t, out.inv)) { err = "Singular matrix in Matrix::invert"; return MTSGPU_EINVAL; }
+    return MTSGPU_OK;
+}
+
+// Rectangle / Disk / Sphere constructors + configure() (rectangle.cpp:80-119,
+// disk.cpp:83-130, sphere.cpp:108-133) and getAABB()
+int configure_analytic(const mtsgpu_mesh_desc &m, MtsgAnalytic &a, float lo[3], float hi[3], std::string &err) {
+    std::memset(&a, 0, sizeof a);
+    a.type = m.shape_type;
+    Xf o2w;
+    int rc;
+    auto grow = [&](V p) {
+        const float q[3] = {p.x, p.y, p.z};
+        for (int i = 0; i < 3; ++i) { lo[i] = std::min(lo[i], q[i]); hi[i] = std::max(hi[i], q[i]); }
+    };
+    for (int i = 0; i < 3; ++i) { lo[i] = FLT_MAX; hi[i] = -FLT_MAX; }
+    if (m.shape_type == MTSGPU_SHAPE_RECTANGLE || m.shape_type == MTSGPU_SHAPE_DISK) {
+        if ((rc = desc_transform(m.to_world, m.to_world_inv, o2w, err))) return rc;
+        if (m.flip_normals) o2w = compose(o2w, scale(1, 1, -1));   // (prependScale: m_transform * scale)
+        if (m.shape_type == MTSGPU_SHAPE_RECTANGLE) {
+            const V dpdu = xf_vec(o2w.t, v(2, 0, 0)), dpdv = xf_vec(o2w.t, v(0, 2, 0));
+            const V n = normalize(xf_normal(o2w.inv, v(0, 0, 1)));
+            put3(a.dpdu, dpdu); put3(a.dpdv, dpdv); put3(a.n, n);
+            put3(a.fs, normalize(dpdu)); put3(a.ft, normalize(dpdv));
+            a.inv_area = 1.0f / (length(dpdu) * length(dpdv));
+            if (std::fabs(dot(normalize(dpdu), normalize(dpdv))) > 1e-4f) {
+                err = "Error: 'toWorld' transformation contains shear!"; return MTSGPU_EINVAL;
+            }
+            grow(xf_point(o2w.t, v(-1, -1, 0))); grow(xf_point(o2w.t, v(1, -1, 0)));
+            grow(xf_point(o2w.t, v(1, 1, 0))); grow(xf_point(o2w.t, v(-1, 1, 0)));
+        } else {
+            const V dpdu = xf_vec(o2w.t, v(1, 0, 0)), dpdv = xf_vec(o2w.t, v(0, 1, 0));
+            if (std::fabs(dot(normalize(dpdu), normalize(dpdv))) > 1e-3f) {
+                err = "Error: 'toWorld' transformation contains shear!"; return MTSGPU_EINVAL;
+            }
+            if (std::fabs(length(dpdu) / length(dpdv) - 1) > 1e-3f) {
+                err = "Error: 'toWorld' transformation contains a non-uniform scale!"; return MTSGPU_EINVAL;
+            }
+            a.inv_area = 1.0f / (kPi * length(dpdu) * length(dpdu));
+            put3(a.n, normalize(xf_normal(o2w.inv, v(0, 0, 1))));
+            grow(xf_point(o2w.t, v(1, 0, 0))); grow(xf_point(o2w.t, v(-1, 0, 0)));
+            grow(xf_point(o2w.t, v(0, 1, 0))); grow(xf_point(o2w.t, v(0, -1, 0)));
+        }
+    } else if (m.shape_type == MTSGPU_SHAPE_SPHERE) {
+        o2w = translate(m.center[0], m.center[1], m.center[2]);
+        float radius = m.radius;
+        if (m.has_to_world) {
+            Xf T;
+            if ((rc = desc_transform(m.to_world, m.to_world_inv, T, err))) return rc;
+            const float r = length(xf_vec(T.t, v(1, 0, 0)));
+            const float ir = 1 / r;
+            o2w = compose(compose(T, scale(ir, ir, ir)), o2w);
+            radius *= r;
+        }
+        a.flip = m.flip_normals ? 1 : 0;
+        const V c = xf_point(o2w.t, v(0, 0, 0));
+        put3(a.center, c);
+        a.radius = radius;
+        a.inv_area = 1 / (4 * kPi * radius * radius);
+        if (radius <= 0) { err = "Cannot create spheres of radius <= 0"; return MTSGPU_EINVAL; }
+        grow(c - v(radius, radius, radius));
+        grow(c + v(radius, radius, radius));
+    } else {
+        err = "unsupported shape type"; return MTSGPU_EINVAL;
+    }
+    put16(a.to_world, o2w.t);
+    put16(a.to_obj, o2w.inv);
+    return MTSGPU_OK;
+}
+
 int configure_camera(const mtsgpu_sensor_desc &s, MtsgCamera &cam, std::string &err) {
     if (s.film_width == 0 || s.film_height == 0) { err = "film size must be positive"; return MTSGPU_EINVAL; }
     const float aspect = (float)s.film_width / (float)s.film_height;
@@ -964,6 +1052,8 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
         const MtsgBsdf &b = S.bsdfs[i];
         if (b.type >= MTSGPU_BSDF_ROUGHPLASTIC || b.refl_tex.type || b.alpha_tex.type) S.ext = true;
     }
+    for (uint32_t i = 0; i < D->num_meshes; ++i)   // analytic shapes run the EXT | ANA variant
+        if (D->meshes[i].shape_type != MTSGPU_SHAPE_TRIMESH) S.ext = true;
     {   // Shape::configure defaults (shape.cpp:48-70): black for emitters, 0.5 otherwise
         mtsgpu_bsdf_desc dd; std::memset(&dd, 0, sizeof dd);
         dd.type = MTSGPU_BSDF_DIFFUSE; dd.ensure_energy_conservation = 1;
@@ -996,6 +1086,7 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     uint32_t prims = 0, verts = 0;
     for (uint32_t i = 0; i < D->num_meshes; ++i) {
         const mtsgpu_mesh_desc &m = D->meshes[i];
+        if (m.shape_type != MTSGPU_SHAPE_TRIMESH) { prims += 1; continue; }
         if (m.num_triangles == 0 || !m.positions || !m.indices) { err = "Encountered an empty triangle mesh!"; return MTSGPU_EINVAL; }
         prims += m.num_triangles; verts += m.num_vertices;
     }
@@ -1010,6 +1101,51 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     uint32_t voff = 0, poff = 0;
     for (uint32_t si = 0; si < D->num_meshes; ++si) {
         const mtsgpu_mesh_desc &m = D->meshes[si];
+        if (m.shape_type != MTSGPU_SHAPE_TRIMESH) {
+            // one analytic primitive (ShapeKDTree: k = KNoTriangleFlag, skdtree.cpp:74-109)
+            MtsgShape &sh = S.shapes[si];
+            std::memset(&sh, 0, sizeof sh);
+            if (m.emitter >= (int)D->num_emitters) { err = "emitter index out of range"; return MTSGPU_EINVAL; }
+            if (m.bsdf >= (int)nb) { err = "bsdf index out of range"; return MTSGPU_EINVAL; }
+            sh.emitter = m.emitter;
+            sh.bsdf = m.bsdf >= 0 ? m.bsdf : (m.emitter >= 0 ? (int)nb : (int)nb + 1);
+            sh.kind = m.shape_type;
+            sh.has_uv = 1;
+            sh.analytic = (int32_t)S.analytic.size();
+            MtsgAnalytic a;
+            float lo[3], hi[3];
+            if ((rc = configure_analytic(m, a, lo, hi, err))) return rc;
+            S.analytic.push_back(a);
+            const uint32_t p = poff;
+            S.prim_vtx[4 * p] = S.prim_vtx[4 * p + 1] = S.prim_vtx[4 * p + 2] = 0;
+            S.prim_vtx[4 * p + 3] = si;
+            S.dpdu[3 * p] = S.dpdu[3 * p + 1] = S.dpdu[3 * p + 2] = 0.0f;
+            MtsgTri &ta = tacc[p];
+            std::memset(&ta, 0, sizeof ta);
+            ta.k = MTSG_K_ANALYTIC;
+            std::memcpy(&ta.n_u, &sh.analytic, sizeof(float));
+            ta.prim = p;
+            ta.shape = si;
+            BuildPrim &q = bp[p];
+            q.id = p;
+            for (int ax = 0; ax < 3; ++ax) {
+                q.box.lo[ax] = lo[ax]; q.box.hi[ax] = hi[ax];
+                q.c[ax] = 0.5f * (lo[ax] + hi[ax]);
+                amin[ax] = std::min(amin[ax], lo[ax]);
+                amax[ax] = std::max(amax[ax], hi[ax]);
+            }
+            if (m.emitter >= 0) {
+                MtsgEmitter &e = S.emitters[m.emitter];
+                if (e.shape >= 0) { err = "Tried to attach multiple emitters to a shape!"; return MTSGPU_EINVAL; }
+                e.shape = (int)si;
+                e.tri_first = p;
+                e.tri_count = 1;
+                e.cdf_offset = 0;
+                e.inv_area = a.inv_area;
+            }
+            poff += 1;
+            continue;
+        }
         const uint32_t nv = m.num_vertices, nt = m.num_triangles;
         std::vector<V> P(nv), N;
         for (uint32_t k = 0; k < nv; ++k) P[k] = v(m.positions[3 * k], m.positions[3 * k + 1], m.positions[3 * k + 2]);
@@ -1018,6 +1154,8 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
             if (idx[k] >= nv) { err = "triangle index out of range"; return MTSGPU_EINVAL; }
         MtsgShape &sh = S.shapes[si];
         sh.emitter = m.emitter;
+        sh.kind = MTSGPU_SHAPE_TRIMESH;
+        sh.analytic = -1;
         if (m.emitter >= (int)D->num_emitters) { err = "emitter index out of range"; return MTSGPU_EINVAL; }
         if (m.bsdf >= (int)nb) { err = "bsdf index out of range"; return MTSGPU_EINVAL; }
         sh.bsdf = m.bsdf >= 0 ? m.bsdf : (m.emitter >= 0 ? (int)nb : (int)nb + 1);

@@ -45,6 +45,7 @@ struct HostScene {
     // roughplastic tables (MtsgBsdf::rt_ext / rt_int offsets) and per-vertex UVs
     std::vector<float> rtrans, texcoords;
     bool ext = false;   // roughplastic or textured BSDFs: the MTSG_FEAT_EXT kernel variant
+    std::vector<MtsgAnalytic> analytic;   // rectangle / disk / sphere records (MTSG_FEAT_ANA variant)
 };
 
 // Returns MTSGPU_OK or an error code; `err` receives the message.

@@ -185,8 +185,12 @@ class Emitter:
 
 @dataclass
 class Mesh:
-    positions: np.ndarray                 # (n,3) float32, world space
-    indices: np.ndarray                   # (m,3) uint32
+    """A shape: a world-space triangle mesh (obj/ply/serialized/cube) or, with
+    `shape` = 'rectangle' / 'disk' / 'sphere', an analytic shape intersected
+    exactly (src/shapes/{rectangle,disk,sphere}.cpp) -- then positions/indices
+    are None and toWorld (+ its carried inverse), center and radius apply."""
+    positions: Optional[np.ndarray] = None   # (n,3) float32, world space
+    indices: Optional[np.ndarray] = None     # (m,3) uint32
     normals: Optional[np.ndarray] = None
     texcoords: Optional[np.ndarray] = None
     bsdf: int = -1
@@ -194,6 +198,15 @@ class Mesh:
     faceNormals: bool = False
     flipNormals: bool = False
     name: str = ''
+    shape: str = 'trimesh'
+    toWorld: object = None                   # 'toWorld': transform.Transform or 4x4 (rectangle / disk / sphere)
+    toWorldInv: Optional[np.ndarray] = None  # its inverse as the reference's Transform carries it
+    center: tuple = (0.0, 0.0, 0.0)          # sphere
+    radius: float = 1.0                      # sphere
+
+    @property
+    def analytic(self):
+        return self.shape != 'trimesh'
 
 
 @dataclass
@@ -238,13 +251,32 @@ class Scene:
 
     @property
     def num_triangles(self):
-        return sum(int(m.indices.shape[0]) for m in self.meshes)
+        """Primitives of the acceleration structure (an analytic shape counts one)."""
+        return sum(1 if m.analytic else int(m.indices.shape[0]) for m in self.meshes)
 
     def desc(self):
         """Pack into abi.SceneDesc; the returned object keeps every buffer alive."""
         keep = []
         md = (abi.MeshDesc * len(self.meshes))()
         for i, m in enumerate(self.meshes):
+            if m.analytic:
+                md[i].shape_type = {'rectangle': abi.SHAPE_RECTANGLE, 'disk': abi.SHAPE_DISK,
+                                    'sphere': abi.SHAPE_SPHERE}[m.shape]
+                md[i].bsdf, md[i].emitter = m.bsdf, m.emitter
+                md[i].flip_normals = int(m.flipNormals)
+                md[i].has_to_world = int(m.toWorld is not None)
+                tw, twi = m.toWorld, m.toWorldInv
+                if hasattr(tw, 'inv'):           # a transform.Transform: matrix + carried inverse
+                    tw, twi = tw.m, tw.inv
+                T = np.eye(4, dtype=np.float32) if tw is None else np.asarray(tw, np.float32)
+                md[i].to_world[:] = [float(x) for x in T.reshape(-1)]
+                if twi is not None:
+                    md[i].to_world_inv[:] = [float(x) for x in np.asarray(twi, np.float32).reshape(-1)]
+                elif tw is None:
+                    md[i].to_world_inv[:] = [float(x) for x in T.reshape(-1)]
+                md[i].center[:] = [float(x) for x in m.center]
+                md[i].radius = float(m.radius)
+                continue
             pos = np.ascontiguousarray(m.positions, np.float32)
             idx = np.ascontiguousarray(m.indices, np.uint32)
             nrm = None if m.normals is None else np.ascontiguousarray(m.normals, np.float32)

@@ -136,6 +136,8 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
         base = len(bsdfs)
         bsdfs += plastic_materials()
         floor_b, short_b, tall_b, back_b = base + 4, base + 1, base + 0, base + 5
+    if materials == 'shapes':
+        return _cornell_shapes(width, height, spp, rfilter, max_depth)
     green_b, flip_back = 2, False
     if materials == 'smooth':
         # the back wall shows its back side (flipped normals) through twosided
@@ -160,6 +162,36 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
     integ = PathIntegrator(maxDepth=max_depth, rrDepth=5, sampleCount=spp, rfilter=rfilter,
                            rfilterParam=0.5)
     return scene, integ
+
+
+def _cornell_shapes(width, height, spp, rfilter, max_depth):
+    """The Cornell room with analytic shapes (rectangle.cpp, disk.cpp, sphere.cpp):
+    a rectangle area light in place of the light quad, a gold sphere and a glass
+    sphere in place of the blocks, a small emitting sphere (cone sampling), a
+    disk on the floor and a flipped, twosided mirror rectangle on the green wall."""
+    sc, integ = cornell_box(width, height, spp, rfilter, max_depth)
+    walls = sc.meshes[:5]
+    bsdfs = sc.bsdfs + [
+        BSDF('roughconductor', distribution='ggx', alpha=0.15, material='Au'),
+        BSDF('dielectric', intIOR=1.5),
+        BSDF('diffuse', reflectance=(0.2, 0.6, 0.8)),
+        BSDF('twosided', nested=[BSDF('conductor', material='none', specularReflectance=0.9)]),
+    ]
+    gold, glass, blue, mirror = 3, 4, 5, 6
+    T = Transform
+    light = T().scale(65 * S, 52.5 * S, 1).rotate((1, 0, 0), 90).translate(278 * S, 548.7 * S, 279.5 * S)
+    disk = T().scale(0.6).rotate((1, 0, 0), -90).translate(450 * S, 1 * S, 120 * S)
+    mir = T().scale(1.2, 1.0, 1).rotate((0, 1, 0), 90).translate(1 * S, 2.5, 3.2)
+    meshes = walls + [
+        Mesh(shape='rectangle', toWorld=light, bsdf=-1, emitter=0),
+        Mesh(shape='sphere', center=(370 * S, 90 * S, 350 * S), radius=0.9, bsdf=gold),
+        Mesh(shape='sphere', center=(185 * S, 80 * S, 170 * S), radius=0.8, bsdf=glass),
+        Mesh(shape='sphere', toWorld=T().scale(0.3).translate(1.5, 4.0, 4.0), bsdf=-1, emitter=1),
+        Mesh(shape='disk', toWorld=disk, bsdf=blue),
+        Mesh(shape='rectangle', toWorld=mir, flipNormals=True, bsdf=mirror),
+    ]
+    emitters = [Emitter('area', radiance=(17.0, 12.0, 4.0)), Emitter('area', radiance=(4.0, 4.0, 8.0))]
+    return Scene(sc.sensor, meshes, bsdfs, emitters, name='cornell-shapes'), integ
 
 
 def procedural_envmap(width=1024, height=512, seed=0x5EED):

@@ -359,9 +359,15 @@ class XMLSceneLoader:
                                        faceNormals=fn, flipNormals=flip), '', None)]
         elif t == 'cube':
             meshes = [(cube_mesh(tw, flip), '', None)]
+        elif t in ('rectangle', 'disk'):            # rectangle.cpp:80-85, disk.cpp:83-88
+            meshes = [(Mesh(shape=t, toWorld=tw, flipNormals=flip), '', None)]
+        elif t == 'sphere':                          # sphere.cpp:108-130
+            c = p.get('center', (0.0, 0.0, 0.0))
+            meshes = [(Mesh(shape='sphere', center=tuple(float(x) for x in c), radius=float(p.get('radius', 1.0)),
+                            toWorld=tw, flipNormals=flip), '', None)]
         else:
-            raise NotImplementedError('shape plugin "%s": the GPU path intersects triangle meshes (obj, ply, '
-                                      'serialized, cube); analytic shapes are not supported' % t)
+            raise NotImplementedError('shape plugin "%s": the GPU path has obj, ply, serialized, cube, '
+                                      'rectangle, disk and sphere' % t)
         return meshes
 
     # -- scene --------------------------------------------------------------------
@@ -696,11 +702,20 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     for i, b in enumerate(scene.bsdfs):
         L += _bsdf_xml(b, '  ', 'bsdf%d' % i)
     for i, m in enumerate(scene.meshes):
-        fn = 'mesh%03d.ply' % i
-        write_ply(os.path.join(directory, fn), m)
-        L.append('  <shape type="ply">')
-        L.append('    <string name="filename" value="%s"/>' % fn)
-        L.append('    <boolean name="faceNormals" value="%s"/>' % str(bool(m.faceNormals)).lower())
+        if m.analytic:
+            L.append('  <shape type="%s">' % m.shape)
+            if m.shape == 'sphere':
+                L.append('    <point name="center" x="%s" y="%s" z="%s"/>' % tuple(_fmt(x) for x in m.center))
+                L.append('    <float name="radius" value="%s"/>' % _fmt(m.radius))
+            if m.toWorld is not None:
+                t = m.toWorld if hasattr(m.toWorld, 'inv') else Transform(m.toWorld, m.toWorldInv)
+                L.append('    <transform name="toWorld">%s</transform>' % _transform_xml(t))
+        else:
+            fn = 'mesh%03d.ply' % i
+            write_ply(os.path.join(directory, fn), m)
+            L.append('  <shape type="ply">')
+            L.append('    <string name="filename" value="%s"/>' % fn)
+            L.append('    <boolean name="faceNormals" value="%s"/>' % str(bool(m.faceNormals)).lower())
         L.append('    <boolean name="flipNormals" value="%s"/>' % str(bool(m.flipNormals)).lower())
         if m.bsdf >= 0:
             L.append('    <ref id="bsdf%d"/>' % m.bsdf)

@@ -1645,6 +1645,278 @@ static inline int triaccel_intersect(const TriAccel *ta, const Ray *ray, float m
 }
 
 /* ------------------------------------------------------------------------ */
+/* analytic shapes: rectangle.cpp, disk.cpp, sphere.cpp                      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    int type, flip;
+    Xform o2w;            /* m_objectToWorld with its carried inverse (m_worldToObject) */
+    V3 center, n, fs, ft, dpdu, dpdv;
+    float radius, invArea;
+    float bmin[3], bmax[3];  /* getAABB() */
+} Ana;
+
+static V3 xf_normal(const M4 *inv, V3 v) { /* Transform::operator()(Normal) (transform.h:203-211) */
+    return v3(inv->m[0][0] * v.x + inv->m[1][0] * v.y + inv->m[2][0] * v.z,
+              inv->m[0][1] * v.x + inv->m[1][1] * v.y + inv->m[2][1] * v.z,
+              inv->m[0][2] * v.x + inv->m[1][2] * v.y + inv->m[2][2] * v.z);
+}
+static void ana_grow(Ana *a, V3 p) {
+    for (int i = 0; i < 3; ++i) {
+        float x = vget(p, i);
+        if (x < a->bmin[i]) a->bmin[i] = x;
+        if (x > a->bmax[i]) a->bmax[i] = x;
+    }
+}
+static int desc_xform(const float *t16, const float *inv16, Xform *out) {
+    memcpy(&out->t.m[0][0], t16, 16 * sizeof(float));
+    int have = 0;
+    for (int i = 0; i < 16; ++i) have |= inv16[i] != 0.0f;
+    if (have) { memcpy(&out->inv.m[0][0], inv16, 16 * sizeof(float)); return MTSGPU_OK; }
+    return m4_invert(&out->t, &out->inv) ? MTSGPU_OK : MTSGPU_EINVAL;
+}
+
+/* constructors + configure() + getAABB() (rectangle.cpp:80-119, disk.cpp:83-130, sphere.cpp:108-157) */
+static int ana_configure(const mtsgpu_mesh_desc *md, Ana *a) {
+    memset(a, 0, sizeof *a);
+    a->type = md->shape_type;
+    for (int i = 0; i < 3; ++i) { a->bmin[i] = FLT_MAX; a->bmax[i] = -FLT_MAX; }
+    if (md->shape_type == MTSGPU_SHAPE_RECTANGLE || md->shape_type == MTSGPU_SHAPE_DISK) {
+        if (desc_xform(md->to_world, md->to_world_inv, &a->o2w)) return MTSGPU_EINVAL;
+        if (md->flip_normals) { Xform sc = xf_scale(1, 1, -1); a->o2w = xf_compose(&a->o2w, &sc); }
+        const M4 *T = &a->o2w.t;
+        if (md->shape_type == MTSGPU_SHAPE_RECTANGLE) {
+            a->dpdu = xf_vector(T, v3(2, 0, 0));
+            a->dpdv = xf_vector(T, v3(0, 2, 0));
+            a->n = vnormalize(xf_normal(&a->o2w.inv, v3(0, 0, 1)));
+            a->fs = vnormalize(a->dpdu);
+            a->ft = vnormalize(a->dpdv);
+            a->invArea = 1.0f / (vlen(a->dpdu) * vlen(a->dpdv));
+            if (fabsf(vdot(vnormalize(a->dpdu), vnormalize(a->dpdv))) > EPSILON) return MTSGPU_EINVAL; /* shear */
+            ana_grow(a, xf_point(T, v3(-1, -1, 0))); ana_grow(a, xf_point(T, v3(1, -1, 0)));
+            ana_grow(a, xf_point(T, v3(1, 1, 0))); ana_grow(a, xf_point(T, v3(-1, 1, 0)));
+        } else {
+            V3 dpdu = xf_vector(T, v3(1, 0, 0)), dpdv = xf_vector(T, v3(0, 1, 0));
+            if (fabsf(vdot(vnormalize(dpdu), vnormalize(dpdv))) > 1e-3f) return MTSGPU_EINVAL;
+            if (fabsf(vlen(dpdu) / vlen(dpdv) - 1) > 1e-3f) return MTSGPU_EINVAL;
+            a->invArea = 1.0f / (M_PI_F * vlen(dpdu) * vlen(dpdu));
+            a->n = vnormalize(xf_normal(&a->o2w.inv, v3(0, 0, 1)));
+            ana_grow(a, xf_point(T, v3(1, 0, 0))); ana_grow(a, xf_point(T, v3(-1, 0, 0)));
+            ana_grow(a, xf_point(T, v3(0, 1, 0))); ana_grow(a, xf_point(T, v3(0, -1, 0)));
+        }
+        return MTSGPU_OK;
+    }
+    if (md->shape_type != MTSGPU_SHAPE_SPHERE) return MTSGPU_EINVAL;
+    a->o2w = xf_translate(md->center[0], md->center[1], md->center[2]);
+    float radius = md->radius;
+    if (md->has_to_world) {
+        Xform T;
+        if (desc_xform(md->to_world, md->to_world_inv, &T)) return MTSGPU_EINVAL;
+        float r = vlen(xf_vector(&T.t, v3(1, 0, 0)));
+        float ir = 1 / r;
+        Xform sc = xf_scale(ir, ir, ir);
+        Xform ts = xf_compose(&T, &sc);
+        a->o2w = xf_compose(&ts, &a->o2w);
+        radius *= r;
+    }
+    a->flip = md->flip_normals != 0;
+    a->center = xf_point(&a->o2w.t, v3(0, 0, 0));
+    a->radius = radius;
+    a->invArea = 1 / (4 * M_PI_F * radius * radius);
+    if (radius <= 0) return MTSGPU_EINVAL;
+    ana_grow(a, vsub(a->center, v3(radius, radius, radius)));
+    ana_grow(a, vadd(a->center, v3(radius, radius, radius)));
+    return MTSGPU_OK;
+}
+
+/* solveQuadraticDouble / solveQuadratic (util.cpp:447-525) */
+static int solve_quadratic_d(double a, double b, double c, double *x0, double *x1) {
+    if (a == 0) {
+        if (b != 0) { *x0 = *x1 = -c / b; return 1; }
+        return 0;
+    }
+    double discrim = b * b - 4.0f * a * c;
+    if (discrim < 0) return 0;
+    double temp, sqrtDiscrim = sqrt(discrim);
+    if (b < 0) temp = -0.5f * (b - sqrtDiscrim);
+    else temp = -0.5f * (b + sqrtDiscrim);
+    *x0 = temp / a;
+    *x1 = c / temp;
+    if (*x0 > *x1) { double t = *x0; *x0 = *x1; *x1 = t; }
+    return 1;
+}
+static int solve_quadratic_f(float a, float b, float c, float *x0, float *x1) {
+    if (a == 0) {
+        if (b != 0) { *x0 = *x1 = -c / b; return 1; }
+        return 0;
+    }
+    float discrim = b * b - 4.0f * a * c;
+    if (discrim < 0) return 0;
+    float temp, sqrtDiscrim = sqrtf(discrim);
+    if (b < 0) temp = -0.5f * (b - sqrtDiscrim);
+    else temp = -0.5f * (b + sqrtDiscrim);
+    *x0 = temp / a;
+    *x1 = c / temp;
+    if (*x0 > *x1) { float t = *x0; *x0 = *x1; *x1 = t; }
+    return 1;
+}
+
+/* Shape::rayIntersect(ray, mint, maxt, t, temp) (rectangle.cpp:125-148, disk.cpp:139-162,
+ * sphere.cpp:163-187); shadow = the (ray, mint, maxt) overload (sphere.cpp:189-207).
+ * (*lx, *ly) = the object-space hit kept in `temp` by rectangle/disk */
+static int ana_intersect(const Ana *a, const Ray *ray, float mint, float maxt, int shadow,
+                         float *t, float *lx, float *ly) {
+    if (a->type == MTSGPU_SHAPE_SPHERE) {
+        double ox = (double)ray->o.x - (double)a->center.x, oy = (double)ray->o.y - (double)a->center.y,
+               oz = (double)ray->o.z - (double)a->center.z;
+        double dx = ray->d.x, dy = ray->d.y, dz = ray->d.z;
+        double A = dx * dx + dy * dy + dz * dz;
+        double B = 2 * (ox * dx + oy * dy + oz * dz);
+        double C = (ox * ox + oy * oy + oz * oz) - a->radius * a->radius;
+        double nearT, farT;
+        if (!solve_quadratic_d(A, B, C, &nearT, &farT)) return 0;
+        if (shadow) {
+            if (nearT > maxt || farT < mint) return 0;
+            if (nearT < mint && farT > maxt) return 0;
+            return 1;
+        }
+        if (!(nearT <= maxt && farT >= mint)) return 0;
+        if (nearT < mint) {
+            if (farT > maxt) return 0;
+            *t = (float)farT;
+        } else {
+            *t = (float)nearT;
+        }
+        *lx = *ly = 0.0f;
+        return 1;
+    }
+    /* m_worldToObject.transformAffine(_ray, ray) (transform.h:292-307) */
+    V3 o = xf_point_affine(&a->o2w.inv, ray->o), d = xf_vector(&a->o2w.inv, ray->d);
+    float hit = -o.z / d.z;
+    if (!(hit >= mint && hit <= maxt)) return 0;
+    float px = o.x + d.x * hit, py = o.y + d.y * hit;
+    if (a->type == MTSGPU_SHAPE_RECTANGLE) { if (!(fabsf(px) <= 1 && fabsf(py) <= 1)) return 0; }
+    else if (!(px * px + py * py <= 1)) return 0;
+    *t = hit; *lx = px; *ly = py;
+    return 1;
+}
+
+/* fillIntersectionRecord (rectangle.cpp:155-167, disk.cpp:169-200, sphere.cpp:209-255):
+ * p, geometric normal, shading normal (before computeShadingFrame), dpdu, uv.  The
+ * disk sets only shFrame.n and leaves geoFrame as the record held it: the
+ * oracle (like the product) uses the shading normal there. */
+static void ana_fill(const Ana *a, const Ray *ray, float t, float lx, float ly,
+                     V3 *p, V3 *geoN, V3 *shN, V3 *dpdu, float *u, float *v) {
+    *p = vadd(ray->o, vmul(ray->d, t));
+    if (a->type == MTSGPU_SHAPE_RECTANGLE) {
+        *geoN = *shN = a->n;
+        *dpdu = a->dpdu;
+        *u = 0.5f * (lx + 1); *v = 0.5f * (ly + 1);
+    } else if (a->type == MTSGPU_SHAPE_DISK) {
+        float r = sqrtf(lx * lx + ly * ly), invR = (r == 0) ? 0.0f : (1.0f / r);
+        float phi = o_atan2(ly, lx);
+        if (phi < 0) phi += 2 * M_PI_F;
+        float cosPhi = lx * invR, sinPhi = ly * invR;
+        *dpdu = r != 0 ? xf_vector(&a->o2w.t, v3(cosPhi, sinPhi, 0)) : xf_vector(&a->o2w.t, v3(1, 0, 0));
+        *geoN = *shN = a->n;
+        *u = r; *v = phi * INV_TWOPI_F;
+    } else {
+        *p = vadd(a->center, vmul(vnormalize(vsub(*p, a->center)), a->radius));
+        V3 local = xf_vector(&a->o2w.inv, vsub(*p, a->center));
+        float theta = o_acos(smin(1.0f, smax(-1.0f, local.z / a->radius))); /* math::safe_acos */
+        float phi = o_atan2(local.y, local.x);
+        if (phi < 0) phi += 2 * M_PI_F;
+        *u = phi * (0.5f * INV_PI_F);
+        *v = theta * INV_PI_F;
+        float tp = 2 * M_PI_F;
+        *dpdu = xf_vector(&a->o2w.t, v3(-local.y * tp, local.x * tp, 0 * tp));
+        V3 n = vnormalize(vsub(*p, a->center));
+        if (a->flip) n = vmul(n, -1.0f);
+        *geoN = *shN = n;
+    }
+}
+
+/* m_shape->sampleDirect(dRec, sample) of an analytic area light: samplePosition
+ * (rectangle.cpp:210-216, disk.cpp:247-255) + Shape::sampleDirect (shape.cpp:102-115),
+ * or Sphere::sampleDirect (sphere.cpp:286-355) */
+static void ana_sample_direct(const Ana *a, V3 ref, float sx, float sy, V3 *p, V3 *n, V3 *d, float *dist, float *pdf) {
+    if (a->type == MTSGPU_SHAPE_SPHERE) {
+        V3 refToCenter = vsub(a->center, ref);
+        float refDist2 = vlen2(refToCenter);
+        float invRefDist = (float)1 / sqrtf(refDist2);
+        float sinAlpha = a->radius * invRefDist;
+        if (sinAlpha < 1 - EPSILON) {
+            float cosAlpha = safe_sqrt(1.0f - sinAlpha * sinAlpha);
+            Frame F;
+            F.n = vmul(refToCenter, invRefDist);
+            coordinate_system(F.n, &F.s, &F.t);
+            float cosTheta = (1 - sx) + sx * cosAlpha; /* warp::squareToUniformCone (warp.cpp:54-63) */
+            float sinTheta = safe_sqrt(1.0f - cosTheta * cosTheta);
+            float sinPhi, cosPhi;
+            o_sincos(2.0f * M_PI_F * sy, &sinPhi, &cosPhi);
+            *d = to_world(&F, v3(cosPhi * sinTheta, sinPhi * sinTheta, cosTheta));
+            *pdf = INV_TWOPI_F / (1 - cosAlpha);
+            float projDist = vdot(refToCenter, *d);
+            float baseT = refDist2 / projDist;
+            V3 query = vadd(ref, vmul(*d, baseT));
+            V3 queryToCenter = vsub(a->center, query);
+            float queryDist2 = vlen2(queryToCenter);
+            float queryProjDist = vdot(queryToCenter, *d);
+            float A = 1.0f, B = -2 * queryProjDist, C = queryDist2 - a->radius * a->radius;
+            float nearT, farT;
+            if (!solve_quadratic_f(A, B, C, &nearT, &farT)) nearT = queryProjDist;
+            *dist = baseT + nearT;
+            *n = vnormalize(vsub(vmul(*d, nearT), queryToCenter));
+            *p = vadd(a->center, vmul(*n, a->radius));
+        } else {
+            float z = 1.0f - 2.0f * sy; /* warp::squareToUniformSphere (warp.cpp:25-31) */
+            float r = safe_sqrt(1.0f - z * z);
+            float sinPhi, cosPhi;
+            o_sincos(2.0f * M_PI_F * sx, &sinPhi, &cosPhi);
+            V3 dv = v3(r * cosPhi, r * sinPhi, z);
+            *p = vadd(a->center, vmul(dv, a->radius));
+            *n = dv;
+            *d = vsub(*p, ref);
+            float dist2 = vlen2(*d);
+            *dist = sqrtf(dist2);
+            *d = vdiv(*d, *dist);
+            *pdf = a->invArea * dist2 / vabsdot(*d, *n);
+        }
+        if (a->flip) *n = vmul(*n, -1.0f);
+        return;
+    }
+    if (a->type == MTSGPU_SHAPE_RECTANGLE) {
+        *p = xf_point(&a->o2w.t, v3(sx * 2 - 1, sy * 2 - 1, 0));
+    } else {
+        float px, py;
+        square_to_disk_concentric(sx, sy, &px, &py);
+        *p = xf_point(&a->o2w.t, v3(px, py, 0));
+    }
+    *n = a->n;
+    *pdf = a->invArea;
+    *d = vsub(*p, ref);
+    float distSquared = vlen2(*d);
+    *dist = sqrtf(distSquared);
+    *d = vdiv(*d, *dist);
+    float dp = vabsdot(*d, *n);
+    *pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+}
+
+/* pdfDirect in solid angle (shape.cpp:117-126; sphere.cpp:357-387) */
+static float ana_pdf_direct(const Ana *a, V3 ref, V3 d, V3 n, float dist) {
+    if (a->type == MTSGPU_SHAPE_SPHERE) {
+        V3 refToCenter = vsub(a->center, ref);
+        float invRefDist = (float)1.0f / vlen(refToCenter);
+        float sinAlpha = a->radius * invRefDist;
+        if (sinAlpha < 1 - EPSILON) {
+            float cosAlpha = safe_sqrt(1 - sinAlpha * sinAlpha);
+            return INV_TWOPI_F / (1 - cosAlpha);
+        }
+        return a->invArea * dist * dist / vabsdot(d, n);
+    }
+    return a->invArea * (dist * dist) / vabsdot(d, n);
+}
+
+/* ------------------------------------------------------------------------ */
 /* scene (configure): meshes, emitters, acceleration                          */
 /* ------------------------------------------------------------------------ */
 /* ------------------------------------------------------------------------ */
@@ -2010,6 +2282,8 @@ typedef struct {
     int bsdf, emitter;
     float *areaCdf;       /* nt+1 */
     float invArea;
+    int kind;             /* MTSGPU_SHAPE_* (analytic: nt = 1, no vertices) */
+    Ana ana;
 } Mesh;
 
 typedef struct { int type; V3 radiance; float weight; int mesh; } Emitter;
@@ -2231,6 +2505,21 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
     for (uint32_t i = 0; i < D->num_meshes; ++i) {
         const mtsgpu_mesh_desc *md = &D->meshes[i];
         Mesh *m = &S->meshes[i];
+        if (md->shape_type != MTSGPU_SHAPE_TRIMESH) { /* one primitive */
+            m->kind = md->shape_type;
+            if ((rc = ana_configure(md, &m->ana))) return rc;
+            m->nt = 1; m->primOffset = prims; prims += 1;
+            m->emitter = md->emitter;
+            if (md->emitter >= (int)D->num_emitters) return MTSGPU_EINVAL;
+            if (md->bsdf >= 0) { if (md->bsdf >= (int)D->num_bsdfs) return MTSGPU_EINVAL; m->bsdf = md->bsdf; }
+            else m->bsdf = (md->emitter >= 0) ? (int)D->num_bsdfs : (int)D->num_bsdfs + 1;
+            if (md->emitter >= 0) {
+                if (S->emitters[md->emitter].mesh >= 0) return MTSGPU_EINVAL;
+                S->emitters[md->emitter].mesh = (int)i;
+                m->invArea = m->ana.invArea;
+            }
+            continue;
+        }
         if (md->num_triangles == 0 || !md->positions || !md->indices) return MTSGPU_EINVAL;
         m->nv = md->num_vertices; m->nt = md->num_triangles; m->primOffset = prims;
         prims += m->nt;
@@ -2280,6 +2569,19 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
     float amin[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, amax[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (uint32_t i = 0; i < S->nmeshes; ++i) {
         Mesh *m = &S->meshes[i];
+        if (m->kind != MTSGPU_SHAPE_TRIMESH) { /* k = KNoTriangleFlag (skdtree.cpp:74-109) */
+            uint32_t p = m->primOffset;
+            memset(&S->ta[p], 0, sizeof(TriAccel));
+            S->ta[p].k = 0xFFFFFFFFu;
+            S->taMesh[p] = i; S->taTri[p] = 0;
+            for (int a = 0; a < 3; ++a) {
+                pb[p].bmin[a] = m->ana.bmin[a]; pb[p].bmax[a] = m->ana.bmax[a];
+                pb[p].c[a] = 0.5f * (m->ana.bmin[a] + m->ana.bmax[a]);
+                if (m->ana.bmin[a] < amin[a]) amin[a] = m->ana.bmin[a];
+                if (m->ana.bmax[a] > amax[a]) amax[a] = m->ana.bmax[a];
+            }
+            continue;
+        }
         for (uint32_t t = 0; t < m->nt; ++t) {
             uint32_t p = m->primOffset + t;
             V3 A = m->pos[m->idx[3 * t]], B = m->pos[m->idx[3 * t + 1]], C = m->pos[m->idx[3 * t + 2]];
@@ -2362,6 +2664,14 @@ static inline int node_hit(const BNode *n, const Ray *r, float tmin, float tmax)
 
 typedef struct { uint64_t rays, shadow, tests, nodes; } Counters;
 
+/* ShapeKDTree::intersect (skdtree.h:248-338): TriAccel or Shape::rayIntersect */
+static inline int prim_intersect(const Scene *S, uint32_t p, const Ray *ray, float mint, float maxt, int shadow,
+                                 float *u, float *v, float *t) {
+    if (S->ta[p].k == 0xFFFFFFFFu)
+        return ana_intersect(&S->meshes[S->taMesh[p]].ana, ray, mint, maxt, shadow, t, u, v);
+    return triaccel_intersect(&S->ta[p], ray, mint, maxt, u, v, t);
+}
+
 /* closest hit over [mint, maxt] (the clipped interval ShapeKDTree passes to
  * rayIntersectHavran, sahkdtree3.h:178-308); ties -> larger prim index */
 static int trace_closest(const Scene *S, const Ray *ray, float mint, float maxt,
@@ -2378,7 +2688,7 @@ static int trace_closest(const Scene *S, const Ray *ray, float mint, float maxt,
                 uint32_t p = S->order[i];
                 float u, v, t;
                 C->tests++;
-                if (triaccel_intersect(&S->ta[p], ray, mint, bt, &u, &v, &t)) {
+                if (prim_intersect(S, p, ray, mint, bt, 0, &u, &v, &t)) {
                     if (!found || t < bt || p > best) { found = 1; best = p; bt = t; bu = u; bv = v; }
                 }
             }
@@ -2400,7 +2710,7 @@ static int trace_any(const Scene *S, const Ray *ray, float mint, float maxt, Cou
             for (uint32_t i = n->first; i < n->first + n->count; ++i) {
                 float u, v, t;
                 C->tests++;
-                if (triaccel_intersect(&S->ta[S->order[i]], ray, mint, maxt, &u, &v, &t)) return 1;
+                if (prim_intersect(S, S->order[i], ray, mint, maxt, 1, &u, &v, &t)) return 1;
             }
         } else {
             stack[sp++] = n->right; stack[sp++] = n->left;
@@ -2439,6 +2749,13 @@ static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *
     uint32_t tri = S->taTri[prim];
     its->valid = 1; its->t = t; its->mesh = (int)S->taMesh[prim]; its->tri = tri;
     its->bu = u; its->bv = v;
+    if (m->kind != MTSGPU_SHAPE_TRIMESH) { /* Shape::fillIntersectionRecord + skdtree.h:425-427 */
+        V3 shN, dpdu;
+        ana_fill(&m->ana, ray, t, u, v, &its->p, &its->geoN, &shN, &dpdu, &its->u, &its->v);
+        compute_shading_frame(shN, dpdu, &its->sh);
+        its->wi = to_local(&its->sh, vneg(ray->d));
+        return;
+    }
     const float bx = 1 - u - v, by = u, bz = v;
     const uint32_t i0 = m->idx[3 * tri], i1 = m->idx[3 * tri + 1], i2 = m->idx[3 * tri + 2];
     V3 p0 = m->pos[i0], p1 = m->pos[i1], p2 = m->pos[i2];
@@ -2555,6 +2872,16 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
     V3 value;
     if (e->type == MTSGPU_EMITTER_ENVMAP) {
         value = env_sample_direct(S->env, dRec, sx, sy);
+    } else if (S->meshes[e->mesh].kind != MTSGPU_SHAPE_TRIMESH) {
+        ana_sample_direct(&S->meshes[e->mesh].ana, dRec->ref, sx, sy, &dRec->p, &dRec->n, &dRec->d, &dRec->dist,
+                          &dRec->pdf);
+        dRec->measureSolidAngle = 1;
+        if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0 && dRec->pdf != 0) { /* area.cpp:158-173 */
+            value = vdiv(e->radiance, dRec->pdf);
+        } else {
+            dRec->pdf = 0.0f;
+            value = zero;
+        }
     } else {
     const Mesh *m = &S->meshes[e->mesh];
     /* samplePosition */
@@ -2611,8 +2938,13 @@ static float pdf_emitter_direct(const Scene *S, const DRec *dRec) {
     if (e->type == MTSGPU_EMITTER_ENVMAP) {
         pdf = env_pdf_direction(S->env, dRec->d);
     } else if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0) {
-        float pdfPos = S->meshes[e->mesh].invArea;
-        pdf = pdfPos * (dRec->dist * dRec->dist) / vabsdot(dRec->d, dRec->n);
+        const Mesh *m = &S->meshes[e->mesh];
+        if (m->kind != MTSGPU_SHAPE_TRIMESH) {
+            pdf = ana_pdf_direct(&m->ana, dRec->ref, dRec->d, dRec->n, dRec->dist);
+        } else {
+            float pdfPos = m->invArea;
+            pdf = pdfPos * (dRec->dist * dRec->dist) / vabsdot(dRec->d, dRec->n);
+        }
     }
     return pdf * (e->weight * S->emNorm);
 }

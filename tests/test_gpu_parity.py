@@ -188,21 +188,51 @@ def test_smooth_bsdfs_all_materials(gpu_ctx, oracle):
         assert same.mean() > 0.999, (mi, same.mean())
 
 
+def test_analytic_shapes_bitexact(gpu_ctx, oracle):
+    """rectangle / disk / sphere shapes (exact intersection in double for spheres,
+    plugin hit records and UVs), a rectangle area light, an emitting sphere
+    (cone sampling and its solid-angle pdf), flipNormals with twosided."""
+    sc, it = scenes.build('C1', width=48, height=48, spp=16, materials='shapes')
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
+def test_analytic_shapes_under_envmap(gpu_ctx, oracle):
+    """The ENV | EXT | ANA kernel: spheres and a disk in the envmap scene."""
+    from mitsuba_amd.scene import BSDF, Mesh
+    from mitsuba_amd.transform import Transform
+    sc, it = _c3_small()
+    sc.bsdfs.append(BSDF('plastic', diffuseReflectance=(0.7, 0.2, 0.2)))
+    b = len(sc.bsdfs) - 1
+    sc.meshes.append(Mesh(shape='sphere', center=(1.6, 0.6, 0.4), radius=0.6, bsdf=b))
+    sc.meshes.append(Mesh(shape='disk', toWorld=Transform().scale(0.8).rotate((1, 0, 0), -90).translate(-1.5, 0.01, 0.5),
+                          bsdf=b))
+    gpu_ctx.upload(sc)
+    film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
+    same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
+    assert same.mean() > 0.999, same.mean()
+
+
 def _random_rays(sc, n, seed):
     rng = np.random.default_rng(seed)
-    lo = np.min([m.positions.min(0) for m in sc.meshes], 0)
-    hi = np.max([m.positions.max(0) for m in sc.meshes], 0)
+    lo = np.min([m.positions.min(0) for m in sc.meshes if not m.analytic], 0)
+    hi = np.max([m.positions.max(0) for m in sc.meshes if not m.analytic], 0)
     o = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
     d = rng.normal(size=(n, 3)).astype(np.float32)
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     return o, d
 
 
-@pytest.mark.parametrize('cfg', ['C3', 'C4'])
+@pytest.mark.parametrize('cfg', ['C3', 'C4', 'shapes'])
 def test_trace_rays_bitexact(gpu_ctx, oracle, cfg):
     """mtsgpu_trace_rays (Scene::rayIntersect / occlusion in batch) == the oracle's
-    kd-tree-semantics query: same t, barycentrics and primitive, bit for bit."""
-    sc, _ = scenes.build(cfg)
+    kd-tree-semantics query: same t, barycentrics (an analytic shape's object-space
+    hit) and primitive, bit for bit."""
+    sc, _ = scenes.build('C1', materials='shapes') if cfg == 'shapes' else scenes.build(cfg)
     gpu_ctx.upload(sc)
     o, d = _random_rays(sc, 100000, 5)
     for shadow, maxt in ((False, np.inf), (True, 3.0)):

@@ -17,6 +17,7 @@ from mitsuba_amd.xmlscene import SceneError, cube_mesh, load_scene, read_pfm, sa
 @pytest.mark.parametrize('cfg,kw', [('C1', dict(width=40, height=30, spp=4)),
                                     ('C1', dict(width=24, height=24, spp=4, materials='rough')),
                                     ('C1', dict(width=24, height=24, spp=4, materials='smooth')),
+                                    ('C1', dict(width=24, height=24, spp=4, materials='shapes')),
                                     ('C3', dict(width=32, height=18, spp=4, env_size=(64, 32), blob=(24, 16)))])
 def test_round_trip_renders_identically(tmp_path, oracle, cfg, kw):
     sc, it = scenes.build(cfg, **kw)
@@ -135,7 +136,7 @@ def test_pfm_and_cube(tmp_path):
 
 
 def test_unsupported_plugins_raise(tmp_path):
-    for shape in ('<shape type="sphere"/>', '<shape type="rectangle"/>'):
+    for shape in ('<shape type="cylinder"/>', '<shape type="hair"/>'):
         path = _write_scene(str(tmp_path), '<scene version="0.6.0">%s%s</scene>' % (SENSOR.replace('$depth', '2'), shape))
         with pytest.raises(NotImplementedError):
             load_scene(path)
