@@ -106,7 +106,10 @@ typedef struct {
     int32_t nested[2];
 } mtsgpu_bsdf_desc;
 
-enum { MTSGPU_EMITTER_AREA = 0, MTSGPU_EMITTER_ENVMAP = 1 };
+enum { MTSGPU_EMITTER_AREA = 0,      /* area.cpp: on a shape (mesh_desc.emitter)          */
+       MTSGPU_EMITTER_ENVMAP = 1,    /* envmap.cpp: lat-long image (env_* fields)          */
+       MTSGPU_EMITTER_CONSTANT = 2   /* constant.cpp: uniform 'radiance' environment       */
+};
 
 typedef struct {
     int32_t type;                   /* MTSGPU_EMITTER_*                            */

@@ -16,7 +16,7 @@ BSDF_CONDUCTOR, BSDF_DIELECTRIC, BSDF_PLASTIC, BSDF_TWOSIDED = 4, 5, 6, 7
 TEX_NONE, TEX_CHECKERBOARD = 0, 1
 ABI_VERSION = 3
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
-EMITTER_AREA, EMITTER_ENVMAP = 0, 1
+EMITTER_AREA, EMITTER_ENVMAP, EMITTER_CONSTANT = 0, 1, 2
 SHAPE_TRIMESH, SHAPE_RECTANGLE, SHAPE_DISK, SHAPE_SPHERE = 0, 1, 2, 3
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1

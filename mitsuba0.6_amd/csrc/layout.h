@@ -76,7 +76,7 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
     int32_t nested[2];
 };
 
-enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1 };
+enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1, MTSG_EMITTER_CONSTANT = 2 };
 enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4 };   // path_kernel variants   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
 
 struct MtsgShape {
@@ -133,6 +133,8 @@ struct MtsgFilter {
 #define MTSG_EWA_LUT 64             // MTS_MIPMAP_LUT_SIZE (mipmap.h:37)
 struct MtsgEnv {
     int32_t emitter;                // index into the emitter list
+    int32_t constant;               // 1: ConstantBackgroundEmitter (constant.cpp): `radiance` only
+    float radiance[3];
     int32_t levels;
     int32_t w0, h0;
     float normalization;            // m_normalization

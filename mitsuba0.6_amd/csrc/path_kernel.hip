@@ -595,6 +595,44 @@ __device__ __forceinline__ f3 area_Le(const MtsgDeviceScene &S, const Hit &h, f3
     return ld3(e.radiance);
 }
 
+// ConstantBackgroundEmitter (emitters/constant.cpp): pdfDirect in solid angle
+// (:216-231) and sampleDirect (:167-214) on the scene's bounding sphere
+#define D_INV_FOURPI 0.07957747154594766788f
+__device__ __forceinline__ float const_pdf_direct(f3 d, f3 refN) {
+    if (!is_zero(refN)) return D_INV_PI * smax(0.0f, dot(d, refN));
+    return D_INV_FOURPI;   // warp::squareToUniformSpherePdf
+}
+__device__ __noinline__ EnvSample const_sample_direct(glb_env *E, f3 ref, f3 refN, float sx, float sy) {
+    EnvSample r;
+    r.value = mk(0, 0, 0); r.pdf = 0.0f; r.dist = 0.0f;
+    f3 d;
+    float pdf;
+    if (!is_zero(refN)) {
+        d = square_to_cosine_hemisphere(sx, sy);
+        pdf = D_INV_PI * d.z;
+        Frame F;
+        F.n = refN;
+        coordinate_system(refN, F.s, F.t);
+        d = to_world(F, d);
+    } else {
+        const float z = 1.0f - 2.0f * sy;   // warp::squareToUniformSphere (warp.cpp:25-31)
+        const float rr = safe_sqrt(1.0f - z * z);
+        float sinPhi, cosPhi;
+        d_sincos(2.0f * D_PI * sx, &sinPhi, &cosPhi);
+        d = mk(rr * cosPhi, rr * sinPhi, z);
+        pdf = D_INV_FOURPI;
+    }
+    r.d = d;
+    float nearT, farT;
+    if (!env_bsphere(E, ref, d, nearT, farT)) return r;
+    if (!(nearT < 0 && farT > 0)) return r;
+    r.dist = farT;
+    r.pdf = pdf;
+    if (!is_zero(refN) && dot(d, refN) <= 0) return r;   // roundoff moved the sample to the backside
+    r.value = divs(mk(E->radiance[0], E->radiance[1], E->radiance[2]), pdf);
+    return r;
+}
+
 // compact pixel index (8x8 tiles over the window's active rows) -> image pixel
 __device__ __forceinline__ bool pixel_of(const MtsgLaunch &L, uint32_t p, int &px, int &py) {
     const uint32_t tile = p >> 6, in = p & 63;
@@ -804,7 +842,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     // missed: the environment emitter, if any (path.cpp:233-247)
                     if (ENV && !(L.hide_emitters && !P.scattered)) {
                         glb_env *E = (glb_env *)S.env;
-                        const f3 value = env_eval(E, rd);
+                        const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : env_eval(E, rd);
                         float nT, fT;
                         // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
                         if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
@@ -812,7 +850,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             P.eta *= P.bsdfEta;
                             float lumPdf = 0;
                             if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
-                                lumPdf = env_pdf_direction(E, rd) * (S.emitters[S.env_emitter].weight * S.em_norm);
+                                lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : env_pdf_direction(E, rd)) *
+                                         (S.emitters[S.env_emitter].weight * S.em_norm);
                             const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
                             P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
                         }
@@ -874,11 +913,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                     W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
                         rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
                         ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
+                        glb_env *E = (glb_env *)S.env;
+                        if (E->constant) {   // ConstantBackgroundEmitter::evalEnvironment (constant.cpp:241-243)
+                            P.L = add(P.L, mulv(P.thr, mk(E->radiance[0], E->radiance[1], E->radiance[2])));
+                        } else {
 #ifdef MTSG_ABL_BILINEAR_PRIMARY   // timing ablation only
-                        P.L = add(P.L, mulv(P.thr, env_eval((glb_env *)S.env, rd)));
+                        P.L = add(P.L, mulv(P.thr, env_eval(E, rd)));
 #else
-                        P.L = add(P.L, mulv(P.thr, env_eval_diff((glb_env *)S.env, rd, rxd, ryd)));
+                        P.L = add(P.L, mulv(P.thr, env_eval_diff(E, rd, rxd, ryd)));
 #endif
+                        }
                     }
                     endPath = true;
                 } else {
@@ -901,9 +945,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             const MtsgEmitter &e = S.emitters[ei];
                             f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
                             float pdf = 0.0f, dist = 0.0f;
-                            if (ENV && e.type == MTSG_EMITTER_ENVMAP) {
+                            if (ENV && e.type != MTSG_EMITTER_AREA) {
 #ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
-                                const EnvSample es = env_sample_direct((glb_env *)S.env, P.its.p, ex, ey);
+                                glb_env *E = (glb_env *)S.env;
+                                const EnvSample es = E->constant ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
+                                                                 : env_sample_direct(E, P.its.p, ex, ey);
                                 value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
 #endif
                             } else if (ANA && S.shapes[e.shape].analytic >= 0) {

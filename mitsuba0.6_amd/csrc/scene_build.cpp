@@ -1077,6 +1077,16 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
                 return MTSGPU_EINVAL;
             }
             if ((rc = build_envmap(e, (int)i, S, err))) return rc;
+        } else if (e.type == MTSGPU_EMITTER_CONSTANT) {
+            // ConstantBackgroundEmitter (constant.cpp:44-96): a uniform environment on the
+            // scene's bounding sphere (createShape, :67-91, as envmap_bsphere below)
+            if (S.env.emitter >= 0) {
+                err = "Only one environment emitter can be specified per scene.";
+                return MTSGPU_EINVAL;
+            }
+            S.env.emitter = (int)i;
+            S.env.constant = 1;
+            for (int k = 0; k < 3; ++k) S.env.radiance[k] = e.radiance[k];
         } else if (e.type != MTSGPU_EMITTER_AREA) {
             err = "unsupported emitter type";
             return MTSGPU_EINVAL;

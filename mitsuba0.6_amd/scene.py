@@ -156,7 +156,8 @@ class BSDF:
 
 @dataclass
 class Emitter:
-    """`area` (src/emitters/area.cpp) or `envmap` (src/emitters/envmap.cpp).
+    """`area` (src/emitters/area.cpp), `envmap` (src/emitters/envmap.cpp) or
+    `constant` (src/emitters/constant.cpp: a uniform `radiance` environment).
 
     envmap: `bitmap` is the decoded lat-long image, (H, W, 3) linear RGB float32
     (what Bitmap(EAuto, stream) yields for an RGB EXR/PFM/HDR file), `scale` and
@@ -170,7 +171,7 @@ class Emitter:
 
     def to_desc(self):
         d = abi.EmitterDesc()
-        d.type = {'area': abi.EMITTER_AREA, 'envmap': abi.EMITTER_ENVMAP}[self.type]
+        d.type = {'area': abi.EMITTER_AREA, 'envmap': abi.EMITTER_ENVMAP, 'constant': abi.EMITTER_CONSTANT}[self.type]
         d.radiance[:] = self.radiance
         d.sampling_weight = self.samplingWeight
         d.env_scale = self.scale

@@ -19,7 +19,7 @@ Plugins:
   `gaussian`.
 - shapes `obj`, `ply`, `serialized`, `cube` (triangle meshes).
 - BSDFs `diffuse`, `roughconductor`, `roughdielectric`.
-- emitters `area` (inside a shape) and `envmap` (PFM files).
+- emitters `area` (inside a shape), `envmap` (PFM/EXR/RGBE files) and `constant`.
 
 Anything else raises NotImplementedError naming the plugin. That includes
 analytic shapes (`rectangle`, `sphere`, `disk`, `cylinder`), which the
@@ -334,6 +334,9 @@ class XMLSceneLoader:
         return Emitter('area', radiance=p.get('radiance', (1.0, 1.0, 1.0)), samplingWeight=p.get('samplingWeight', 1.0))
 
     def make_envmap(self, p):
+        if p.plugin == 'constant':   # constant.cpp:46-49; Spectrum::getD65() is 1 in the RGB build (spectrum.cpp:163-165)
+            return Emitter('constant', radiance=p.get('radiance', (1.0, 1.0, 1.0)),
+                           samplingWeight=float(p.get('samplingWeight', 1.0)))
         fn = p.get('filename')
         if fn is None:
             raise SceneError('envmap: missing filename')
@@ -405,9 +408,9 @@ class XMLSceneLoader:
                 self.parse_object(el)       # named object for later <ref>
             elif el.tag == 'emitter':
                 p = self.parse_object(el)
-                if p.plugin != 'envmap':
-                    raise NotImplementedError('emitter plugin "%s" (area lights on shapes and envmap are '
-                                              'supported)' % p.plugin)
+                if p.plugin not in ('envmap', 'constant'):
+                    raise NotImplementedError('emitter plugin "%s" (area lights on shapes, envmap and constant '
+                                              'are supported)' % p.plugin)
                 env_props.append(p)
             elif el.tag in ('medium', 'subsurface'):
                 raise NotImplementedError('<%s>: participating media / subsurface are not on the path' % el.tag)
@@ -725,6 +728,10 @@ def save_scene(scene, integ, directory, name='scene.xml'):
                      % (_rgb('radiance', e.radiance), _fmt(e.samplingWeight)))
         L.append('  </shape>')
     for j, e in enumerate(scene.emitters):
+        if e.type == 'constant':
+            L.append('  <emitter type="constant">%s<float name="samplingWeight" value="%s"/></emitter>'
+                     % (_rgb('radiance', e.radiance), _fmt(e.samplingWeight)))
+            continue
         if e.type != 'envmap':
             continue
         fn = 'envmap%d.pfm' % j

@@ -1927,6 +1927,8 @@ static float ana_pdf_direct(const Ana *a, V3 ref, V3 d, V3 n, float dist) {
 #define EWA_LUT 64 /* MTS_MIPMAP_LUT_SIZE, mipmap.h:37 */
 
 typedef struct Env {
+    int constant;  /* ConstantBackgroundEmitter (constant.cpp): radiance only */
+    V3 radiance;
     int levels, w0, h0;
     int lw[ENV_MAX_LEVELS], lh[ENV_MAX_LEVELS];
     float ratioX[ENV_MAX_LEVELS], ratioY[ENV_MAX_LEVELS];
@@ -2216,8 +2218,9 @@ static V3 env_eval_filtered(const Env *E, float uvx, float uvy, float d0x, float
 }
 static inline float safe_acosf(float v) { return o_acos(smin(1.0f, smax(-1.0f, v))); } /* math.h:250-252 */
 
-/* EnvironmentMap::evalEnvironment (envmap.cpp:380-410) */
+/* EnvironmentMap::evalEnvironment (envmap.cpp:380-410); constant.cpp:241-243 */
 static V3 env_eval(const Env *E, const Ray *ray) {
+    if (E->constant) return E->radiance;
     V3 v = xf_vector(&E->toLocal, ray->d);
     float uvx = o_atan2(v.x, -v.z) * INV_TWOPI_F, uvy = safe_acosf(v.y) * INV_PI_F;
     V3 value;
@@ -2493,6 +2496,12 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
             S->env = (Env *)calloc(1, sizeof(Env));
             S->envIndex = (int)i;
             if ((rc = env_configure(e, S->env))) return rc;
+        } else if (e->type == MTSGPU_EMITTER_CONSTANT) { /* constant.cpp:44-96 */
+            if (S->env) return MTSGPU_EINVAL;
+            S->env = (Env *)calloc(1, sizeof(Env));
+            S->envIndex = (int)i;
+            S->env->constant = 1;
+            S->env->radiance = v3(e->radiance[0], e->radiance[1], e->radiance[2]);
         } else if (e->type != MTSGPU_EMITTER_AREA) {
             return MTSGPU_EINVAL;
         }
@@ -2808,6 +2817,39 @@ typedef struct {
 } DRec;
 
 /* EnvironmentMap::sampleDirect (envmap.cpp:516-543) + internalSampleDirection (:567-603) */
+/* ConstantBackgroundEmitter::sampleDirect (constant.cpp:167-214) */
+static V3 const_sample_direct(const Env *E, DRec *dRec, float sx, float sy) {
+    V3 d;
+    float pdf;
+    if (!vzero(dRec->refN)) {
+        d = square_to_cosine_hemisphere(sx, sy);
+        pdf = cosine_hemisphere_pdf(d);
+        Frame F;
+        F.n = dRec->refN;
+        coordinate_system(F.n, &F.s, &F.t);
+        d = to_world(&F, d);
+    } else {
+        float z = 1.0f - 2.0f * sy; /* warp::squareToUniformSphere (warp.cpp:25-31) */
+        float r = safe_sqrt(1.0f - z * z);
+        float sinPhi, cosPhi;
+        o_sincos(2.0f * M_PI_F * sx, &sinPhi, &cosPhi);
+        d = v3(r * cosPhi, r * sinPhi, z);
+        pdf = 0.07957747154594766788f; /* INV_FOURPI */
+    }
+    float nearT, farT;
+    dRec->pdf = 0.0f;
+    if (!env_bsphere(E, dRec->ref, d, &nearT, &farT)) return v3(0, 0, 0);
+    if (!(nearT < 0 && farT > 0)) return v3(0, 0, 0);
+    dRec->p = vadd(dRec->ref, vmul(d, farT));
+    dRec->n = vnormalize(vsub(E->center, dRec->p));
+    dRec->measureSolidAngle = 1;
+    dRec->d = d;
+    dRec->dist = farT;
+    dRec->pdf = pdf;
+    if (!vzero(dRec->refN) && vdot(dRec->d, dRec->refN) <= 0) return v3(0, 0, 0);
+    return vdiv(E->radiance, pdf);
+}
+
 static V3 env_sample_direct(const Env *E, DRec *dRec, float sx, float sy) {
     uint32_t row = env_sample_reuse(E->cdfRows, (uint32_t)E->h0, &sy);
     uint32_t col = env_sample_reuse(E->cdfCols + (size_t)row * (E->w0 + 1), (uint32_t)E->w0, &sx);
@@ -2872,6 +2914,8 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
     V3 value;
     if (e->type == MTSGPU_EMITTER_ENVMAP) {
         value = env_sample_direct(S->env, dRec, sx, sy);
+    } else if (e->type == MTSGPU_EMITTER_CONSTANT) {
+        value = const_sample_direct(S->env, dRec, sx, sy);
     } else if (S->meshes[e->mesh].kind != MTSGPU_SHAPE_TRIMESH) {
         ana_sample_direct(&S->meshes[e->mesh].ana, dRec->ref, sx, sy, &dRec->p, &dRec->n, &dRec->d, &dRec->dist,
                           &dRec->pdf);
@@ -2937,6 +2981,8 @@ static float pdf_emitter_direct(const Scene *S, const DRec *dRec) {
     float pdf = 0.0f;
     if (e->type == MTSGPU_EMITTER_ENVMAP) {
         pdf = env_pdf_direction(S->env, dRec->d);
+    } else if (e->type == MTSGPU_EMITTER_CONSTANT) { /* constant.cpp:216-231, solid angle */
+        pdf = !vzero(dRec->refN) ? INV_PI_F * smax(0.0f, vdot(dRec->d, dRec->refN)) : 0.07957747154594766788f;
     } else if (vdot(dRec->d, dRec->refN) >= 0 && vdot(dRec->d, dRec->n) < 0) {
         const Mesh *m = &S->meshes[e->mesh];
         if (m->kind != MTSGPU_SHAPE_TRIMESH) {

@@ -217,6 +217,22 @@ def test_analytic_shapes_under_envmap(gpu_ctx, oracle):
     assert same.mean() > 0.999, same.mean()
 
 
+def test_constant_emitter_bitexact(gpu_ctx, oracle):
+    """constant.cpp: uniform environment on the scene's bounding sphere -- camera and
+    BSDF-sampled misses, cosine-sampled NEE (uniform-sphere NEE where refN = 0:
+    the roughdielectric sphere), its solid-angle pdf in MIS; with an area light."""
+    from mitsuba_amd.scene import BSDF, Emitter, Mesh
+    sc, it = _c3_small(area_light=True)
+    sc.emitters[0] = Emitter('constant', radiance=(0.8, 0.9, 1.1), samplingWeight=1.5)
+    sc.bsdfs.append(BSDF('roughdielectric', distribution='ggx', alpha=0.2, intIOR=1.5))
+    sc.meshes.append(Mesh(shape='sphere', center=(-1.6, 0.7, 0.3), radius=0.7, bsdf=len(sc.bsdfs) - 1))
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
 def _random_rays(sc, n, seed):
     rng = np.random.default_rng(seed)
     lo = np.min([m.positions.min(0) for m in sc.meshes if not m.analytic], 0)

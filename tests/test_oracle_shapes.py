@@ -125,3 +125,20 @@ def test_rectangle_light_matches_quad_mesh(oracle):
     m2, e2 = _mean_radiance(oracle, sc, it, 256)
     assert quad.emitter == 0
     assert np.all(np.abs(m1 - m2) <= 5 * np.hypot(e1, e2)), (m1, m2, e1, e2)
+
+
+def test_constant_emitter_furnace(oracle):
+    """White furnace (constant.cpp): a white Lambertian sphere and disk under a uniform
+    environment are invisible in expectation -- cosine-sampled NEE on the bounding
+    sphere, its pdf in MIS, and the BSDF-sampled environment hits must all agree."""
+    base, it = scenes.build('C1', width=16, height=16, spp=4)
+    from mitsuba_amd.scene import look_at, Sensor
+    sensor = Sensor(fov=30.0, fovAxis='x', toWorld=look_at(np.array([0, 0, -6.0]), np.array([0, 0, 0.0]), (0, 1, 0)),
+                    width=16, height=16)
+    white = BSDF('diffuse', reflectance=1.0)
+    meshes = [Mesh(shape='sphere', center=(0, 0, 0), radius=1.0, bsdf=0),
+              Mesh(shape='disk', toWorld=Transform().scale(1.2).translate(0.5, 0.3, -1.5), bsdf=1)]
+    sc = Scene(sensor, meshes, [white, BSDF('twosided', nested=[BSDF('diffuse', reflectance=1.0)])],
+               [Emitter('constant', radiance=(0.5, 0.5, 0.5))])
+    m, e = _mean_radiance(oracle, sc, it, 512)
+    assert np.all(np.abs(m - 0.5) <= 5 * e + 1e-3), (m, e)
