@@ -303,6 +303,8 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // small scenes: stage the whole BVH + TriAccel array in LDS (<= 32 KiB)
     const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri);
     L.scene_lds = (sceneBytes <= (32u << 10) && !std::getenv("MTSGPU_NO_SCENE_LDS")) ? 1u : 0u;
+    L.scan = (L.scene_lds && H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty() && !std::getenv("MTSGPU_NO_SCAN"))
+                 ? 1u : 0u;
     // large scenes are latency-bound: run 4 waves/SIMD when 4 blocks' traversal
     // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
     // LDS as the rest allows (the others are read through L1/L2)

@@ -19,6 +19,7 @@
 #define MTSG_SOBOL_SIZE 52
 #define MTSG_FILTER_RES 31
 #define MTSG_BLOCK_SIZE 32
+#define MTSG_SCAN_MAX 64      // primitives up to which SCENE_LDS scenes scan instead of traversing
 
 // node child reference: >= 0 inner node index; < 0 leaf: ~ref = first << 4 | count
 static inline int32_t mtsg_leaf_ref(uint32_t first, uint32_t count) {
@@ -214,6 +215,7 @@ struct MtsgLaunch {
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
+    uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

@@ -379,6 +379,46 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
 
 #endif
 
+// Tiny scenes (<= MTSG_SCAN_MAX primitives, e.g. the Cornell box): every lane tests
+// every TriAccel record in one wave-uniform loop.  The records are read through
+// the constant address space with a uniform index, i.e. by scalar loads into
+// SGPRs: no traversal stack, no divergent node loop, no VGPRs for the records.
+// The closest hit and the tie rule are those of traverse().
+typedef __attribute__((address_space(4))) const MtsgTri cst_tri;
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool scan_tris(cst_tri *tris, uint32_t n, f3 o, f3 d, float mint, float maxt,
+                                          uint32_t &bestSlot, float &bu, float &bv, float &bt,
+                                          unsigned long long &tests) {
+    bool found = false;
+    uint32_t bestPrim = 0;
+    bt = maxt;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (STATS) tests++;
+        cst_tri &tr = tris[i];
+        const uint32_t k = tr.k;
+        float o_u, o_v, o_k, d_u, d_v, d_k;
+        if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+        else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+        else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+        else continue;
+        // TriAccel::rayIntersect (triaccel.h:92-160)
+        const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
+        if (t < mint || t > bt) continue;
+        const float hu = o_u + t * d_u - tr.a_u;
+        const float hv = o_v + t * d_v - tr.a_v;
+        const float u = hv * tr.b_nu + hu * tr.b_nv;
+        const float v = hu * tr.c_nu + hv * tr.c_nv;
+        if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+            if (ANY) return true;
+            const uint32_t prim = tr.prim;
+            if (!found || t < bt || prim > bestPrim) {
+                found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+            }
+        }
+    }
+    return found;
+}
+
 // AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
 __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, float &nearT, float &farT) {
     nearT = -INFINITY; farT = INFINITY;
@@ -558,8 +598,7 @@ struct PathVars {
     Hit its;          // current vertex
     f3 neeC;          // throughput*value*bsdfVal*weight, committed if the shadow ray is unoccluded
     f3 refN;          // DirectSamplingRecord::refN of the current vertex
-    f3 bsdfWeight;
-    float bsdfPdf, bsdfEta;
+    float bsdfPdf;
     int sampledType;
 };
 
@@ -802,7 +841,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             if (!is_zero(P.neeC) && ray_interval(S, P.its.p, sd, D_EPSILON, smaxt, true, mint, maxt)) {
 #endif
                 uint32_t sl; float a0, a1, a2;
-                if (SCENE_LDS)
+                if (SCENE_LDS && L.scan)
+                    occluded = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, P.its.p, sd, mint, maxt, sl, a0, a1, a2, cTests);
+                else if (SCENE_LDS)
                     occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
                 else
                     occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
@@ -815,7 +856,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             cRays++;
             float mint, maxt;
             if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
-                if (SCENE_LDS)
+                if (SCENE_LDS && L.scan)
+                    hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, ro, rd, mint, maxt, slot, hu, hv, ht, cTests);
+                else if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
                 else
                     hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
@@ -833,7 +876,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 endPath = true;   // the BSDF sample at the previous vertex failed
             } else {
                 // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
-                if (hit) fill_hit<EXT, ANA>(S, slot, hu, hv, ht, ro, rd, P.its); else P.its.valid = 0;
+                // a miss overwrites the whole record: no field of the previous vertex stays
+                // live across the next traversal except through an explicit use
+                if (hit) fill_hit<EXT, ANA>(S, slot, hu, hv, ht, ro, rd, P.its); else P.its = Hit{};
                 if (STATS && hit) cHits++;
                 if (primary) {
                     P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
@@ -846,8 +891,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                         float nT, fT;
                         // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
                         if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
-                            P.thr = mulv(P.thr, P.bsdfWeight);
-                            P.eta *= P.bsdfEta;
                             float lumPdf = 0;
                             if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
                                 lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : env_pdf_direction(E, rd)) *
@@ -859,8 +902,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     endPath = true;   // !its.isValid(): break after the environment term
                 } else {
                     const MtsgShape &sh = S.shapes[P.its.shape];
-                    P.thr = mulv(P.thr, P.bsdfWeight);
-                    P.eta *= P.bsdfEta;
                     if (sh.emitter >= 0) {
                         const f3 value = area_Le(S, P.its, neg(rd));
                         float lumPdf = 0;
@@ -1044,9 +1085,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             P.scattered |= bs.sampledType != MTSG_F_NULL;
                             const f3 wo = to_world(P.its.sh, bs.wo);
                             if (!L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
-                                P.bsdfWeight = bs.weight;
+                                // throughput *= bsdfWeight; eta *= bRec.eta (path.cpp:256-257): the same
+                                // products as after the hit, formed now so they need not stay live
+                                P.thr = mulv(P.thr, bs.weight);
                                 P.bsdfPdf = bs.pdf;
-                                P.bsdfEta = bs.eta;
+                                P.eta *= bs.eta;
                                 P.sampledType = bs.sampledType;
                                 ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
                                 rd = wo;
