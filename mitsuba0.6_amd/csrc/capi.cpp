@@ -301,7 +301,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.stack_depth = H.bvh_depth + 2;
     L.num_nodes = (uint32_t)H.nodes.size();
     // small scenes: stage the whole BVH + TriAccel array in LDS (<= 32 KiB)
-    const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri);
+    L.num_verts = (uint32_t)(H.positions.size() / 3);
+    L.num_shapes = (uint32_t)H.shapes.size();
+    const size_t sceneBytes = H.nodes.size() * sizeof(MtsgNode) + H.tris.size() * sizeof(MtsgTri) +
+                              H.prim_vtx.size() * 4 + H.dpdu.size() * 4 + H.positions.size() * 4 +
+                              H.normals.size() * 4 + H.shapes.size() * sizeof(MtsgShape);
     L.scene_lds = (sceneBytes <= (32u << 10) && !std::getenv("MTSGPU_NO_SCENE_LDS")) ? 1u : 0u;
     L.scan = (L.scene_lds && H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty() && !std::getenv("MTSGPU_NO_SCAN"))
                  ? 1u : 0u;

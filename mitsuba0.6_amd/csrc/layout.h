@@ -216,6 +216,7 @@ struct MtsgLaunch {
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
+    uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

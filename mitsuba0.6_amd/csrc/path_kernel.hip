@@ -465,10 +465,20 @@ __device__ __forceinline__ Frame shading_frame(f3 n, f3 dpdu) {
     return f;
 }
 
+// Where a vertex's triangle data comes from: HBM, or (small scenes, SCENE_LDS)
+// the LDS copy every workgroup stages next to the BVH
+typedef __attribute__((address_space(3))) const float lds_f32;
+typedef __attribute__((address_space(1))) const MtsgShape glb_shape;
+typedef __attribute__((address_space(3))) const MtsgShape lds_shape;
+template <bool INLDS> struct HitSrc;
+template <> struct HitSrc<false> { glb_u32 *pv; glb_f32 *pos, *nrm, *dpdu; glb_shape *shapes; };
+template <> struct HitSrc<true> { lds_u32 *pv; lds_f32 *pos, *nrm, *dpdu; lds_shape *shapes; };
+template <typename P> __device__ __forceinline__ f3 ldp3(P p) { return mk(p[0], p[1], p[2]); }
+
 // fillIntersectionRecord<true> (skdtree.h:343-429); UV = TEX
-template <bool TEX, bool ANA = false>
-__device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot, float u, float v, float t, f3 o, f3 d,
-                                         Hit &h) {
+template <bool TEX, bool ANA, typename HS>
+__device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, const HS &hs, uint32_t slot, uint32_t prim, float u,
+                                         float v, float t, f3 o, f3 d, Hit &h) {
     if constexpr (ANA) {
         const MtsgTri &tr = S.tris[slot];
         if (tr.k == MTSG_K_ANALYTIC) {   // Shape::fillIntersectionRecord + skdtree.h:425-427
@@ -484,24 +494,23 @@ __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot
             return;
         }
     }
-    const uint32_t prim = S.tris[slot].prim;
-    const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
+    const uint4 pv = make_uint4(hs.pv[4 * prim], hs.pv[4 * prim + 1], hs.pv[4 * prim + 2], hs.pv[4 * prim + 3]);
     h.valid = 1;
     h.t = t;
     h.shape = (int)pv.w;
     const float bx = 1 - u - v, by = u, bz = v;
-    const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
-             p2 = ld3(S.positions + 3 * (size_t)pv.z);
+    const f3 p0 = ldp3(hs.pos + 3 * (size_t)pv.x), p1 = ldp3(hs.pos + 3 * (size_t)pv.y),
+             p2 = ldp3(hs.pos + 3 * (size_t)pv.z);
     h.p = add(add(mul(p0, bx), mul(p1, by)), mul(p2, bz));
     const f3 side1 = sub(p1, p0), side2 = sub(p2, p0);
     f3 faceNormal = cross(side1, side2);
     const float length = len(faceNormal);
     if (!is_zero(faceNormal)) faceNormal = divs(faceNormal, length);
-    const f3 dpdu = ld3(S.dpdu + 3 * (size_t)prim);
+    const f3 dpdu = ldp3(hs.dpdu + 3 * (size_t)prim);
     f3 shN;
-    if (S.shapes[h.shape].has_normals) {
-        const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
-                 n2 = ld3(S.normals + 3 * (size_t)pv.z);
+    if (hs.shapes[h.shape].has_normals) {
+        const f3 n0 = ldp3(hs.nrm + 3 * (size_t)pv.x), n1 = ldp3(hs.nrm + 3 * (size_t)pv.y),
+                 n2 = ldp3(hs.nrm + 3 * (size_t)pv.z);
         shN = normalize(add(add(mul(n0, bx), mul(n1, by)), mul(n2, bz)));
         if (dot(faceNormal, shN) < 0) faceNormal = neg(faceNormal);
     } else {
@@ -511,7 +520,7 @@ __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, uint32_t slot
     h.sh = shading_frame(shN, dpdu);
     h.wi = to_local(h.sh, neg(d));
     if constexpr (TEX) {   // skdtree.h:398-405: t0*b.x + t1*b.y + t2*b.z, else (b.y, b.z)
-        if (S.shapes[h.shape].has_uv) {
+        if (hs.shapes[h.shape].has_uv) {
             const float *tc = S.texcoords;
             h.u = tc[2 * (size_t)pv.x] * bx + tc[2 * (size_t)pv.y] * by + tc[2 * (size_t)pv.z] * bz;
             h.v = tc[2 * (size_t)pv.x + 1] * bx + tc[2 * (size_t)pv.y + 1] * by + tc[2 * (size_t)pv.z + 1] * bz;
@@ -749,12 +758,40 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
         for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[base2 + i] = gn[i];
         for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[base2 + nodeWords + i] = gt[i];
         sceneWords = nodeWords + triWords;
+        // the vertices' triangle data: prim_vtx, dpdu, positions, normals, shape records
+        const uint32_t np = S.num_prims, nv = L.num_verts, ns = L.num_shapes * (sizeof(MtsgShape) / 4);
+        const uint32_t *srcs[5] = {S.prim_vtx, reinterpret_cast<const uint32_t *>(S.dpdu),
+                                   reinterpret_cast<const uint32_t *>(S.positions),
+                                   reinterpret_cast<const uint32_t *>(S.normals),
+                                   reinterpret_cast<const uint32_t *>(S.shapes)};
+        const uint32_t lens[5] = {4 * np, 3 * np, 3 * nv, 3 * nv, ns};
+        for (int a = 0; a < 5; ++a) {
+            for (uint32_t i = threadIdx.x; i < lens[a]; i += BLOCK) lds[base2 + sceneWords + i] = srcs[a][i];
+            sceneWords += lens[a];
+        }
     }
     __syncthreads();
     lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
     // base2 and the node array size are multiples of 4 words: 16-byte aligned (ds_read_b128)
     lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
     lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
+    // triangle data of hit records and emitter samples (HitSrc)
+    HitSrc<SCENE_LDS> hs;
+    if constexpr (SCENE_LDS) {
+        const uint32_t np = S.num_prims, nv = L.num_verts;
+        lds_u32 *b = (lds_u32 *)(lds + base2 + L.num_nodes * 16 + np * 12);
+        hs.pv = b;
+        hs.dpdu = (lds_f32 *)(b + 4 * np);
+        hs.pos = (lds_f32 *)(b + 7 * np);
+        hs.nrm = (lds_f32 *)(b + 7 * np + 3 * nv);
+        hs.shapes = (lds_shape *)(b + 7 * np + 6 * nv);
+    } else {
+        hs.pv = (glb_u32 *)S.prim_vtx;
+        hs.dpdu = (glb_f32 *)S.dpdu;
+        hs.pos = (glb_f32 *)S.positions;
+        hs.nrm = (glb_f32 *)S.normals;
+        hs.shapes = (glb_shape *)S.shapes;
+    }
     SobolCtx SC;
     SC.lds = (lds_u32 *)lds;
     SC.glob = (glb_u32 *)L.sobol_nib;
@@ -878,7 +915,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
                 // a miss overwrites the whole record: no field of the previous vertex stays
                 // live across the next traversal except through an explicit use
-                if (hit) fill_hit<EXT, ANA>(S, slot, hu, hv, ht, ro, rd, P.its); else P.its = Hit{};
+                if (hit) {
+                    const uint32_t prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+                    fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, ro, rd, P.its);
+                } else {
+                    P.its = Hit{};
+                }
                 if (STATS && hit) cHits++;
                 if (primary) {
                     P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
@@ -901,7 +943,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     }
                     endPath = true;   // !its.isValid(): break after the environment term
                 } else {
-                    const MtsgShape &sh = S.shapes[P.its.shape];
+                    auto &sh = hs.shapes[P.its.shape];
                     if (sh.emitter >= 0) {
                         const f3 value = area_Le(S, P.its, neg(rd));
                         float lumPdf = 0;
@@ -967,7 +1009,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     }
                     endPath = true;
                 } else {
-                    const MtsgShape &sh = S.shapes[P.its.shape];
+                    auto &sh = hs.shapes[P.its.shape];
                     GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
                     if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
                         P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
@@ -1005,17 +1047,18 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             float py2 = ey;
                             const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
                             const uint32_t prim = e.tri_first + lt;
-                            const uint4 pv = *reinterpret_cast<const uint4 *>(S.prim_vtx + 4 * (size_t)prim);
+                            const uint4 pv = make_uint4(hs.pv[4 * prim], hs.pv[4 * prim + 1], hs.pv[4 * prim + 2],
+                                                        hs.pv[4 * prim + 3]);
                             const float a = safe_sqrt(1.0f - ex);
                             const float bx = 1 - a, by = a * py2;
-                            const f3 p0 = ld3(S.positions + 3 * (size_t)pv.x), p1 = ld3(S.positions + 3 * (size_t)pv.y),
-                                     p2 = ld3(S.positions + 3 * (size_t)pv.z);
+                            const f3 p0 = ldp3(hs.pos + 3 * (size_t)pv.x), p1 = ldp3(hs.pos + 3 * (size_t)pv.y),
+                                     p2 = ldp3(hs.pos + 3 * (size_t)pv.z);
                             const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
                             const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
                             f3 ln;
-                            if (S.shapes[e.shape].has_normals) {
-                                const f3 n0 = ld3(S.normals + 3 * (size_t)pv.x), n1 = ld3(S.normals + 3 * (size_t)pv.y),
-                                         n2 = ld3(S.normals + 3 * (size_t)pv.z);
+                            if (hs.shapes[e.shape].has_normals) {
+                                const f3 n0 = ldp3(hs.nrm + 3 * (size_t)pv.x), n1 = ldp3(hs.nrm + 3 * (size_t)pv.y),
+                                         n2 = ldp3(hs.nrm + 3 * (size_t)pv.z);
                                 ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
                             } else {
                                 ln = normalize(cross(sideA, sideB));
@@ -1225,7 +1268,9 @@ __global__ void arith_probe(const float *a, const float *b, float *out, int n) {
 // host-side launchers (called by capi.cpp)
 // ---------------------------------------------------------------------------
 size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
-    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
+    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * (12 + 7) +
+                                        (size_t)L.num_verts * 6 + (size_t)L.num_shapes * (sizeof(MtsgShape) / 4))
+                                     : 0;
     return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2) * 4;
 }
 
