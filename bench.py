@@ -128,8 +128,14 @@ def main():
 
     if rank == 0:
         value = total_samples / elapsed_max / 1e6
-        # roofline: traversal counters from a bounded stats pass (1/16 of the rows)
-        _, _, sst = ctx.render(integ, row=(ROW_BLOCK, 16, 0), traversal_stats=True)
+        # roofline: traversal counters from a bounded stats pass (1/16 of the rows), always
+        # through the BVH: tiny scenes' linear TriAccel scan (an implementation choice that
+        # reads every record from the scalar cache) must not inflate the workload's bytes
+        os.environ['MTSGPU_NO_SCAN'] = '1'
+        try:
+            _, _, sst = ctx.render(integ, row=(ROW_BLOCK, 16, 0), traversal_stats=True)
+        finally:
+            os.environ.pop('MTSGPU_NO_SCAN', None)
         bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
         avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
         per_launch_samples = samples_rank / max(1, len(kernel_ms))

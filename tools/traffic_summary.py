@@ -27,7 +27,7 @@ def counter(path_glob, name):
     return vals
 
 
-for cfg in ('C2', 'C3', 'C4'):
+for cfg in ('C2', 'C3', 'C4', 'C5'):
     fetch = counter(os.path.join(src, 'pmc_%s_FETCH_SIZE' % cfg, '**', '*counter_collection.csv'), 'FETCH_SIZE')
     write = counter(os.path.join(src, 'pmc_%s_WRITE_SIZE' % cfg, '**', '*counter_collection.csv'), 'WRITE_SIZE')
     if fetch and write:
