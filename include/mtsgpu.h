@@ -193,7 +193,15 @@ typedef struct {
     uint32_t row_block, row_stride, row_phase;
     const volatile int32_t *cancel; /* polled between launches, may be NULL        */
     uint32_t flags;                 /* MTSGPU_FLAG_*                               */
+    /* the integrator plugin: MTSGPU_INTEGRATOR_PATH (path.cpp; max_depth, rr_depth)
+       or MTSGPU_INTEGRATOR_DIRECT (direct.cpp:90-306): 'emitterSamples' and
+       'bsdfSamples' (both default to 'shadingSamples' = 1); strict_normals and
+       hide_emitters apply to both */
+    int32_t integrator;
+    uint32_t emitter_samples, bsdf_samples;
 } mtsgpu_render_params;
+
+enum { MTSGPU_INTEGRATOR_PATH = 0, MTSGPU_INTEGRATOR_DIRECT = 1 };
 
 /* render flags */
 #define MTSGPU_FLAG_TRAVERSAL_STATS 1u  /* count BVH node visits / TriAccel tests   */

@@ -240,8 +240,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (!ctx || !P) return MTSGPU_EINVAL;
     if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "render called before a successful upload_scene");
     if (P->spp == 0) return fail(ctx, MTSGPU_EINVAL, "sampleCount must be positive");
-    if (P->rr_depth <= 0) return fail(ctx, MTSGPU_EINVAL, "'rrDepth' must be set to a value greater than zero!");
-    if (P->max_depth <= 0 && P->max_depth != -1)
+    if (P->integrator == MTSGPU_INTEGRATOR_PATH && P->rr_depth <= 0)
+        return fail(ctx, MTSGPU_EINVAL, "'rrDepth' must be set to a value greater than zero!");
+    if (P->integrator == MTSGPU_INTEGRATOR_PATH && P->max_depth <= 0 && P->max_depth != -1)
         return fail(ctx, MTSGPU_EINVAL, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
     const HostScene &H = ctx->host;
     if ((uint64_t)P->x0 + P->width > H.film_w || (uint64_t)P->y0 + P->height > H.film_h)
@@ -291,8 +292,14 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     const uint32_t tilesY = (rowsCompact + 7) / 8;
     L.num_pixels = L.tiles_x * tilesY * 64;
     // Sobol index width: frame << 2m | 2m bits (sobolseq.h:93-125); 52 columns per dimension
+    // the direct integrator's 2D sample arrays index the Sobol sequence at spp x count
+    const bool direct = P->integrator == MTSGPU_INTEGRATOR_DIRECT;
+    if (P->integrator != MTSGPU_INTEGRATOR_PATH && !direct) return fail(ctx, MTSGPU_EINVAL, "unknown integrator");
+    if (direct && P->emitter_samples + P->bsdf_samples == 0)
+        return fail(ctx, MTSGPU_EINVAL, "direct: emitterSamples + bsdfSamples must be positive");
+    const uint64_t perSampleIdx = direct ? std::max<uint64_t>(1, std::max(P->emitter_samples, P->bsdf_samples)) : 1;
     uint32_t sppBits = 0;
-    while ((1ull << sppBits) < (uint64_t)P->spp) ++sppBits;
+    while ((1ull << sppBits) < (uint64_t)P->spp * perSampleIdx) ++sppBits;
     const uint32_t indexBits = (m > 1 ? 2 * m : 0) + sppBits;
     if (indexBits > 52) return fail(ctx, MTSGPU_EINVAL, "sample index exceeds the 52-bit Sobol direction numbers");
     L.nibbles = indexBits <= 32 ? 8 : MTSG_NIBBLES;
@@ -314,6 +321,21 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // LDS as the rest allows (the others are read through L1/L2)
     L.ext = H.ext ? 1u : 0u;
     L.ana = H.analytic.empty() ? 0u : 1u;
+    // MIDirectIntegrator::configure / configureSampler (direct.cpp:128-143)
+    L.integrator = P->integrator;
+    L.array_end = 5;
+    if (direct) {
+        const uint32_t nl = P->emitter_samples, nb = P->bsdf_samples;
+        const size_t sum = (size_t)nl + nb;
+        L.lum_samples = nl;
+        L.bsdf_samples = nb;
+        L.weight_bsdf = 1 / (float)nb;
+        L.weight_lum = 1 / (float)nl;
+        L.frac_bsdf = nb / (float)sum;
+        L.frac_lum = nl / (float)sum;
+        if (nl > 1) { L.lum_dim = L.array_end; L.array_end += 2; }
+        if (nb > 1) { L.bsdf_dim = L.array_end; L.array_end += 2; }
+    }
     L.waves = 3;
     if (!L.scene_lds) {
         const size_t perBlock = (160u << 10) / 4;

@@ -1187,6 +1187,402 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     if (cErr) atomicAdd(L.counters + 6, cErr);
 }
 
+// ===========================================================================
+// The `direct` integrator: MIDirectIntegrator::Li (integrators/direct/direct.cpp:
+// 144-306) at rRec.depth = 1, one lane per (sample, pixel) item.  Per item: the
+// camera ray; at its hit, `emitterSamples` emitter samples (each with its shadow
+// ray) and `bsdfSamples` BSDF samples (each with its closest-hit ray), MIS-
+// weighted with the integrator's fractions and per-technique weights.
+// ===========================================================================
+
+// SobolSampler with requested 2D arrays: next1D/next2D skip dims [5, arrayEnd)
+// (sobol.cpp:219-250)
+__device__ __forceinline__ float next1d_a(const SobolCtx &C, SamplerState &s, uint32_t arrayEnd) {
+    if (s.dim >= 5 && s.dim < arrayEnd) s.dim = arrayEnd;
+    return next1d(C, s);
+}
+__device__ __forceinline__ void next2d_a(const SobolCtx &C, float res, SamplerState &s, int px, int py,
+                                         uint32_t arrayEnd, float &u, float &v) {
+    if (s.dim + 1 >= 5 && s.dim < arrayEnd) s.dim = arrayEnd;
+    next2d(C, res, s, px, py, u, v);
+}
+// element k of the sample's `size`-point 2D array at dimension `dim`: Sampler::
+// next2DArray (sampler.cpp:82-92) over SobolSampler::generate's arrays (sobol.cpp:188-197)
+template <typename T>
+__device__ __forceinline__ void sobol_array2d(const SobolCtx &C, const MtsgLookup &Lu, T *ycolTab, uint32_t nibbles,
+                                              uint32_t j, uint32_t size, uint32_t k, int px, int py,
+                                              uint64_t scramble64, uint32_t dim, float &u, float &v) {
+    const uint32_t frame = j * size + k;
+    const uint64_t idx = Lu.m >= 1 ? sobol_lookup_lds(Lu, ycolTab, nibbles, frame, (uint32_t)px, (uint32_t)py, scramble64)
+                                   : (uint64_t)frame;
+    u = sobol_sample(C, idx, dim);
+    v = sobol_sample(C, idx, dim + 1);
+}
+
+// PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298): origin, direction, [mint, maxt]
+__device__ __forceinline__ void camera_ray(const MtsgCamera &cam, float sx, float sy, f3 &ro, f3 &rd, float &mint,
+                                           float &maxt) {
+    const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+    const f3 dl = normalize(nearP);
+    const float invZ = 1.0f / dl.z;
+    mint = cam.near_clip * invZ;
+    maxt = cam.far_clip * invZ;
+    const float *W = cam.to_world;
+    ro = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
+            W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);
+    rd = mk(W[0] * dl.x + W[1] * dl.y + W[2] * dl.z, W[4] * dl.x + W[5] * dl.y + W[6] * dl.z,
+            W[8] * dl.x + W[9] * dl.y + W[10] * dl.z);
+}
+
+// Scene::evalEnvironment of a camera ray with its (scaled) differentials
+__device__ __forceinline__ f3 env_camera(const MtsgLaunch &L, float sx, float sy, f3 rd) {
+    glb_env *E = (glb_env *)L.scene.env;
+    if (E->constant) return mk(E->radiance[0], E->radiance[1], E->radiance[2]);
+    const MtsgCamera &cam = L.scene.cam;
+    const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+    const f3 rxl = normalize(add(nearP, ld3(cam.dx))), ryl = normalize(add(nearP, ld3(cam.dy)));
+    const float *W = cam.to_world;
+    f3 rxd = mk(W[0] * rxl.x + W[1] * rxl.y + W[2] * rxl.z, W[4] * rxl.x + W[5] * rxl.y + W[6] * rxl.z,
+                W[8] * rxl.x + W[9] * rxl.y + W[10] * rxl.z);
+    f3 ryd = mk(W[0] * ryl.x + W[1] * ryl.y + W[2] * ryl.z, W[4] * ryl.x + W[5] * ryl.y + W[6] * ryl.z,
+                W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
+    rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));
+    ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
+    return env_eval_diff(E, rd, rxd, ryd);
+}
+
+// Scene::sampleEmitterDirect without the visibility test (scene.cpp:828-852):
+// value = radiance / (pdf * emPdf) and pdf = dRec.pdf * emPdf when pdf != 0
+struct NeeSample { f3 value, d; float dist, pdf; };
+template <bool ENV, bool ANA, typename HS>
+__device__ __forceinline__ NeeSample emitter_sample(const MtsgDeviceScene &S, const HS &hs, f3 ref, f3 refN, float ex,
+                                                    float ey) {
+    NeeSample r;
+    r.value = mk(0, 0, 0); r.d = mk(0, 0, 1); r.dist = 0.0f; r.pdf = 0.0f;
+    float emPdf;
+    const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
+    const MtsgEmitter &e = S.emitters[ei];
+    f3 value = mk(0, 0, 0);
+    float pdf = 0.0f;
+    if (ENV && e.type != MTSG_EMITTER_AREA) {
+        glb_env *E = (glb_env *)S.env;
+        const EnvSample es = E->constant ? const_sample_direct(E, ref, refN, ex, ey) : env_sample_direct(E, ref, ex, ey);
+        value = es.value; r.d = es.d; r.dist = es.dist; pdf = es.pdf;
+    } else if (ANA && S.shapes[e.shape].analytic >= 0) {
+        const AnaSample as = ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], ref, ex, ey);
+        r.d = as.d; r.dist = as.dist; pdf = as.pdf;
+        if (dot(r.d, refN) >= 0 && dot(r.d, as.n) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);   // area.cpp:158-173
+        else pdf = 0.0f;
+    } else {
+        // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
+        float py2 = ey;
+        const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
+        const uint32_t prim = e.tri_first + lt;
+        const uint4 pv = make_uint4(hs.pv[4 * prim], hs.pv[4 * prim + 1], hs.pv[4 * prim + 2], hs.pv[4 * prim + 3]);
+        const float a = safe_sqrt(1.0f - ex);
+        const float bx = 1 - a, by = a * py2;
+        const f3 p0 = ldp3(hs.pos + 3 * (size_t)pv.x), p1 = ldp3(hs.pos + 3 * (size_t)pv.y),
+                 p2 = ldp3(hs.pos + 3 * (size_t)pv.z);
+        const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
+        const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
+        f3 ln;
+        if (hs.shapes[e.shape].has_normals) {
+            const f3 n0 = ldp3(hs.nrm + 3 * (size_t)pv.x), n1 = ldp3(hs.nrm + 3 * (size_t)pv.y),
+                     n2 = ldp3(hs.nrm + 3 * (size_t)pv.z);
+            ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
+        } else {
+            ln = normalize(cross(sideA, sideB));
+        }
+        pdf = e.inv_area;
+        r.d = sub(lp, ref);   // Shape::sampleDirect (shape.cpp:102-115)
+        const float distSquared = len2(r.d);
+        r.dist = dsqrt(distSquared);
+        r.d = divs(r.d, r.dist);
+        const float dp = absdot(r.d, ln);
+        pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+        if (dot(r.d, refN) >= 0 && dot(r.d, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+        else pdf = 0.0f;
+    }
+    if (pdf != 0) {
+        r.pdf = pdf * emPdf;
+        r.value = divs(value, emPdf);
+    }
+    return r;
+}
+
+// Scene::pdfEmitterDirect for an area-light hit h reached along d from `ref`
+// (area.cpp:175-181, shape.cpp:117-126 / sphere.cpp:357-387, scene.h:848-850)
+template <bool ANA>
+__device__ __forceinline__ float area_hit_pdf(const MtsgDeviceScene &S, const Hit &h, f3 ref, f3 d, f3 refN) {
+    const MtsgEmitter &e = S.emitters[S.shapes[h.shape].emitter];
+    const f3 dn = h.sh.n;
+    float pdf = 0.0f;
+    if (dot(d, refN) >= 0 && dot(d, dn) < 0) {
+        if (ANA && S.shapes[h.shape].analytic >= 0)
+            pdf = ana_pdf_direct(((GAna *)S.analytic)[S.shapes[h.shape].analytic], ref, d, dn, h.t);
+        else
+            pdf = e.inv_area * (h.t * h.t) / absdot(d, dn);
+    }
+    return pdf * (e.weight * S.em_norm);
+}
+
+// BSDF eval/pdf/sample through a twosided wrapper (twosided.cpp:105-172)
+template <bool EXT>
+__device__ __forceinline__ void bsdf_eval_pdf_2s(const MtsgDeviceScene &S, GBsdf &bsdf, const Hit &h, f3 wo, f3 &val,
+                                                 float *pdf) {
+    f3 qwi = h.wi, qwo = wo;
+    GBsdf *qb = &bsdf;
+    if constexpr (EXT) {
+        if (bsdf.type == BSDF_TWOSIDED) {
+            const bool flip = !(qwi.z > 0);
+            qb = &((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
+            if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
+        }
+    }
+    val = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+    if (pdf) *pdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+}
+template <bool EXT>
+__device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsdf &bsdf, const Hit &h, float bx,
+                                                  float by, float u1d) {
+    if (EXT && bsdf.type == BSDF_TWOSIDED) {
+        const bool flip = h.wi.z < 0;
+        f3 qwi = h.wi;
+        if (flip) qwi.z = -qwi.z;
+        BSample bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
+                                      u1d, h.u, h.v);
+        if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
+        return bs;
+    }
+    return bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
+}
+
+template <bool SCENE_LDS, int FEAT>
+__global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLaunch L) {
+    constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
+                   ANA = (FEAT & MTSG_FEAT_ANA) != 0;
+    extern __shared__ uint32_t lds[];
+    const MtsgDeviceScene &S = L.scene;
+    // LDS as path_kernel: [Sobol nibble tables][look_up column tables][scene (small scenes)][stacks]
+    const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
+    for (uint32_t i = threadIdx.x; i < tabWords; i += BLOCK) {
+        const uint32_t d = i / (L.nibbles * 16), r = i % (L.nibbles * 16);
+        lds[i] = L.sobol_nib[(size_t)d * MTSG_NIBBLES * 16 + r];
+    }
+    for (uint32_t i = threadIdx.x; i < 16 * 16; i += BLOCK) {
+        const uint32_t c = i >> 4, v = i & 15;
+        uint32_t r = 0;
+        for (int b = 0; b < 4; ++b)
+            if ((v >> b) & 1) r ^= L.lut.ycol[4 * c + b];
+        lds[tabWords + i] = r;
+    }
+    const uint32_t base2 = tabWords + 16 * 16;
+    uint32_t sceneWords = 0;
+    if (SCENE_LDS) {
+        const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
+        const uint32_t *gn = reinterpret_cast<const uint32_t *>(S.nodes);
+        const uint32_t *gt = reinterpret_cast<const uint32_t *>(S.tris);
+        for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[base2 + i] = gn[i];
+        for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[base2 + nodeWords + i] = gt[i];
+        sceneWords = nodeWords + triWords;
+        const uint32_t np = S.num_prims, nv = L.num_verts, ns = L.num_shapes * (sizeof(MtsgShape) / 4);
+        const uint32_t *srcs[5] = {S.prim_vtx, reinterpret_cast<const uint32_t *>(S.dpdu),
+                                   reinterpret_cast<const uint32_t *>(S.positions),
+                                   reinterpret_cast<const uint32_t *>(S.normals),
+                                   reinterpret_cast<const uint32_t *>(S.shapes)};
+        const uint32_t lens[5] = {4 * np, 3 * np, 3 * nv, 3 * nv, ns};
+        for (int a = 0; a < 5; ++a) {
+            for (uint32_t i = threadIdx.x; i < lens[a]; i += BLOCK) lds[base2 + sceneWords + i] = srcs[a][i];
+            sceneWords += lens[a];
+        }
+    }
+    __syncthreads();
+    lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
+    lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
+    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
+    HitSrc<SCENE_LDS> hs;
+    if constexpr (SCENE_LDS) {
+        const uint32_t np = S.num_prims, nv = L.num_verts;
+        lds_u32 *b = (lds_u32 *)(lds + base2 + L.num_nodes * 16 + np * 12);
+        hs.pv = b;
+        hs.dpdu = (lds_f32 *)(b + 4 * np);
+        hs.pos = (lds_f32 *)(b + 7 * np);
+        hs.nrm = (lds_f32 *)(b + 7 * np + 3 * nv);
+        hs.shapes = (lds_shape *)(b + 7 * np + 6 * nv);
+    } else {
+        hs.pv = (glb_u32 *)S.prim_vtx;
+        hs.dpdu = (glb_f32 *)S.dpdu;
+        hs.pos = (glb_f32 *)S.positions;
+        hs.nrm = (glb_f32 *)S.normals;
+        hs.shapes = (glb_shape *)S.shapes;
+    }
+    SobolCtx SC;
+    SC.lds = (lds_u32 *)lds;
+    SC.glob = (glb_u32 *)L.sobol_nib;
+    SC.lds_dims = L.lds_dims;
+    SC.nibbles = L.nibbles;
+    SC.scramble = L.scramble;
+    lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
+    unsigned long long cRays = 0, cShadow = 0, cSamples = 0, cErr = 0, cN = 0, cT = 0;
+
+    // closest hit / occlusion through the scene's structure (scan, LDS BVH or HBM BVH)
+    auto closest = [&](f3 o, f3 d, float rmint, float rmaxt, Hit &h) -> bool {
+        cRays++;
+        float mint, maxt;
+        uint32_t slot = 0;
+        float hu = 0, hv = 0, ht = 0;
+        bool hit = false;
+        if (ray_interval(S, o, d, rmint, rmaxt, false, mint, maxt)) {
+            if (SCENE_LDS && L.scan)
+                hit = scan_tris<false, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+            else if (SCENE_LDS)
+                hit = traverse<false, false, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht, cN,
+                                                  cT, S.analytic);
+            else
+                hit = traverse<false, false, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
+                                                  slot, hu, hv, ht, cN, cT, S.analytic);
+        }
+        if (hit) {
+            const uint32_t prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+            fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, o, d, h);
+        } else {
+            h = Hit{};
+        }
+        return hit;
+    };
+    // Shadow rays run the closest-hit traversal: the same occlusion answer as
+    // the any-hit instantiation, which hipcc (ROCm 7.2) miscompiles inside
+    // this kernel ("direct integrator")
+    auto occluded = [&](f3 o, f3 d, float dist) -> bool {   // Ray(ref, d, Epsilon, dist*(1-ShadowEpsilon))
+        cShadow++;
+        float mint, maxt;
+        if (!ray_interval(S, o, d, D_EPSILON, dist * (1 - D_SHADOW_EPSILON), true, mint, maxt)) return false;
+        uint32_t sl; float a0, a1, a2;
+        if (SCENE_LDS && L.scan)
+            return scan_tris<false, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, sl, a0, a1, a2, cT);
+        if (SCENE_LDS)
+            return traverse<false, false, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, sl, a0, a1, a2, cN, cT,
+                                               S.analytic);
+        return traverse<false, false, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD, sl, a0,
+                                           a1, a2, cN, cT, S.analytic);
+    };
+
+    const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
+    for (uint64_t it = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; it < L.num_items; it += lanes) {
+        const uint32_t jj = (uint32_t)(it / L.num_pixels);
+        const uint32_t pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
+        int px, py;
+        if (!pixel_of(L, pix, px, py)) continue;
+        const uint32_t j = L.j0 + jj;
+        SamplerState smp;
+        smp.dim = 0;
+        smp.sampleIndex = j;
+        smp.err = false;
+        smp.sobolIndex = (L.lut.m > 1) ? sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py,
+                                                          L.scramble64)
+                                       : (uint64_t)j;
+        float u, v;
+        next2d(SC, L.resolution, smp, px, py, u, v);
+        const float sx = (float)px + u, sy = (float)py + v;
+        f3 ro, rd;
+        float rmint, rmaxt;
+        camera_ray(S.cam, sx, sy, ro, rd, rmint, rmaxt);
+        f3 Li = mk(0, 0, 0);
+        Hit its;
+        const bool hit = closest(ro, rd, rmint, rmaxt, its);
+        const float alpha = L.has_alpha ? (hit ? 1.0f : 0.0f) : 1.0f;
+        if (!hit) {
+            if (ENV && !L.hide_emitters) Li = env_camera(L, sx, sy, rd);
+        } else {
+            auto &sh = hs.shapes[its.shape];
+            GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
+            if (sh.emitter >= 0 && !L.hide_emitters) Li = add(Li, area_Le(S, its, neg(rd)));
+            if (!(L.strict_normals && dot(rd, its.geoN) * its.wi.z >= 0)) {
+                const f3 refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? its.sh.n : mk(0, 0, 0);
+                // emitter sampling (direct.cpp:199-239)
+                float su = 0, sv = 0;
+                if (L.lum_samples <= 1) next2d_a(SC, L.resolution, smp, px, py, L.array_end, su, sv);
+                if (bsdf.flags & MTSG_F_SMOOTH) {
+                    for (uint32_t i = 0; i < L.lum_samples; ++i) {
+                        float nx = su, ny = sv;
+                        if (L.lum_samples > 1)
+                            sobol_array2d(SC, L.lut, ycolTab, L.nibbles, j, L.lum_samples, i, px, py, L.scramble64,
+                                          L.lum_dim, nx, ny);
+                        NeeSample ns = emitter_sample<ENV, ANA>(S, hs, its.p, refN, nx, ny);
+                        if (ns.pdf != 0 && occluded(its.p, ns.d, ns.dist)) ns.value = mk(0, 0, 0);
+                        if (ns.pdf == 0) ns.value = mk(0, 0, 0);
+                        if (!is_zero(ns.value)) {
+                            const f3 wo = to_local(its.sh, ns.d);
+                            f3 bsdfVal;
+                            float bsdfPdf;
+                            bsdf_eval_pdf_2s<EXT>(S, bsdf, its, wo, bsdfVal, &bsdfPdf);
+                            if (!is_zero(bsdfVal) && (!L.strict_normals || dot(its.geoN, ns.d) * wo.z > 0)) {
+                                const float pa = ns.pdf * L.frac_lum, pb = bsdfPdf * L.frac_bsdf;
+                                const float weight = (pa * pa) / (pa * pa + pb * pb) * L.weight_lum;
+                                Li = add(Li, mul(mulv(ns.value, bsdfVal), weight));
+                            }
+                        }
+                    }
+                }
+                // BSDF sampling (direct.cpp:241-304)
+                if (L.bsdf_samples <= 1) next2d_a(SC, L.resolution, smp, px, py, L.array_end, su, sv);
+                for (uint32_t i = 0; i < L.bsdf_samples; ++i) {
+                    float bx = su, by = sv;
+                    if (L.bsdf_samples > 1)
+                        sobol_array2d(SC, L.lut, ycolTab, L.nibbles, j, L.bsdf_samples, i, px, py, L.scramble64,
+                                      L.bsdf_dim, bx, by);
+                    float u1d = 0.0f;
+                    if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d_a(SC, smp, L.array_end);
+                    const BSample bs = bsdf_sample_2s<EXT>(S, bsdf, its, bx, by, u1d);
+                    if (is_zero(bs.weight)) continue;
+                    const f3 wo = to_world(its.sh, bs.wo);
+                    if (L.strict_normals && dot(its.geoN, wo) * bs.wo.z <= 0) continue;
+                    Hit h2;
+                    f3 value;
+                    float lumPdf = 0.0f;
+                    if (closest(its.p, wo, D_EPSILON, INFINITY, h2)) {
+                        if (hs.shapes[h2.shape].emitter < 0) continue;
+                        value = area_Le(S, h2, neg(wo));
+                        if (!(bs.sampledType & MTSG_F_DELTA)) lumPdf = area_hit_pdf<ANA>(S, h2, its.p, wo, refN);
+                    } else {
+                        if (!ENV || (L.hide_emitters && bs.sampledType == MTSG_F_NULL)) continue;
+                        glb_env *E = (glb_env *)S.env;
+                        value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : env_eval(E, wo);
+                        float nT, fT;
+                        if (!env_bsphere(E, its.p, wo, nT, fT) || nT > 0 || fT < 0) continue;
+                        if (!(bs.sampledType & MTSG_F_DELTA))
+                            lumPdf = (E->constant ? const_pdf_direct(wo, refN) : env_pdf_direction(E, wo)) *
+                                     (S.emitters[S.env_emitter].weight * S.em_norm);
+                    }
+                    const float pa = bs.pdf * L.frac_bsdf, pb = lumPdf * L.frac_lum;
+                    const float weight = (pa * pa) / (pa * pa + pb * pb) * L.weight_bsdf;
+                    Li = add(Li, mul(mulv(value, bs.weight), weight));
+                }
+            }
+        }
+        // block->put(samplePos, spec, alpha) (integrator.cpp:184), as path_kernel
+        const float val[5] = {Li.x, Li.y, Li.z, alpha, 1.0f};
+        float ownW = 0.0f;
+        const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
+        float4 rec4 = valid ? make_float4(Li.x, Li.y, Li.z, alpha == 0.0f ? -ownW : ownW) : make_float4(0, 0, 0, 0);
+        reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
+        if (L.samples) {
+            const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
+            float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
+            rec[0] = Li.x; rec[1] = Li.y; rec[2] = Li.z; rec[3] = alpha;
+            rec[4] = sx; rec[5] = sy; rec[6] = 1.0f; rec[7] = smp.err ? 1.0f : 0.0f;
+        }
+        cSamples++;
+        if (smp.err) cErr++;
+    }
+    atomicAdd(L.counters + 0, cSamples);
+    atomicAdd(L.counters + 1, cRays);
+    atomicAdd(L.counters + 2, cShadow);
+    atomicAdd(L.counters + 3, cSamples);   // rRec.depth = 1 per sample
+    if (cErr) atomicAdd(L.counters + 6, cErr);
+}
+
 // Scene::rayIntersect / Scene::isOccluded on a batch of rays (one ray per lane):
 // rays[2i] = {o, mint}, rays[2i+1] = {d, maxt}; out[i] = {t, u, v, prim bits}
 // (prim 0xffffffff and t = inf: no hit; the shadow query writes t = 1 / 0)
@@ -1296,8 +1692,26 @@ int mtsg_path_features(const MtsgLaunch &L) {
            (L.ana ? MTSG_FEAT_ANA : 0);
 }
 
+template <int FEAT>
+static void launch_direct(const MtsgLaunch &L, int grid, hipStream_t stream) {
+    const size_t lds = mtsg_path_lds_bytes(L);
+    if (L.scene_lds) hipLaunchKernelGGL((direct_kernel<true, FEAT>), dim3(grid), dim3(BLOCK), lds, stream, L);
+    else hipLaunchKernelGGL((direct_kernel<false, FEAT>), dim3(grid), dim3(BLOCK), lds, stream, L);
+}
+
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream) {
     const bool instr = samples || stats;
+    if (L.integrator == MTSG_INTEGRATOR_DIRECT) {
+        switch (mtsg_path_features(L)) {
+            case 0: launch_direct<0>(L, grid, stream); break;
+            case MTSG_FEAT_ENV: launch_direct<MTSG_FEAT_ENV>(L, grid, stream); break;
+            case MTSG_FEAT_EXT: launch_direct<MTSG_FEAT_EXT>(L, grid, stream); break;
+            case MTSG_FEAT_ENV | MTSG_FEAT_EXT: launch_direct<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, stream); break;
+            case MTSG_FEAT_EXT | MTSG_FEAT_ANA: launch_direct<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, stream); break;
+            default: launch_direct<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, stream); break;
+        }
+        return hipGetLastError();
+    }
     switch (mtsg_path_features(L)) {
         case 0: launch_path<0>(L, grid, instr, stream); break;
         case MTSG_FEAT_ENV: launch_path<MTSG_FEAT_ENV>(L, grid, instr, stream); break;

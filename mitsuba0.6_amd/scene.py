@@ -373,6 +373,34 @@ class PathIntegrator:
         p.width = width - x0 if w is None else w
         p.height = height - y0 if h is None else h
         p.row_block, p.row_stride, p.row_phase = row_block, row_stride, row_phase
+        p.integrator = abi.INTEGRATOR_PATH
+        return p
+
+
+@dataclass
+class DirectIntegrator(PathIntegrator):
+    """Properties of the reference `direct` plugin (MIDirectIntegrator,
+    src/integrators/direct/direct.cpp:90-135): `shadingSamples` sets both
+    `emitterSamples` and `bsdfSamples` unless given; strictNormals/hideEmitters
+    as in `path`.  Sampler and film settings as PathIntegrator (maxDepth and
+    rrDepth are unused)."""
+    shadingSamples: int = 1
+    emitterSamples: Optional[int] = None
+    bsdfSamples: Optional[int] = None
+
+    def __post_init__(self):
+        super().__post_init__()
+        if self.emitterSamples is None:
+            self.emitterSamples = self.shadingSamples
+        if self.bsdfSamples is None:
+            self.bsdfSamples = self.shadingSamples
+        if self.emitterSamples + self.bsdfSamples <= 0 or min(self.emitterSamples, self.bsdfSamples) < 0:
+            raise ValueError('direct: emitterSamples + bsdfSamples must be positive (direct.cpp:106)')
+
+    def params(self, *a, **kw):
+        p = super().params(*a, **kw)
+        p.integrator = abi.INTEGRATOR_DIRECT
+        p.emitter_samples, p.bsdf_samples = self.emitterSamples, self.bsdfSamples
         return p
 
 

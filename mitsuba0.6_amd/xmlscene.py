@@ -35,7 +35,7 @@ import numpy as np
 from .film import HDRFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
 from .obj import load_obj, srgb_to_linear, strtof
 from .ply import load_ply
-from .scene import BSDF, Checkerboard, Emitter, Mesh, PathIntegrator, Scene, Sensor
+from .scene import BSDF, Checkerboard, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor
 from .serialized import load_serialized
 from .transform import Transform, _cross, _normalize, normalize_rows
 
@@ -468,8 +468,14 @@ class XMLSceneLoader:
     def _integrator(self, p):
         if p is None:
             raise SceneError('no <integrator> (the GPU path implements "path")')
+        if p.plugin == 'direct':                     # direct.cpp:92-107
+            n = int(p.get('shadingSamples', 1))
+            return DirectIntegrator(shadingSamples=n, emitterSamples=int(p.get('emitterSamples', n)),
+                                    bsdfSamples=int(p.get('bsdfSamples', n)),
+                                    strictNormals=p.get('strictNormals', False),
+                                    hideEmitters=p.get('hideEmitters', False))
         if p.plugin != 'path':
-            raise NotImplementedError('integrator "%s" (only "path" is on the GPU path)' % p.plugin)
+            raise NotImplementedError('integrator "%s" (the GPU path implements "path" and "direct")' % p.plugin)
         return PathIntegrator(maxDepth=p.get('maxDepth', -1), rrDepth=p.get('rrDepth', 5),
                               strictNormals=p.get('strictNormals', False), hideEmitters=p.get('hideEmitters', False))
 
@@ -670,9 +676,14 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     os.makedirs(directory, exist_ok=True)
     from .ply import write_ply
     L = ['<?xml version="1.0" encoding="utf-8"?>', '<scene version="0.6.0">']
-    L.append('  <integrator type="path">')
-    L.append('    <integer name="maxDepth" value="%d"/>' % integ.maxDepth)
-    L.append('    <integer name="rrDepth" value="%d"/>' % integ.rrDepth)
+    if isinstance(integ, DirectIntegrator):
+        L.append('  <integrator type="direct">')
+        L.append('    <integer name="emitterSamples" value="%d"/>' % integ.emitterSamples)
+        L.append('    <integer name="bsdfSamples" value="%d"/>' % integ.bsdfSamples)
+    else:
+        L.append('  <integrator type="path">')
+        L.append('    <integer name="maxDepth" value="%d"/>' % integ.maxDepth)
+        L.append('    <integer name="rrDepth" value="%d"/>' % integ.rrDepth)
     L.append('    <boolean name="strictNormals" value="%s"/>' % str(bool(integ.strictNormals)).lower())
     L.append('    <boolean name="hideEmitters" value="%s"/>' % str(bool(integ.hideEmitters)).lower())
     L.append('  </integrator>')

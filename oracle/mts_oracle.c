@@ -444,6 +444,7 @@ typedef struct {
     int px, py;
     uint64_t sampleIndex, sobolIndex;
     uint32_t dim;
+    uint32_t arrayEnd; /* m_arrayEndDim: dims [5, arrayEnd) hold the requested 2D arrays */
     int err;
 } Sampler;
 
@@ -457,6 +458,7 @@ static void sampler_init(Sampler *s, uint64_t scramble, uint32_t w, uint32_t h) 
     s->resolution = (float)r;
     uint32_t lg = 0; while ((1u << lg) < r) ++lg;
     s->logRes = lg;
+    s->arrayEnd = 5;
 }
 
 static void sampler_set_index(Sampler *s, uint64_t idx) { /* sobol.cpp:204-217 */
@@ -469,13 +471,13 @@ static void sampler_set_index(Sampler *s, uint64_t idx) { /* sobol.cpp:204-217 *
 }
 static void sampler_generate(Sampler *s, int px, int py) { s->px = px; s->py = py; sampler_set_index(s, 0); }
 
-static float next1d(Sampler *s) { /* sobol.cpp:219-229; arrays [5,5) are empty */
-    if (s->dim >= 5 && s->dim < 5) s->dim = 5;
+static float next1d(Sampler *s) { /* sobol.cpp:219-229; dims [5, arrayEnd) are the arrays' */
+    if (s->dim >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
     if (s->dim >= SOBOL_DIMS) { s->err = 1; return 0.0f; }
     return oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
 }
 static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
-    if (s->dim + 1 >= 5 && s->dim < 5) s->dim = 5;
+    if (s->dim + 1 >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
     if (s->dim + 1 >= SOBOL_DIMS) { s->err = 1; *u = *v = 0.0f; return; }
     if (s->dim == 0 && s->sobolIndex != s->sampleIndex) {
         *u = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble) * s->resolution - (float)s->px;
@@ -484,6 +486,16 @@ static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
         *u = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
         *v = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
     }
+}
+
+/* element k of this sample's requested 2D array of `size` points starting at
+ * dimension `dim`: Sampler::next2DArray (sampler.cpp:82-92) over the arrays
+ * SobolSampler::generate fills (sobol.cpp:171-197) */
+static void sampler_array2d(const Sampler *s, uint32_t dim, uint32_t size, uint32_t k, float *u, float *v) {
+    uint32_t j = (uint32_t)(s->sampleIndex * size + k);
+    uint64_t idx = oracle_sobol_lookup(s->logRes, j, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
+    *u = oracle_sobol_sample(idx, dim, (uint32_t)s->scramble);
+    *v = oracle_sobol_sample(idx, dim + 1, (uint32_t)s->scramble);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -3115,6 +3127,111 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
 }
 
 /* ------------------------------------------------------------------------ */
+/* MIDirectIntegrator::Li (integrators/direct/direct.cpp:144-306), rRec.depth = 1 */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    uint32_t nLum, nBSDF;          /* m_emitterSamples, m_bsdfSamples */
+    float weightLum, weightBSDF, fracLum, fracBSDF;
+    uint32_t lumDim, bsdfDim;      /* first dimension of each requested 2D array */
+} DirectParams;
+
+static void direct_configure(uint32_t nLum, uint32_t nBSDF, DirectParams *D, Sampler *smp) { /* :128-143 */
+    size_t sum = nLum + nBSDF;
+    D->nLum = nLum; D->nBSDF = nBSDF;
+    D->weightBSDF = 1 / (float)nBSDF;
+    D->weightLum = 1 / (float)nLum;
+    D->fracBSDF = nBSDF / (float)sum;
+    D->fracLum = nLum / (float)sum;
+    uint32_t dim = 5;
+    if (nLum > 1) { D->lumDim = dim; dim += 2; }
+    if (nBSDF > 1) { D->bsdfDim = dim; dim += 2; }
+    smp->arrayEnd = dim;
+}
+
+static V3 Li_direct(const Scene *S, const PathParams *P, const DirectParams *D, Ray ray, Sampler *smp, float *alpha,
+                    Counters *C) {
+    Its its;
+    V3 L = v3(0, 0, 0);
+    scene_intersect(S, &ray, &its, C);
+    *alpha = P->hasAlpha ? (its.valid ? 1.0f : 0.0f) : 1.0f;
+    if (!its.valid) {
+        if (S->env && !P->hide) return env_eval(S->env, &ray);
+        return L;
+    }
+    if (S->meshes[its.mesh].emitter >= 0 && !P->hide) L = vadd(L, its_Le(S, &its, vneg(ray.d)));
+    const Bsdf *bsdf = &S->bsdfs[S->meshes[its.mesh].bsdf];
+    if (P->strict && vdot(ray.d, its.geoN) * its.wi.z >= 0) return L;
+
+    /* emitter sampling */
+    float u2[2];
+    if (D->nLum <= 1) next2d(smp, &u2[0], &u2[1]);
+    DRec dRec;
+    memset(&dRec, 0, sizeof dRec);
+    dRec.ref = its.p;
+    dRec.refN = (bsdf->flags & (E_TRANSMISSION | E_BACK)) == 0 ? its.sh.n : v3(0, 0, 0);
+    if (bsdf->flags & E_SMOOTH) {
+        for (uint32_t i = 0; i < D->nLum; ++i) {
+            float nx = u2[0], ny = u2[1];
+            if (D->nLum > 1) sampler_array2d(smp, D->lumDim, D->nLum, i, &nx, &ny);
+            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C);
+            if (!vzero(value)) {
+                BRec bRec;
+                bRec.wi = its.wi;
+                bRec.wo = to_local(&its.sh, dRec.d);
+                bRec.u = its.u; bRec.v = its.v;
+                V3 bsdfVal = bsdf_eval(bsdf, &bRec);
+                if (!vzero(bsdfVal) && (!P->strict || vdot(its.geoN, dRec.d) * bRec.wo.z > 0)) {
+                    float bsdfPdf = bsdf_pdf(bsdf, &bRec); /* emitter->isOnSurface(): all of ours */
+                    float weight = mi_weight(dRec.pdf * D->fracLum, bsdfPdf * D->fracBSDF) * D->weightLum;
+                    L = vadd(L, vmul(vmulv(value, bsdfVal), weight));
+                }
+            }
+        }
+    }
+
+    /* BSDF sampling */
+    if (D->nBSDF <= 1) next2d(smp, &u2[0], &u2[1]);
+    for (uint32_t i = 0; i < D->nBSDF; ++i) {
+        float bx = u2[0], by = u2[1];
+        if (D->nBSDF > 1) sampler_array2d(smp, D->bsdfDim, D->nBSDF, i, &bx, &by);
+        float bsdfPdf;
+        BRec bRec;
+        bRec.wi = its.wi; bRec.eta = 1.0f; bRec.sampledType = 0; bRec.u = its.u; bRec.v = its.v;
+        V3 bsdfVal = bsdf_sample(bsdf, &bRec, &bsdfPdf, bx, by, smp);
+        if (vzero(bsdfVal)) continue;
+        const V3 wo = to_world(&its.sh, bRec.wo);
+        float woDotGeoN = vdot(its.geoN, wo);
+        if (P->strict && woDotGeoN * bRec.wo.z <= 0) continue;
+        Ray bray;
+        bray.o = its.p; ray_set_dir(&bray, wo); bray.mint = EPSILON; bray.maxt = INFINITY; bray.hasDiff = 0;
+        Its bits;
+        V3 value;
+        scene_intersect(S, &bray, &bits, C);
+        if (bits.valid) {
+            if (S->meshes[bits.mesh].emitter < 0) continue;
+            value = its_Le(S, &bits, vneg(bray.d));
+            dRec.p = bits.p; dRec.n = bits.sh.n; dRec.measureSolidAngle = 1;
+            dRec.emitter = S->meshes[bits.mesh].emitter; dRec.d = bray.d; dRec.dist = bits.t;
+        } else {
+            if (!S->env || (P->hide && bRec.sampledType == E_NULL)) continue;
+            value = env_eval(S->env, &bray);
+            float nearT, farT;
+            if (!env_bsphere(S->env, bray.o, bray.d, &nearT, &farT) || nearT > 0 || farT < 0) continue;
+            dRec.p = ray_at(&bray, farT);
+            dRec.n = vnormalize(vsub(S->env->center, dRec.p));
+            dRec.measureSolidAngle = 1;
+            dRec.emitter = S->envIndex;
+            dRec.d = bray.d;
+            dRec.dist = farT;
+        }
+        float lumPdf = !(bRec.sampledType & E_DELTA) ? pdf_emitter_direct(S, &dRec) : 0;
+        float weight = mi_weight(bsdfPdf * D->fracBSDF, lumPdf * D->fracLum) * D->weightBSDF;
+        L = vadd(L, vmul(vmulv(value, bsdfVal), weight));
+    }
+    return L;
+}
+
+/* ------------------------------------------------------------------------ */
 /* film: ImageBlock::put (render/imageblock.h:124-204) + rfilter LUT          */
 /* (libcore/rfilter.cpp:37-55, rfilters/box.cpp, rfilters/gaussian.cpp)       */
 /* ------------------------------------------------------------------------ */
@@ -3204,7 +3321,10 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
                   float *film, float *samples, mtsgpu_stats *stats, int libm_mode, int threads) {
     if (!g_sobol_ready) return MTSGPU_ESTATE;
     if (!scene || !P || !film) return MTSGPU_EINVAL;
-    if (P->spp == 0 || P->rr_depth <= 0 || (P->max_depth <= 0 && P->max_depth != -1)) return MTSGPU_EINVAL;
+    const int direct = P->integrator == MTSGPU_INTEGRATOR_DIRECT;
+    if (P->integrator != MTSGPU_INTEGRATOR_PATH && !direct) return MTSGPU_EINVAL;
+    if (P->spp == 0 || (!direct && (P->rr_depth <= 0 || (P->max_depth <= 0 && P->max_depth != -1)))) return MTSGPU_EINVAL;
+    if (direct && P->emitter_samples + P->bsdf_samples == 0) return MTSGPU_EINVAL;
     g_cr = libm_mode;
     Scene S;
     int rc = scene_configure(scene, &S);
@@ -3233,6 +3353,9 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
         if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
         Sampler smp;
         sampler_init(&smp, P->scramble, P->width, P->height);   /* crop size (integrator.cpp:37-41) */
+        DirectParams DP;
+        memset(&DP, 0, sizeof DP);
+        if (direct) direct_configure(P->emitter_samples, P->bsdf_samples, &DP, &smp); /* configureSampler */
         sampler_generate(&smp, px, py);
         Counters C = {0, 0, 0, 0};
         for (uint32_t j = 0; j < P->spp; ++j) {
@@ -3246,8 +3369,8 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
             ray.ryO = vadd(ray.o, vmul(vsub(ray.ryO, ray.o), diffScale));
             ray.rxD = vadd(ray.d, vmul(vsub(ray.rxD, ray.d), diffScale));
             ray.ryD = vadd(ray.d, vmul(vsub(ray.ryD, ray.d), diffScale));
-            float alpha; int depth;
-            V3 L = Li(&S, &PP, ray, &smp, &alpha, &depth, &C);
+            float alpha; int depth = 1;
+            V3 L = direct ? Li_direct(&S, &PP, &DP, ray, &smp, &alpha, &C) : Li(&S, &PP, ray, &smp, &alpha, &depth, &C);
             if (smp.err) err = 1;
             pathLen += (uint64_t)depth; nsamples++;
             float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};

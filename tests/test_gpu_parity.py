@@ -233,6 +233,31 @@ def test_constant_emitter_bitexact(gpu_ctx, oracle):
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
 
+@pytest.mark.parametrize('counts', [(1, 1), (4, 2), (2, 3)])
+def test_direct_integrator_bitexact(gpu_ctx, oracle, counts):
+    """direct.cpp on the GPU: emitter and BSDF samples per shading point, the
+    sampler's 2D arrays for counts > 1, MIS fractions and weights."""
+    from mitsuba_amd.scene import DirectIntegrator
+    sc, _ = scenes.build('C1', width=40, height=32, spp=8, materials='smooth')
+    d = DirectIntegrator(sampleCount=8, rfilter='box', emitterSamples=counts[0], bsdfSamples=counts[1])
+    gpu_ctx.upload(sc)
+    film_g, smp_g, st_g = gpu_ctx.render(d, samples=True)
+    film_o, smp_o, st_o = oracle.render(sc, d, samples=True, libm_mode=1)
+    _compare(film_g, smp_g, film_o, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
+def test_direct_integrator_envmap_and_shapes(gpu_ctx, oracle):
+    from mitsuba_amd.scene import DirectIntegrator
+    for sc, _ in (_c3_small(area_light=True), scenes.build('C1', width=32, height=32, spp=4, materials='shapes')):
+        d = DirectIntegrator(sampleCount=4, rfilter='box', emitterSamples=2, bsdfSamples=2)
+        gpu_ctx.upload(sc)
+        film_g, smp_g, _ = gpu_ctx.render(d, samples=True)
+        film_o, smp_o, _ = oracle.render(sc, d, samples=True, libm_mode=1)
+        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
+        assert same.mean() > 0.999, same.mean()
+
+
 def _random_rays(sc, n, seed):
     rng = np.random.default_rng(seed)
     lo = np.min([m.positions.min(0) for m in sc.meshes if not m.analytic], 0)
