@@ -1,4 +1,5 @@
-"""`hdrfilm`: film output of the GPU path -- develop + OpenEXR / PFM / RGBE files.
+"""`hdrfilm` and `mfilm`: film output of the GPU path -- develop + OpenEXR /
+PFM / RGBE files (hdrfilm), MATLAB / Mathematica text or NumPy `.npy` (mfilm).
 
 Mirrors HDRFilm (src/films/hdrfilm.cpp:205-360, 481-535):
 - The property names, defaults and errors of the constructor (raised as
@@ -141,6 +142,135 @@ class HDRFilm:
         else:
             write_rgbe(path, image)
         return path
+
+
+MFILM_EXTENSIONS = {'matlab': '.m', 'mathematica': '.m', 'numpy': '.npy'}
+
+
+@dataclass
+class MFilm:
+    """The `mfilm` plugin (src/films/mfilm.cpp:81-396): MATLAB / Mathematica
+    ASCII or NumPy `.npy` output of the developed film.
+
+    Its storage and develop are hdrfilm's: the same ImageBlock, converted by
+    Bitmap::convert(pixelFormat, EFloat) (mfilm.cpp:264-265), so `develop()`
+    runs the same device kernel with the component format fixed to float32.
+    Film defaults that differ from hdrfilm's: 1x1 pixels (film.cpp:27-33) and
+    a box filter (mfilm.cpp:156-165); both are applied by the XML loader."""
+    fileFormat: str = 'matlab'
+    pixelFormat: str = 'luminance'
+    digits: int = 4
+    variable: str = 'data'
+    banner = False
+
+    def __post_init__(self):
+        fmt = self.pixelFormat.lower()
+        if fmt in ('spectrum', 'spectrumalpha'):       # mfilm.cpp:118-121
+            raise ValueError('You requested to render a spectral image, but Mitsuba is currently configured '
+                             'for a RGB flow (i.e. SPECTRUM_SAMPLES = 3).')
+        if fmt not in PIXEL_FORMATS:                    # mfilm.cpp:96-116
+            raise ValueError('The "pixelFormat" parameter must either be equal to "luminance", "luminanceAlpha", '
+                             '"rgb", "rgba", "xyz", "xyza", "spectrum", or "spectrumAlpha"!')
+        self.fileFormat = self.fileFormat.lower()
+        if self.fileFormat not in MFILM_EXTENSIONS:      # mfilm.cpp:123-132
+            raise ValueError('The "fileFormat" parameter must either be equal to "matlab" or "mathematica" or '
+                             '"numpy" or "numpycompressed"!')
+        self._fmt = fmt
+        self.digits = int(self.digits)
+        self.componentFormat = 'float32'
+
+    @property
+    def pixel_format(self):
+        return self._fmt
+
+    @property
+    def channel_names(self):
+        return list(PIXEL_FORMATS[self._fmt][1])
+
+    @property
+    def hasAlpha(self):
+        """MFilm::hasAlpha (mfilm.cpp:366-372)."""
+        return self._fmt in ('luminancealpha', 'rgba', 'xyza')
+
+    develop_params = HDRFilm.develop_params
+    output_array = HDRFilm.output_array
+
+    def develop(self, ctx, film, border):
+        """Bitmap::convert(pixelFormat, EFloat) on the device: (H, W, C) float32."""
+        return ctx.develop(film, border, self)
+
+    def output_path(self, dest):
+        """mfilm.cpp:251-262: `.m` for matlab/mathematica, `.npy` for numpy."""
+        root, ext = os.path.splitext(str(dest))
+        proper = MFILM_EXTENSIONS[self.fileFormat]
+        return str(dest) if ext.lower() == proper else root + proper
+
+    def write(self, dest, image):
+        path = self.output_path(dest)
+        if self.fileFormat == 'numpy':
+            write_npy(path, image)
+        else:
+            with open(path, 'w') as f:
+                f.write(mfilm_text(image, self.fileFormat, self.digits, self.variable))
+        return path
+
+
+def _fmt_g(x, digits):
+    """`os << std::setprecision(digits) << float` (libstdc++: printf "%.*g" of the value as double)."""
+    x = float(x)
+    if x != x:
+        return '-nan' if np.signbit(x) else 'nan'
+    return '%.*g' % (digits, x)
+
+
+def mfilm_text(img, fileFormat, digits=4, variable='data'):
+    """The MATLAB / Mathematica ASCII text MFilm::develop writes (mfilm.cpp:269-334)."""
+    img = np.asarray(img, np.float32)
+    if img.ndim == 2:
+        img = img[:, :, None]
+    H, W, C = img.shape
+    mat = fileFormat == 'matlab'
+    out = []
+    for ch in range(C):
+        if mat:
+            out.append('%s = [' % variable if ch == 0 else '\n%s(:, :, %d) = [' % (variable, ch + 1))
+        elif ch == 0:
+            out.append('%s = {{' % variable if C == 1 else '%s = Transpose[{{{' % variable)
+        for y in range(H):
+            vals = [_fmt_g(v, digits) for v in img[y, :, ch]]
+            if not mat:   # Mathematica's '*^' exponent notation (boost::replace_first "e" -> "*^")
+                vals = [s.replace('e', '*^', 1) for s in vals]
+            out.append(', '.join(vals))
+            if mat:
+                out.append(';\n\t' if y + 1 < H else '];\n')
+            elif y + 1 < H:
+                out.append('},\n\t{')
+            elif ch + 1 == C:
+                out.append('}};\n' if C == 1 else '}}}, {3,1,2}];\n')
+            else:
+                out.append('}},\n\n\t{{')
+    return ''.join(out)
+
+
+def npy_header(shape, descr='<f4'):
+    """cnpy::create_npy_header (src/films/cnpy.h:207-236): NPY 1.0 with the dict
+    padded by spaces (16 more when already aligned) so that 10 + len is a
+    multiple of 16, its last byte a newline."""
+    d = "{'descr': '%s', 'fortran_order': False, 'shape': (%s" % (descr, ', '.join(str(int(s)) for s in shape))
+    d += ',' if len(shape) == 1 else ''
+    d += '), }'
+    pad = 16 - (10 + len(d)) % 16
+    d = (d + ' ' * pad)[:-1] + '\n'
+    return b'\x93NUMPY\x01\x00' + struct.pack('<H', len(d)) + d.encode('ascii')
+
+
+def write_npy(path, img):
+    """cnpy::npy_save(filename, data, {H, W, C}, C == 1 ? 2 : 3, "w") (mfilm.cpp:336-347)."""
+    img = np.ascontiguousarray(img, np.float32)
+    shape = img.shape[:2] if img.ndim == 2 or img.shape[2] == 1 else img.shape
+    with open(path, 'wb') as f:
+        f.write(npy_header(shape))
+        f.write(img.astype('<f4').tobytes())
 
 
 _banner_warned = False

@@ -41,6 +41,13 @@ def load_library(path=None):
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise NativeUnavailable('libmtsgpu.so not built: %s (run __graft_entry__.build())' % p)
+    # PyTorch ships its own libamdhip64: load it first, so that libmtsgpu binds
+    # to the same HIP runtime and device pointers / streams from torch are valid
+    # in both (two runtimes in one process hide the GPU from the second one).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(p)
     P = C.POINTER
     L.mtsgpu_create.argtypes = [C.c_int, P(C.c_void_p)]

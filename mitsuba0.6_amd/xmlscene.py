@@ -32,7 +32,7 @@ import xml.etree.ElementTree as ET
 
 import numpy as np
 
-from .film import HDRFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
+from .film import HDRFilm, MFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
 from .obj import load_obj, srgb_to_linear, strtof
 from .ply import load_ply
 from .scene import BSDF, Checkerboard, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor
@@ -489,21 +489,32 @@ class XMLSceneLoader:
         width, height = 768, 576
         rfilter, rparam, has_alpha, crop, hdr = 'gaussian', 0.5, False, None, HDRFilm()
         if film is not None:
-            if film.plugin != 'hdrfilm':
-                raise NotImplementedError('film "%s" (hdrfilm)' % film.plugin)
-            width, height = film.get('width', 768), film.get('height', 576)
+            if film.plugin not in ('hdrfilm', 'mfilm'):
+                raise NotImplementedError('film "%s" (hdrfilm, mfilm)' % film.plugin)
+            mf = film.plugin == 'mfilm'
+            width, height = film.get('width', 1 if mf else 768), film.get('height', 1 if mf else 576)   # film.cpp:27-33
             try:
-                hdr = HDRFilm(fileFormat=film.get('fileFormat', 'openexr'), pixelFormat=film.get('pixelFormat', 'rgb'),
-                              componentFormat=film.get('componentFormat', 'float16'),
-                              channelNames=film.get('channelNames', ''), banner=film.get('banner', True),
-                              attachLog=film.get('attachLog', True))
+                if mf:
+                    hdr = MFilm(fileFormat=film.get('fileFormat', 'matlab'), pixelFormat=film.get('pixelFormat',
+                                                                                                   'luminance'),
+                                digits=film.get('digits', 4), variable=film.get('variable', 'data'))
+                    rfilter, rparam = 'box', 0.5            # mfilm.cpp:156-165: box by default
+                else:
+                    hdr = HDRFilm(fileFormat=film.get('fileFormat', 'openexr'),
+                                  pixelFormat=film.get('pixelFormat', 'rgb'),
+                                  componentFormat=film.get('componentFormat', 'float16'),
+                                  channelNames=film.get('channelNames', ''), banner=film.get('banner', True),
+                                  attachLog=film.get('attachLog', True))
             except ValueError as e:
                 raise SceneError(str(e))
             if film.get('highQualityEdges', False):
-                raise NotImplementedError('hdrfilm highQualityEdges=true (renders the border pixels outside the crop)')
+                raise NotImplementedError('highQualityEdges=true (renders the border pixels outside the crop)')
             has_alpha = hdr.hasAlpha
             crop = (film.get('cropOffsetX', 0), film.get('cropOffsetY', 0), film.get('cropWidth', width),
                     film.get('cropHeight', height))
+            if (crop[0] < 0 or crop[1] < 0 or crop[2] <= 0 or crop[3] <= 0 or crop[0] + crop[2] > width
+                    or crop[1] + crop[3] > height):     # film.cpp:44-48
+                raise SceneError('Invalid crop window specification!')
             rf = next((c for _, c in film.children if c.tag == 'rfilter'), None)
             if rf is not None:
                 if rf.plugin == 'box':
@@ -696,14 +707,19 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     L.append('    <transform name="toWorld">%s</transform>' % _matrix(s.toWorld))
     L.append('    <sampler type="sobol"><integer name="sampleCount" value="%d"/>'
              '<integer name="scramble" value="%d"/></sampler>' % (integ.sampleCount, integ.scramble))
-    L.append('    <film type="hdrfilm">')
-    L.append('      <integer name="width" value="%d"/><integer name="height" value="%d"/>' % (s.width, s.height))
     hf = integ.film or HDRFilm()
+    mf = isinstance(hf, MFilm)
+    L.append('    <film type="%s">' % ('mfilm' if mf else 'hdrfilm'))
+    L.append('      <integer name="width" value="%d"/><integer name="height" value="%d"/>' % (s.width, s.height))
     fmt = hf.pixel_format if hf.hasAlpha == bool(integ.hasAlpha) else ('rgba' if integ.hasAlpha else 'rgb')
     L.append('      <string name="pixelFormat" value="%s"/>' % fmt)
-    L.append('      <string name="fileFormat" value="%s"/><string name="componentFormat" value="%s"/>'
-             % (hf.fileFormat, hf.componentFormat))
-    L.append('      <boolean name="banner" value="%s"/>' % str(bool(hf.banner)).lower())
+    if mf:
+        L.append('      <string name="fileFormat" value="%s"/><integer name="digits" value="%d"/>'
+                 '<string name="variable" value="%s"/>' % (hf.fileFormat, hf.digits, hf.variable))
+    else:
+        L.append('      <string name="fileFormat" value="%s"/><string name="componentFormat" value="%s"/>'
+                 % (hf.fileFormat, hf.componentFormat))
+        L.append('      <boolean name="banner" value="%s"/>' % str(bool(hf.banner)).lower())
     if integ.crop:
         x0, y0, w, h = integ.crop
         L.append('      <integer name="cropOffsetX" value="%d"/><integer name="cropOffsetY" value="%d"/>'

@@ -215,3 +215,87 @@ def test_xml_film_properties(tmp_path):
     (tmp_path / 'b.xml').write_text(bad)
     with pytest.raises(xmlscene.SceneError, match='spectral'):
         xmlscene.load_scene(str(tmp_path / 'b.xml'))
+
+
+# --- mfilm (src/films/mfilm.cpp) ---------------------------------------------
+_MF_IMG = np.array([[[1, 4], [0.5, 0], [1e-5, 7]], [[2.25, 8], [123456, 9], [-3, 10]]], np.float32)   # (2, 3, 2)
+
+
+def test_mfilm_matlab_text():
+    """mfilm.cpp:278-318: `var = [` rows `, `-separated, `;\\n\\t` between rows,
+    `];\\n` at the end, later channels as `\\nvar(:, :, c) = [`; %.{digits}g values."""
+    t = F.mfilm_text(_MF_IMG[:, :, :1], 'matlab')
+    assert t == 'data = [1, 0.5, 1e-05;\n\t2.25, 1.235e+05, -3];\n'
+    t = F.mfilm_text(_MF_IMG, 'matlab', digits=2, variable='img')
+    assert t == ('img = [1, 0.5, 1e-05;\n\t2.2, 1.2e+05, -3];\n'
+                 '\nimg(:, :, 2) = [4, 0, 7;\n\t8, 9, 10];\n')
+
+
+def test_mfilm_mathematica_text():
+    """mfilm.cpp:285-330: nested braces, `Transpose[..., {3,1,2}]` for several
+    channels, and the `*^` exponent notation."""
+    t = F.mfilm_text(_MF_IMG[:, :, :1], 'mathematica')
+    assert t == 'data = {{1, 0.5, 1*^-05},\n\t{2.25, 1.235*^+05, -3}};\n'
+    t = F.mfilm_text(_MF_IMG, 'mathematica')
+    assert t == ('data = Transpose[{{{1, 0.5, 1*^-05},\n\t{2.25, 1.235*^+05, -3}},\n\n\t{{'
+                 '4, 0, 7},\n\t{8, 9, 10}}}, {3,1,2}];\n')
+
+
+def test_mfilm_npy_header_is_cnpy():
+    """cnpy::create_npy_header (cnpy.h:207-236): dict padded to 10 + len = 0 mod 16,
+    a full extra 16 spaces when already aligned, and the array reads back."""
+    h = F.npy_header((24, 32, 3))
+    d = "{'descr': '<f4', 'fortran_order': False, 'shape': (24, 32, 3), }"
+    assert h == b'\x93NUMPY\x01\x00' + struct.pack('<H', 70) + (d + ' ' * 5 + '\n').encode()
+    h = F.npy_header((10000, 1000, 10))          # 10 + 70 already aligned -> 16 more
+    assert len(h) == 10 + 86 and h.endswith(b' ' * 15 + b'\n')
+    assert F.npy_header((5,))[10:].startswith(b"{'descr': '<f4', 'fortran_order': False, 'shape': (5,), }")
+
+
+def test_mfilm_write_and_properties(tmp_path):
+    mf = F.MFilm(fileFormat='numpy', pixelFormat='rgba')
+    assert mf.hasAlpha and mf.componentFormat == 'float32' and mf.channel_names == ['R', 'G', 'B', 'A']
+    img = np.random.default_rng(3).random((5, 7, 4), dtype=np.float32)
+    p = mf.write(str(tmp_path / 'out.exr'), img)
+    assert p.endswith('out.npy')
+    assert np.array_equal(np.load(p), img)
+    lum = F.MFilm(fileFormat='numpy')            # one channel -> 2D array (mfilm.cpp:343-344)
+    p = lum.write(str(tmp_path / 'y.NPY'), img[:, :, :1])
+    assert p.endswith('y.NPY') and np.load(p).shape == (5, 7)
+    m = F.MFilm()
+    assert (m.fileFormat, m.pixel_format, m.digits, m.variable) == ('matlab', 'luminance', 4, 'data')
+    assert m.write(str(tmp_path / 'a.txt'), img[:, :, :1]).endswith('a.m')
+    assert F.MFilm(fileFormat='mathematica').output_path('x.M') == 'x.M'
+    with pytest.raises(ValueError, match='fileFormat'):
+        F.MFilm(fileFormat='csv')
+    with pytest.raises(ValueError, match='spectral'):
+        F.MFilm(pixelFormat='spectrumAlpha')
+    with pytest.raises(ValueError, match='pixelFormat'):
+        F.MFilm(pixelFormat='bgr')
+
+
+def test_xml_mfilm(tmp_path):
+    """<film type="mfilm">: 1x1 default size (film.cpp:27-33), box filter by
+    default (mfilm.cpp:156-165), its own properties, and a save/load round trip."""
+    (tmp_path / 's.xml').write_text('''<scene version="0.6.0">
+      <integrator type="path"/>
+      <sensor type="perspective"><float name="fov" value="40"/>
+        <sampler type="sobol"><integer name="sampleCount" value="4"/></sampler>
+        <film type="mfilm"><string name="fileFormat" value="numpy"/><string name="pixelFormat" value="rgb"/>
+          <integer name="digits" value="6"/><string name="variable" value="img"/></film></sensor>
+      <shape type="cube"/></scene>''')
+    sc, it = xmlscene.load_scene(str(tmp_path / 's.xml'))
+    assert (sc.sensor.width, sc.sensor.height) == (1, 1)
+    assert (it.rfilter, it.rfilterParam) == ('box', 0.5)
+    assert isinstance(it.film, F.MFilm) and (it.film.fileFormat, it.film.pixel_format) == ('numpy', 'rgb')
+    assert (it.film.digits, it.film.variable) == (6, 'img') and not it.hasAlpha
+    xmlscene.save_scene(sc, it, str(tmp_path / 'out'))
+    sc2, it2 = xmlscene.load_scene(str(tmp_path / 'out' / 'scene.xml'))
+    assert isinstance(it2.film, F.MFilm)
+    assert (it2.film.fileFormat, it2.film.pixel_format, it2.film.digits, it2.film.variable) == ('numpy', 'rgb', 6,
+                                                                                                'img')
+    bad = (tmp_path / 's.xml').read_text().replace('<film type="mfilm">',
+                                                   '<film type="mfilm"><integer name="cropWidth" value="2"/>')
+    (tmp_path / 'b.xml').write_text(bad)
+    with pytest.raises(xmlscene.SceneError, match='crop window'):
+        xmlscene.load_scene(str(tmp_path / 'b.xml'))

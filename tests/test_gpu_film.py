@@ -68,6 +68,22 @@ def test_develop_rendered_film_and_exr(gpu_ctx, oracle, tmp_path):
     assert np.array_equal(_bits(np.stack([planes[c] for c in 'RGB'], -1)), _bits(img))
 
 
+@pytest.mark.parametrize('fmt', FORMATS)
+def test_mfilm_develop_and_npy(gpu_ctx, fmt, tmp_path):
+    """mfilm develops through the same device kernel as Bitmap::convert(fmt, EFloat)
+    (mfilm.cpp:264-265); the .npy it writes reads back bit for bit."""
+    sc, it = scenes.build('C1', width=40, height=24, spp=4)
+    gpu_ctx.upload(sc)
+    film_g, _, _ = gpu_ctx.render(it)
+    from mitsuba_amd.scene import film_border
+    b = film_border(it.rfilter, it.rfilterParam)
+    mf = F.MFilm(fileFormat='numpy', pixelFormat=fmt)
+    img = mf.develop(gpu_ctx, film_g, b)
+    assert np.array_equal(_bits(img), _bits(develop_ref(film_g, b, fmt, 'float32')))
+    back = np.load(mf.write(str(tmp_path / 'img'), img))
+    assert np.array_equal(_bits(back.reshape(img.shape)), _bits(img))
+
+
 def test_develop_device_buffers(gpu_ctx):
     """mtsgpu_develop_device on torch HBM tensors and a torch stream."""
     import torch
