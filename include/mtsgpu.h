@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 3
+#define MTSGPU_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -199,9 +199,16 @@ typedef struct {
        hide_emitters apply to both */
     int32_t integrator;
     uint32_t emitter_samples, bsdf_samples;
+    /* the sampler plugin: MTSGPU_SAMPLER_SOBOL (sobol.cpp; 'scramble') or
+       MTSGPU_SAMPLER_INDEPENDENT (independent.cpp:51-116): uniform [0,1) draws
+       from a per-(pixel, sample) counter-based stream in place of the
+       reference's per-thread SFMT19937, whose values depend on the thread
+       schedule; the film x/y must be below 65536 */
+    int32_t sampler;
 } mtsgpu_render_params;
 
 enum { MTSGPU_INTEGRATOR_PATH = 0, MTSGPU_INTEGRATOR_DIRECT = 1 };
+enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1 };
 
 /* render flags */
 #define MTSGPU_FLAG_TRAVERSAL_STATS 1u  /* count BVH node visits / TriAccel tests   */

@@ -14,13 +14,14 @@ STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTA
 BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC, BSDF_ROUGHPLASTIC = 0, 1, 2, 3
 BSDF_CONDUCTOR, BSDF_DIELECTRIC, BSDF_PLASTIC, BSDF_TWOSIDED = 4, 5, 6, 7
 TEX_NONE, TEX_CHECKERBOARD = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP, EMITTER_CONSTANT = 0, 1, 2
 SHAPE_TRIMESH, SHAPE_RECTANGLE, SHAPE_DISK, SHAPE_SPHERE = 0, 1, 2, 3
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 INTEGRATOR_PATH, INTEGRATOR_DIRECT = 0, 1
+SAMPLER_SOBOL, SAMPLER_INDEPENDENT = 0, 1
 SAMPLE_RECORD_FLOATS = 8
 PIX_LUMINANCE, PIX_LUMINANCE_ALPHA, PIX_RGB, PIX_RGBA, PIX_XYZ, PIX_XYZA = 0, 1, 2, 3, 4, 5
 COMP_FLOAT16, COMP_FLOAT32, COMP_UINT32 = 0, 1, 2
@@ -83,7 +84,8 @@ class RenderParams(C.Structure):
                 ('x0', C.c_uint32), ('y0', C.c_uint32), ('width', C.c_uint32), ('height', C.c_uint32),
                 ('row_block', C.c_uint32), ('row_stride', C.c_uint32), ('row_phase', C.c_uint32),
                 ('cancel', C.POINTER(C.c_int32)), ('flags', C.c_uint32),
-                ('integrator', C.c_int32), ('emitter_samples', C.c_uint32), ('bsdf_samples', C.c_uint32)]
+                ('integrator', C.c_int32), ('emitter_samples', C.c_uint32), ('bsdf_samples', C.c_uint32),
+                ('sampler', C.c_int32)]
 
 
 FLAG_TRAVERSAL_STATS = 1

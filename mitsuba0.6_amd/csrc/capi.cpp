@@ -297,11 +297,19 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (P->integrator != MTSGPU_INTEGRATOR_PATH && !direct) return fail(ctx, MTSGPU_EINVAL, "unknown integrator");
     if (direct && P->emitter_samples + P->bsdf_samples == 0)
         return fail(ctx, MTSGPU_EINVAL, "direct: emitterSamples + bsdfSamples must be positive");
+    if (P->sampler != MTSGPU_SAMPLER_SOBOL && P->sampler != MTSGPU_SAMPLER_INDEPENDENT)
+        return fail(ctx, MTSGPU_EINVAL, "unknown sampler");
+    L.sampler = (uint32_t)P->sampler;
     const uint64_t perSampleIdx = direct ? std::max<uint64_t>(1, std::max(P->emitter_samples, P->bsdf_samples)) : 1;
     uint32_t sppBits = 0;
     while ((1ull << sppBits) < (uint64_t)P->spp * perSampleIdx) ++sppBits;
     const uint32_t indexBits = (m > 1 ? 2 * m : 0) + sppBits;
-    if (indexBits > 52) return fail(ctx, MTSGPU_EINVAL, "sample index exceeds the 52-bit Sobol direction numbers");
+    if (L.sampler == MTSGPU_SAMPLER_SOBOL && indexBits > 52)
+        return fail(ctx, MTSGPU_EINVAL, "sample index exceeds the 52-bit Sobol direction numbers");
+    // independent streams are keyed by (x, y, sample): 16 + 16 + 32 bits
+    if (L.sampler == MTSGPU_SAMPLER_INDEPENDENT && (H.film_w > 65536 || H.film_h > 65536 ||
+                                                   (uint64_t)P->spp * perSampleIdx > 0xFFFFFFFFull))
+        return fail(ctx, MTSGPU_EINVAL, "independent sampler: film or sample count too large for the stream key");
     L.nibbles = indexBits <= 32 ? 8 : MTSG_NIBBLES;
     L.lds_dims = 32;
     L.sobol_nib = (const uint32_t *)ctx->sobol.p;

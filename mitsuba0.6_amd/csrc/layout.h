@@ -79,7 +79,8 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
 
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1, MTSG_EMITTER_CONSTANT = 2 };
 enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4 };
-enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1 };   // = MTSGPU_INTEGRATOR_*   // path_kernel variants   // = MTSGPU_EMITTER_* (include/mtsgpu.h)
+enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1 };   // = MTSGPU_INTEGRATOR_*
+enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1 };    // = MTSGPU_SAMPLER_*
 
 struct MtsgShape {
     int32_t bsdf, emitter, has_normals, has_uv;
@@ -218,9 +219,10 @@ struct MtsgLaunch {
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
+    int32_t integrator;               // MTSGPU_INTEGRATOR_*
+    uint32_t sampler;                 // MTSGPU_SAMPLER_*
     // the `direct` integrator (direct.cpp:128-143): sample counts, MIS fractions and
     // weights, and the sampler's 2D arrays (dims [5, array_end))
-    int32_t integrator;               // MTSGPU_INTEGRATOR_*
     uint32_t lum_samples, bsdf_samples;
     float weight_lum, weight_bsdf, frac_lum, frac_bsdf;
     uint32_t lum_dim, bsdf_dim, array_end;

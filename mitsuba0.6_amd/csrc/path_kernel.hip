@@ -61,9 +61,29 @@ struct SobolCtx {
     lds_u32 *lds;             // [lds_dims][nibbles][16]
     glb_u32 *glob;            // [1024][MTSG_NIBBLES][16]
     uint32_t lds_dims, nibbles, scramble;
+    bool indep;               // the `independent` sampler: `index` is a stream key
 };
 
+// The independent sampler (independent.cpp:82-104): a counter-based stream per
+// (pixel, sample) -- splitmix64-finalised key, one finalised draw per dimension
+// -- in place of the reference's per-thread SFMT19937, whose values depend on
+// the thread schedule; Random::nextFloat's [1,2) - 1 conversion
+// (random.cpp:630-639).  The oracle's indep_* functions are the same.
+__device__ __forceinline__ uint64_t indep_mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t indep_key(uint32_t px, uint32_t py, uint32_t frame) {
+    return indep_mix64((((uint64_t)px << 48) | ((uint64_t)py << 32) | frame) ^ 0x6A09E667F3BCC909ull);
+}
+__device__ __forceinline__ float indep_float(uint64_t key, uint32_t dim) {
+    const uint32_t u = (uint32_t)indep_mix64(key + (uint64_t)(dim + 1) * 0x9E3779B97F4A7C15ull);
+    return __uint_as_float((u >> 9) | 0x3f800000u) - 1.0f;
+}
+
 __device__ __forceinline__ float sobol_sample(const SobolCtx &C, uint64_t index, uint32_t dim) {
+    if (C.indep) return indep_float(index, dim);
     uint32_t bits;
     if (dim < C.lds_dims) {
         lds_u32 *t = C.lds + dim * C.nibbles * 16;
@@ -612,14 +632,14 @@ struct PathVars {
 };
 
 __device__ __forceinline__ float next1d(const SobolCtx &C, SamplerState &s) {   // sobol.cpp:219-229
-    if (s.dim >= MTSG_SOBOL_DIMS) { s.err = true; return 0.0f; }
+    if (s.dim >= MTSG_SOBOL_DIMS && !C.indep) { s.err = true; return 0.0f; }
     return sobol_sample(C, s.sobolIndex, s.dim++);
 }
 __device__ __forceinline__ void next2d(const SobolCtx &C, float resolution, SamplerState &s, int px, int py,
                                        float &u, float &v) {                       // sobol.cpp:231-250
     if (s.dim + 1 >= 5 && s.dim < 5) s.dim = 5;   // skip the (empty) array dimensions [5,5)
-    if (s.dim + 1 >= MTSG_SOBOL_DIMS) { s.err = true; u = v = 0.0f; return; }
-    if (s.dim == 0 && s.sobolIndex != (uint64_t)s.sampleIndex) {
+    if (s.dim + 1 >= MTSG_SOBOL_DIMS && !C.indep) { s.err = true; u = v = 0.0f; return; }
+    if (!C.indep && s.dim == 0 && s.sobolIndex != (uint64_t)s.sampleIndex) {
         u = sobol_sample(C, s.sobolIndex, s.dim++) * resolution - (float)px;
         v = sobol_sample(C, s.sobolIndex, s.dim++) * resolution - (float)py;
     } else {
@@ -798,6 +818,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     SC.lds_dims = L.lds_dims;
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
+    SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
     lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
     lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
 
@@ -832,7 +853,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             smp.dim = 0;
             smp.sampleIndex = j;
             smp.err = false;
-            if (L.lut.m > 1)
+            if (SC.indep)
+                smp.sobolIndex = indep_key((uint32_t)px, (uint32_t)py, j);
+            else if (L.lut.m > 1)
                 smp.sobolIndex = sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py, L.scramble64);
             else
                 smp.sobolIndex = j;
@@ -1213,7 +1236,8 @@ __device__ __forceinline__ void sobol_array2d(const SobolCtx &C, const MtsgLooku
                                               uint32_t j, uint32_t size, uint32_t k, int px, int py,
                                               uint64_t scramble64, uint32_t dim, float &u, float &v) {
     const uint32_t frame = j * size + k;
-    const uint64_t idx = Lu.m >= 1 ? sobol_lookup_lds(Lu, ycolTab, nibbles, frame, (uint32_t)px, (uint32_t)py, scramble64)
+    const uint64_t idx = C.indep ? indep_key((uint32_t)px, (uint32_t)py, frame)
+                       : Lu.m >= 1 ? sobol_lookup_lds(Lu, ycolTab, nibbles, frame, (uint32_t)px, (uint32_t)py, scramble64)
                                    : (uint64_t)frame;
     u = sobol_sample(C, idx, dim);
     v = sobol_sample(C, idx, dim + 1);
@@ -1422,6 +1446,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
     SC.lds_dims = L.lds_dims;
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
+    SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
     lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
     lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
     unsigned long long cRays = 0, cShadow = 0, cSamples = 0, cErr = 0, cN = 0, cT = 0;
@@ -1479,7 +1504,8 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         smp.dim = 0;
         smp.sampleIndex = j;
         smp.err = false;
-        smp.sobolIndex = (L.lut.m > 1) ? sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py,
+        smp.sobolIndex = SC.indep ? indep_key((uint32_t)px, (uint32_t)py, j)
+                       : (L.lut.m > 1) ? sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py,
                                                           L.scramble64)
                                        : (uint64_t)j;
         float u, v;

@@ -350,8 +350,11 @@ class PathIntegrator:
     hasAlpha: bool = False         # hdrfilm pixelFormat default "rgb" (hdrfilm.cpp:216)
     crop: Optional[tuple] = None   # hdrfilm crop window (x0, y0, w, h) (film.cpp:35-43); None = whole film
     film: Optional['HDRFilm'] = None   # hdrfilm output format (film.py); None = the hdrfilm defaults
+    sampler: str = 'sobol'         # 'sobol' or 'independent' (include/mtsgpu.h: MTSGPU_SAMPLER_*)
 
     def __post_init__(self):
+        if self.sampler not in ('sobol', 'independent'):
+            raise ValueError('sampler "%s" (sobol, independent)' % self.sampler)
         if self.rrDepth <= 0:
             raise ValueError("'rrDepth' must be set to a value greater than zero!")
         if self.maxDepth <= 0 and self.maxDepth != -1:
@@ -374,6 +377,7 @@ class PathIntegrator:
         p.height = height - y0 if h is None else h
         p.row_block, p.row_stride, p.row_phase = row_block, row_stride, row_phase
         p.integrator = abi.INTEGRATOR_PATH
+        p.sampler = abi.SAMPLER_INDEPENDENT if self.sampler == 'independent' else abi.SAMPLER_SOBOL
         return p
 
 

@@ -12,18 +12,21 @@ semantics (src/librender/scenehandler.cpp):
   `<spectrum>` (constant values), `<point>`, `<vector>`.
 
 Plugins:
-- integrator `path` (maxDepth, rrDepth, strictNormals, hideEmitters).
+- integrators `path` (maxDepth, rrDepth, strictNormals, hideEmitters) and
+  `direct` (shadingSamples, emitterSamples, bsdfSamples, strictNormals,
+  hideEmitters).
 - sensor `perspective` (fov/fovAxis or focalLength, near/farClip, toWorld),
-  with sampler `sobol` (sampleCount, scramble) and film `hdrfilm` (width,
-  height, crop window, pixelFormat rgb|rgba), whose rfilter is `box` or
-  `gaussian`.
-- shapes `obj`, `ply`, `serialized`, `cube` (triangle meshes).
-- BSDFs `diffuse`, `roughconductor`, `roughdielectric`.
+  with sampler `sobol` (sampleCount, scramble) or `independent` (sampleCount;
+  the default without a <sampler>), film `hdrfilm` or `mfilm` (size, crop
+  window, pixel/file formats), whose rfilter is `box` or `gaussian`.
+- shapes `obj`, `ply`, `serialized`, `cube` (triangle meshes) and the analytic
+  `rectangle`, `disk`, `sphere`.
+- BSDFs `diffuse`, `roughconductor`, `roughdielectric`, `roughplastic`,
+  `conductor`, `dielectric`, `plastic`, `twosided`; `checkerboard` textures.
 - emitters `area` (inside a shape), `envmap` (PFM/EXR/RGBE files) and `constant`.
 
-Anything else raises NotImplementedError naming the plugin. That includes
-analytic shapes (`rectangle`, `sphere`, `disk`, `cylinder`), which the
-reference intersects analytically rather than as TriAccel triangles.
+Anything else raises NotImplementedError naming the plugin (e.g. `cylinder`,
+`hair`, media).
 """
 import math
 import os
@@ -524,11 +527,13 @@ class XMLSceneLoader:
                 else:
                     raise NotImplementedError('rfilter "%s" (box, gaussian)' % rf.plugin)
         spp, scramble = 4, 0
-        if sampler is None:
-            raise NotImplementedError('the default "independent" sampler is not reproducible; use "sobol"')
-        if sampler.plugin != 'sobol':
-            raise NotImplementedError('sampler "%s" (sobol)' % sampler.plugin)
-        spp, scramble = sampler.get('sampleCount', 4), sampler.get('scramble', 0)
+        # no <sampler>: an independent sampler with 4 samples per pixel (sensor.cpp:92-97)
+        kind = 'independent' if sampler is None else sampler.plugin
+        if kind not in ('sobol', 'independent'):
+            raise NotImplementedError('sampler "%s" (sobol, independent)' % kind)
+        if sampler is not None:
+            spp = sampler.get('sampleCount', 4)
+            scramble = sampler.get('scramble', 0) if kind == 'sobol' else 0
         if 'fov' in p and 'focalLength' in p:
             raise SceneError("Please specify either a focal length ('focalLength') or a field of view ('fov')!")
         if 'fov' in p:
@@ -550,7 +555,7 @@ class XMLSceneLoader:
         tw = p.get('toWorld', Transform())
         sensor = Sensor(fov=fov, fovAxis=axis, nearClip=float(p.get('nearClip', 1e-2)),
                         farClip=float(p.get('farClip', 1e4)), toWorld=tw.m, width=width, height=height)
-        integ.sampleCount, integ.scramble = spp, scramble
+        integ.sampleCount, integ.scramble, integ.sampler = spp, scramble, kind
         integ.rfilter, integ.rfilterParam, integ.hasAlpha = rfilter, rparam, has_alpha
         integ.crop = crop
         integ.film = hdr
@@ -705,8 +710,12 @@ def save_scene(scene, integ, directory, name='scene.xml'):
     L.append('    <float name="nearClip" value="%s"/>' % _fmt(s.nearClip))
     L.append('    <float name="farClip" value="%s"/>' % _fmt(s.farClip))
     L.append('    <transform name="toWorld">%s</transform>' % _matrix(s.toWorld))
-    L.append('    <sampler type="sobol"><integer name="sampleCount" value="%d"/>'
-             '<integer name="scramble" value="%d"/></sampler>' % (integ.sampleCount, integ.scramble))
+    if integ.sampler == 'independent':
+        L.append('    <sampler type="independent"><integer name="sampleCount" value="%d"/></sampler>'
+                 % integ.sampleCount)
+    else:
+        L.append('    <sampler type="sobol"><integer name="sampleCount" value="%d"/>'
+                 '<integer name="scramble" value="%d"/></sampler>' % (integ.sampleCount, integ.scramble))
     hf = integ.film or HDRFilm()
     mf = isinstance(hf, MFilm)
     L.append('    <film type="%s">' % ('mfilm' if mf else 'hdrfilm'))

@@ -446,7 +446,32 @@ typedef struct {
     uint32_t dim;
     uint32_t arrayEnd; /* m_arrayEndDim: dims [5, arrayEnd) hold the requested 2D arrays */
     int err;
+    int indep;         /* the `independent` sampler (independent.cpp) instead of `sobol` */
 } Sampler;
+
+/* The independent sampler's stream (independent.cpp:82-104).  The reference
+ * draws from one SFMT19937 generator per worker thread, so its values depend on
+ * the block schedule and are not reproducible.  Here every
+ * (pixel, sample) owns a counter-based stream: a splitmix64-finalised key and
+ * one finalised draw per dimension; Random::nextFloat's [1,2) - 1 conversion
+ * of the low 32 bits (random.cpp:630-639).  Same function as the kernel's. */
+static uint64_t indep_mix64(uint64_t z) {
+    z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull;
+    z ^= z >> 27; z *= 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static uint64_t indep_key(uint32_t px, uint32_t py, uint32_t frame) {
+    return indep_mix64((((uint64_t)px << 48) | ((uint64_t)py << 32) | frame) ^ 0x6A09E667F3BCC909ull);
+}
+static float indep_float(uint64_t key, uint32_t dim) {
+    const uint32_t u = (uint32_t)indep_mix64(key + (uint64_t)(dim + 1) * 0x9E3779B97F4A7C15ull);
+    union { uint32_t u; float f; } x;
+    x.u = (u >> 9) | 0x3f800000u;
+    return x.f - 1.0f;
+}
+static float smp_value(const Sampler *s, uint64_t idx, uint32_t dim) {
+    return s->indep ? indep_float(idx, dim) : oracle_sobol_sample(idx, dim, (uint32_t)s->scramble);
+}
 
 static void sampler_init(Sampler *s, uint64_t scramble, uint32_t w, uint32_t h) {
     memset(s, 0, sizeof *s);
@@ -464,7 +489,9 @@ static void sampler_init(Sampler *s, uint64_t scramble, uint32_t w, uint32_t h) 
 static void sampler_set_index(Sampler *s, uint64_t idx) { /* sobol.cpp:204-217 */
     s->dim = 0;
     s->sampleIndex = idx;
-    if (s->logRes > 1 && s->px >= 0)
+    if (s->indep)
+        s->sobolIndex = indep_key((uint32_t)s->px, (uint32_t)s->py, (uint32_t)idx);
+    else if (s->logRes > 1 && s->px >= 0)
         s->sobolIndex = oracle_sobol_lookup(s->logRes, (uint32_t)idx, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
     else
         s->sobolIndex = idx;
@@ -473,13 +500,16 @@ static void sampler_generate(Sampler *s, int px, int py) { s->px = px; s->py = p
 
 static float next1d(Sampler *s) { /* sobol.cpp:219-229; dims [5, arrayEnd) are the arrays' */
     if (s->dim >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
-    if (s->dim >= SOBOL_DIMS) { s->err = 1; return 0.0f; }
-    return oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble);
+    if (s->dim >= SOBOL_DIMS && !s->indep) { s->err = 1; return 0.0f; }
+    return smp_value(s, s->sobolIndex, s->dim++);
 }
 static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
     if (s->dim + 1 >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
-    if (s->dim + 1 >= SOBOL_DIMS) { s->err = 1; *u = *v = 0.0f; return; }
-    if (s->dim == 0 && s->sobolIndex != s->sampleIndex) {
+    if (s->dim + 1 >= SOBOL_DIMS && !s->indep) { s->err = 1; *u = *v = 0.0f; return; }
+    if (s->indep) {
+        *u = indep_float(s->sobolIndex, s->dim++);
+        *v = indep_float(s->sobolIndex, s->dim++);
+    } else if (s->dim == 0 && s->sobolIndex != s->sampleIndex) {
         *u = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble) * s->resolution - (float)s->px;
         *v = oracle_sobol_sample(s->sobolIndex, s->dim++, (uint32_t)s->scramble) * s->resolution - (float)s->py;
     } else {
@@ -493,9 +523,10 @@ static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
  * SobolSampler::generate fills (sobol.cpp:171-197) */
 static void sampler_array2d(const Sampler *s, uint32_t dim, uint32_t size, uint32_t k, float *u, float *v) {
     uint32_t j = (uint32_t)(s->sampleIndex * size + k);
-    uint64_t idx = oracle_sobol_lookup(s->logRes, j, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
-    *u = oracle_sobol_sample(idx, dim, (uint32_t)s->scramble);
-    *v = oracle_sobol_sample(idx, dim + 1, (uint32_t)s->scramble);
+    uint64_t idx = s->indep ? indep_key((uint32_t)s->px, (uint32_t)s->py, j)
+                            : oracle_sobol_lookup(s->logRes, j, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
+    *u = smp_value(s, idx, dim);
+    *v = smp_value(s, idx, dim + 1);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -3353,6 +3384,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
         if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
         Sampler smp;
         sampler_init(&smp, P->scramble, P->width, P->height);   /* crop size (integrator.cpp:37-41) */
+        smp.indep = P->sampler == MTSGPU_SAMPLER_INDEPENDENT;
         DirectParams DP;
         memset(&DP, 0, sizeof DP);
         if (direct) direct_configure(P->emitter_samples, P->bsdf_samples, &DP, &smp); /* configureSampler */

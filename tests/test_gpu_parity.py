@@ -247,6 +247,23 @@ def test_direct_integrator_bitexact(gpu_ctx, oracle, counts):
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
 
+@pytest.mark.parametrize('materials', ['rough', 'shapes'])
+def test_independent_sampler_bitexact(gpu_ctx, oracle, materials):
+    """The independent sampler's per-(pixel, sample) streams: path (no dimension
+    limit, RR) and direct with 2D sample arrays, bit-exact against the oracle."""
+    from mitsuba_amd.scene import DirectIntegrator, PathIntegrator
+    sc, _ = scenes.build('C1', width=40, height=32, spp=8, materials=materials)
+    gpu_ctx.upload(sc)
+    for it in (PathIntegrator(sampleCount=8, rfilter='box', sampler='independent'),
+               DirectIntegrator(sampleCount=8, rfilter='box', sampler='independent', emitterSamples=3,
+                                bsdfSamples=2)):
+        film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
+        film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
+        assert same.mean() > 0.999, same.mean()
+        assert st_g['rays'] == st_o['rays']
+
+
 def test_direct_integrator_envmap_and_shapes(gpu_ctx, oracle):
     from mitsuba_amd.scene import DirectIntegrator
     for sc, _ in (_c3_small(area_light=True), scenes.build('C1', width=32, height=32, spp=4, materials='shapes')):
