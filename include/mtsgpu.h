@@ -196,7 +196,10 @@ typedef struct {
     /* the integrator plugin: MTSGPU_INTEGRATOR_PATH (path.cpp; max_depth, rr_depth)
        or MTSGPU_INTEGRATOR_DIRECT (direct.cpp:90-306): 'emitterSamples' and
        'bsdfSamples' (both default to 'shadingSamples' = 1); strict_normals and
-       hide_emitters apply to both */
+       hide_emitters apply to both; MTSGPU_INTEGRATOR_VOLPATH (volpath.cpp) for
+       scenes without participating media: path's parameters, with volpath's
+       shadow segments (Scene::evalTransmittance), strictNormals test and
+       path-length accounting */
     int32_t integrator;
     uint32_t emitter_samples, bsdf_samples;
     /* the sampler plugin: MTSGPU_SAMPLER_SOBOL (sobol.cpp; 'scramble') or
@@ -207,7 +210,7 @@ typedef struct {
     int32_t sampler;
 } mtsgpu_render_params;
 
-enum { MTSGPU_INTEGRATOR_PATH = 0, MTSGPU_INTEGRATOR_DIRECT = 1 };
+enum { MTSGPU_INTEGRATOR_PATH = 0, MTSGPU_INTEGRATOR_DIRECT = 1, MTSGPU_INTEGRATOR_VOLPATH = 2 };
 enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1 };
 
 /* render flags */

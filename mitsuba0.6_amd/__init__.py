@@ -19,11 +19,13 @@ LIB_PATH = os.path.join(PKG_DIR, '_build', 'libmtsgpu.so')
 SOBOL_PARAMS = os.path.join(DATA_DIR, 'sobol_joe_kuo_1024.txt')
 
 from . import abi  # noqa: E402
-from .scene import BSDF, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor, film_border, look_at  # noqa: E402
+from .scene import (BSDF, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor,  # noqa: E402
+                    VolpathIntegrator, film_border, look_at)
 from .film import HDRFilm, MFilm  # noqa: E402
 from .transform import Transform  # noqa: E402
 from .xmlscene import load_scene, save_scene  # noqa: E402
 
-__all__ = ['abi', 'BSDF', 'DirectIntegrator', 'Emitter', 'Mesh', 'PathIntegrator', 'Scene', 'Sensor', 'HDRFilm', 'MFilm',
+__all__ = ['abi', 'BSDF', 'DirectIntegrator', 'Emitter', 'Mesh', 'PathIntegrator', 'Scene', 'Sensor',
+           'VolpathIntegrator', 'HDRFilm', 'MFilm',
            'film_border', 'look_at', 'Transform', 'load_scene', 'save_scene', 'PKG_DIR', 'LIB_PATH',
            'SOBOL_PARAMS']

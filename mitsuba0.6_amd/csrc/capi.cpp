@@ -240,9 +240,10 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (!ctx || !P) return MTSGPU_EINVAL;
     if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "render called before a successful upload_scene");
     if (P->spp == 0) return fail(ctx, MTSGPU_EINVAL, "sampleCount must be positive");
-    if (P->integrator == MTSGPU_INTEGRATOR_PATH && P->rr_depth <= 0)
+    const bool pathLike = P->integrator == MTSGPU_INTEGRATOR_PATH || P->integrator == MTSGPU_INTEGRATOR_VOLPATH;
+    if (pathLike && P->rr_depth <= 0)
         return fail(ctx, MTSGPU_EINVAL, "'rrDepth' must be set to a value greater than zero!");
-    if (P->integrator == MTSGPU_INTEGRATOR_PATH && P->max_depth <= 0 && P->max_depth != -1)
+    if (pathLike && P->max_depth <= 0 && P->max_depth != -1)
         return fail(ctx, MTSGPU_EINVAL, "'maxDepth' must be set to -1 (infinite) or a value greater than zero!");
     const HostScene &H = ctx->host;
     if ((uint64_t)P->x0 + P->width > H.film_w || (uint64_t)P->y0 + P->height > H.film_h)
@@ -294,7 +295,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // Sobol index width: frame << 2m | 2m bits (sobolseq.h:93-125); 52 columns per dimension
     // the direct integrator's 2D sample arrays index the Sobol sequence at spp x count
     const bool direct = P->integrator == MTSGPU_INTEGRATOR_DIRECT;
-    if (P->integrator != MTSGPU_INTEGRATOR_PATH && !direct) return fail(ctx, MTSGPU_EINVAL, "unknown integrator");
+    if (!pathLike && !direct) return fail(ctx, MTSGPU_EINVAL, "unknown integrator");
     if (direct && P->emitter_samples + P->bsdf_samples == 0)
         return fail(ctx, MTSGPU_EINVAL, "direct: emitterSamples + bsdfSamples must be positive");
     if (P->sampler != MTSGPU_SAMPLER_SOBOL && P->sampler != MTSGPU_SAMPLER_INDEPENDENT)

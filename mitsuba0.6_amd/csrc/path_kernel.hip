@@ -964,6 +964,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
                         }
                     }
+                    // volpath.cpp:326-336: the miss still passes the RR step before the loop ends
+                    if (L.integrator == MTSG_INTEGRATOR_VOLPATH && P.depth++ >= L.rr_depth) (void)next1d(SC, smp);
                     endPath = true;   // !its.isValid(): break after the environment term
                 } else {
                     auto &sh = hs.shapes[P.its.shape];
@@ -1036,8 +1038,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                     GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
                     if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
                         P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
+                    // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
+                    const float snp = dot(rd, P.its.geoN) * P.its.wi.z;
                     if ((P.depth >= L.max_depth && L.max_depth > 0) ||
-                        (L.strict_normals && dot(rd, P.its.geoN) * P.its.wi.z >= 0)) {
+                        (L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
                         endPath = true;
                     } else {
                         P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
@@ -1051,17 +1055,22 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             const MtsgEmitter &e = S.emitters[ei];
                             f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
                             float pdf = 0.0f, dist = 0.0f;
+                            f3 vlp = mk(0, 0, 0);   // dRec.p where it does not define dRec.d exactly (volpath)
+                            bool vrecomp = false, vsurf = true;
                             if (ENV && e.type != MTSG_EMITTER_AREA) {
 #ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
                                 glb_env *E = (glb_env *)S.env;
                                 const EnvSample es = E->constant ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
                                                                  : env_sample_direct(E, P.its.p, ex, ey);
                                 value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
+                                vlp = add(P.its.p, mul(dd, dist));   // dRec.p = ray(farT) (envmap.cpp:536, constant.cpp:254)
+                                vrecomp = true; vsurf = false;
 #endif
                             } else if (ANA && S.shapes[e.shape].analytic >= 0) {
                                 const AnaSample as =
                                     ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], P.its.p, ex, ey);
                                 dd = as.d; dist = as.dist; pdf = as.pdf;
+                                vlp = as.p; vrecomp = true;
                                 // AreaLight::sampleDirect (area.cpp:158-173)
                                 if (dot(dd, P.refN) >= 0 && dot(dd, as.n) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
                                 else pdf = 0.0f;
@@ -1127,6 +1136,14 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                 P.neeC = c;
                                 sd = dd;
                                 smaxt = dist * (1 - D_SHADOW_EPSILON);
+                                if (L.integrator == MTSG_INTEGRATOR_VOLPATH && vrecomp) {
+                                    // Scene::evalTransmittance (scene.cpp:619-679): the segment to dRec.p,
+                                    // re-normalised; no shadow epsilon towards an emitter not on a surface
+                                    const f3 v = sub(vlp, P.its.p);
+                                    const float rem = dsqrt(len2(v));
+                                    sd = divs(v, rem);
+                                    smaxt = vsurf ? rem * (1 - D_SHADOW_EPSILON) : rem;
+                                }
                                 haveShadow = true;
                             }
                         }

@@ -382,6 +382,20 @@ class PathIntegrator:
 
 
 @dataclass
+class VolpathIntegrator(PathIntegrator):
+    """The reference `volpath` plugin (MIVolumetricPathTracer,
+    src/integrators/path/volpath.cpp) on scenes without participating media:
+    path's properties; shadow rays are Scene::evalTransmittance segments to the
+    sampled emitter point, the strictNormals test and the path-length count
+    follow volpath.cpp.  Media are out of scope."""
+
+    def params(self, *a, **kw):
+        p = super().params(*a, **kw)
+        p.integrator = abi.INTEGRATOR_VOLPATH
+        return p
+
+
+@dataclass
 class DirectIntegrator(PathIntegrator):
     """Properties of the reference `direct` plugin (MIDirectIntegrator,
     src/integrators/direct/direct.cpp:90-135): `shadingSamples` sets both

@@ -12,7 +12,8 @@ semantics (src/librender/scenehandler.cpp):
   `<spectrum>` (constant values), `<point>`, `<vector>`.
 
 Plugins:
-- integrators `path` (maxDepth, rrDepth, strictNormals, hideEmitters) and
+- integrators `path` and `volpath` (maxDepth, rrDepth, strictNormals,
+  hideEmitters; volpath without media) and
   `direct` (shadingSamples, emitterSamples, bsdfSamples, strictNormals,
   hideEmitters).
 - sensor `perspective` (fov/fovAxis or focalLength, near/farClip, toWorld),
@@ -38,7 +39,8 @@ import numpy as np
 from .film import HDRFilm, MFilm, load_bitmap, read_pfm, write_pfm  # noqa: F401  (Bitmap readers/writers)
 from .obj import load_obj, srgb_to_linear, strtof
 from .ply import load_ply
-from .scene import BSDF, Checkerboard, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor
+from .scene import (BSDF, Checkerboard, DirectIntegrator, Emitter, Mesh, PathIntegrator, Scene, Sensor,
+                    VolpathIntegrator)
 from .serialized import load_serialized
 from .transform import Transform, _cross, _normalize, normalize_rows
 
@@ -477,10 +479,12 @@ class XMLSceneLoader:
                                     bsdfSamples=int(p.get('bsdfSamples', n)),
                                     strictNormals=p.get('strictNormals', False),
                                     hideEmitters=p.get('hideEmitters', False))
-        if p.plugin != 'path':
-            raise NotImplementedError('integrator "%s" (the GPU path implements "path" and "direct")' % p.plugin)
-        return PathIntegrator(maxDepth=p.get('maxDepth', -1), rrDepth=p.get('rrDepth', 5),
-                              strictNormals=p.get('strictNormals', False), hideEmitters=p.get('hideEmitters', False))
+        if p.plugin not in ('path', 'volpath'):
+            raise NotImplementedError('integrator "%s" (the GPU path implements "path", "volpath" and "direct")'
+                                      % p.plugin)
+        cls = VolpathIntegrator if p.plugin == 'volpath' else PathIntegrator
+        return cls(maxDepth=p.get('maxDepth', -1), rrDepth=p.get('rrDepth', 5),
+                   strictNormals=p.get('strictNormals', False), hideEmitters=p.get('hideEmitters', False))
 
     def _sensor(self, p, integ):
         if p is None:
@@ -697,7 +701,7 @@ def save_scene(scene, integ, directory, name='scene.xml'):
         L.append('    <integer name="emitterSamples" value="%d"/>' % integ.emitterSamples)
         L.append('    <integer name="bsdfSamples" value="%d"/>' % integ.bsdfSamples)
     else:
-        L.append('  <integrator type="path">')
+        L.append('  <integrator type="%s">' % ('volpath' if isinstance(integ, VolpathIntegrator) else 'path'))
         L.append('    <integer name="maxDepth" value="%d"/>' % integ.maxDepth)
         L.append('    <integer name="rrDepth" value="%d"/>' % integ.rrDepth)
     L.append('    <boolean name="strictNormals" value="%s"/>' % str(bool(integ.strictNormals)).lower())

@@ -2949,7 +2949,7 @@ static V3 its_Le(const Scene *S, const Its *its, V3 d) {
 /* Scene::sampleEmitterDirect (scene.cpp:828-852) -> AreaLight::sampleDirect
  * (area.cpp:158-173) -> Shape::sampleDirect (shape.cpp:102-115) ->
  * TriMesh::samplePosition (trimesh.cpp:412-425) -> Triangle::sample (triangle.cpp:24-58) */
-static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, Counters *C) {
+static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, Counters *C, int volpath) {
     V3 zero = v3(0, 0, 0);
     float emPdf;
     uint32_t index = dd_sample_reuse(S->emCdf, S->nemitters, &sx, &emPdf);
@@ -3008,6 +3008,17 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
         sray.mint = EPSILON;
         sray.maxt = dRec->dist * (1 - SHADOW_EPSILON);
         sray.hasDiff = 0;
+        const int env = e->type == MTSGPU_EMITTER_ENVMAP || e->type == MTSGPU_EMITTER_CONSTANT;
+        if (volpath && (env || S->meshes[e->mesh].kind != MTSGPU_SHAPE_TRIMESH)) {
+            /* Scene::sampleAttenuatedEmitterDirect -> evalTransmittance (scene.cpp:619-679, 876-898):
+             * the segment to dRec.p (= ray(farT) for the environment, envmap.cpp:536, constant.cpp:254),
+             * re-normalised; no shadow epsilon towards an emitter that is not on a surface */
+            const V3 lp = env ? vadd(dRec->ref, vmul(dRec->d, dRec->dist)) : dRec->p;
+            const V3 v = vsub(lp, dRec->ref);
+            const float rem = sqrtf(vlen2(v));
+            ray_set_dir(&sray, vdiv(v, rem));
+            sray.maxt = env ? rem : rem * (1 - SHADOW_EPSILON);
+        }
         if (scene_occluded(S, &sray, C)) return zero;
         dRec->emitter = (int)index;
         dRec->pdf *= emPdf;
@@ -3046,7 +3057,7 @@ static inline float mi_weight(float pdfA, float pdfB) { /* path.cpp:296-300 */
 /* ------------------------------------------------------------------------ */
 /* MIPathTracer::Li (integrators/path/path.cpp:119-294)                      */
 /* ------------------------------------------------------------------------ */
-typedef struct { int maxDepth, rrDepth, strict, hide, hasAlpha; } PathParams;
+typedef struct { int maxDepth, rrDepth, strict, hide, hasAlpha, volpath; } PathParams;
 
 static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *alpha, int *depthOut, Counters *C) {
     Its its;
@@ -3070,8 +3081,9 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
         int isEmitter = S->meshes[its.mesh].emitter >= 0;
         if (isEmitter && emitted && (!P->hide || scattered))
             L = vadd(L, vmulv(throughput, its_Le(S, &its, vneg(ray.d))));
-        if ((depth >= P->maxDepth && P->maxDepth > 0) ||
-            (P->strict && vdot(ray.d, its.geoN) * its.wi.z >= 0))
+        /* volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi) */
+        const float snp = vdot(ray.d, its.geoN) * its.wi.z;
+        if ((depth >= P->maxDepth && P->maxDepth > 0) || (P->strict && (P->volpath ? snp > 0 : snp >= 0)))
             break;
 
         DRec dRec;
@@ -3081,7 +3093,7 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
         if (bsdf->flags & E_SMOOTH) {
             float nx, ny;
             next2d(smp, &nx, &ny);
-            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C);
+            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C, P->volpath);
             if (!vzero(value)) {
                 BRec bRec;
                 bRec.wi = its.wi;
@@ -3123,13 +3135,15 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
                 hitEmitter = 1;
             }
         } else {
-            /* path.cpp:233-247 */
-            if (!S->env) break;
-            if (P->hide && !scattered) break;
-            value = env_eval(S->env, &ray);
-            /* EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374) */
+            /* path.cpp:233-247; EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374) */
             float nearT, farT;
-            if (!env_bsphere(S->env, ray.o, ray.d, &nearT, &farT) || nearT > 0 || farT < 0) break;
+            if (!S->env || (P->hide && !scattered) || !env_bsphere(S->env, ray.o, ray.d, &nearT, &farT) ||
+                nearT > 0 || farT < 0) {
+                /* volpath.cpp:326-336: the miss still passes the RR step before the loop ends */
+                if (P->volpath && depth++ >= P->rrDepth) (void)next1d(smp);
+                break;
+            }
+            value = env_eval(S->env, &ray);
             dRec.p = ray_at(&ray, farT);
             dRec.n = vnormalize(vsub(S->env->center, dRec.p));
             dRec.measureSolidAngle = 1;
@@ -3144,7 +3158,10 @@ static V3 Li(const Scene *S, const PathParams *P, Ray ray, Sampler *smp, float *
             float lumPdf = !(bRec.sampledType & E_DELTA) ? pdf_emitter_direct(S, &dRec) : 0;
             L = vadd(L, vmul(vmulv(throughput, value), mi_weight(bsdfPdf, lumPdf)));
         }
-        if (!its.valid) break;
+        if (!its.valid) {
+            if (P->volpath && depth++ >= P->rrDepth) (void)next1d(smp);
+            break;
+        }
         emitted = 0;
         if (depth++ >= P->rrDepth) {
             float q = smin(smaxc(throughput) * eta * eta, (float)0.95f);
@@ -3204,7 +3221,7 @@ static V3 Li_direct(const Scene *S, const PathParams *P, const DirectParams *D, 
         for (uint32_t i = 0; i < D->nLum; ++i) {
             float nx = u2[0], ny = u2[1];
             if (D->nLum > 1) sampler_array2d(smp, D->lumDim, D->nLum, i, &nx, &ny);
-            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C);
+            V3 value = sample_emitter_direct(S, &dRec, nx, ny, C, 0);
             if (!vzero(value)) {
                 BRec bRec;
                 bRec.wi = its.wi;
@@ -3353,7 +3370,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     if (!g_sobol_ready) return MTSGPU_ESTATE;
     if (!scene || !P || !film) return MTSGPU_EINVAL;
     const int direct = P->integrator == MTSGPU_INTEGRATOR_DIRECT;
-    if (P->integrator != MTSGPU_INTEGRATOR_PATH && !direct) return MTSGPU_EINVAL;
+    if (P->integrator != MTSGPU_INTEGRATOR_PATH && P->integrator != MTSGPU_INTEGRATOR_VOLPATH && !direct) return MTSGPU_EINVAL;
     if (P->spp == 0 || (!direct && (P->rr_depth <= 0 || (P->max_depth <= 0 && P->max_depth != -1)))) return MTSGPU_EINVAL;
     if (direct && P->emitter_samples + P->bsdf_samples == 0) return MTSGPU_EINVAL;
     g_cr = libm_mode;
@@ -3368,7 +3385,8 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     const size_t filmFloats = (size_t)fw * fh * 5;
     float *spill = (float *)calloc(filmFloats, sizeof(float));
     memset(film, 0, filmFloats * sizeof(float));
-    PathParams PP = {P->max_depth, P->rr_depth, P->strict_normals, P->hide_emitters, P->has_alpha};
+    PathParams PP = {P->max_depth, P->rr_depth, P->strict_normals, P->hide_emitters, P->has_alpha,
+                     P->integrator == MTSGPU_INTEGRATOR_VOLPATH};
     const uint32_t rb = P->row_block ? P->row_block : 1, rs = P->row_stride ? P->row_stride : 1;
     Counters tot = {0, 0, 0, 0};
     uint64_t pathLen = 0, nsamples = 0;

@@ -264,6 +264,21 @@ def test_independent_sampler_bitexact(gpu_ctx, oracle, materials):
         assert st_g['rays'] == st_o['rays']
 
 
+def test_volpath_bitexact(gpu_ctx, oracle):
+    """volpath without media: evalTransmittance shadow segments (env without
+    shadow epsilon, re-normalised sphere-light directions), strictNormals and
+    path-length accounting, on the envmap scene and the analytic-shape box."""
+    from mitsuba_amd.scene import VolpathIntegrator
+    for sc, _ in (_c3_small(area_light=True), scenes.build('C1', width=32, height=32, spp=8, materials='shapes')):
+        v = VolpathIntegrator(sampleCount=8, rfilter='box', strictNormals=True)
+        gpu_ctx.upload(sc)
+        film_g, smp_g, st_g = gpu_ctx.render(v, samples=True)
+        film_o, smp_o, st_o = oracle.render(sc, v, samples=True, libm_mode=1)
+        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
+        assert same.mean() > 0.999, same.mean()
+        assert st_g['path_length_sum'] == st_o['path_length_sum']
+
+
 def test_direct_integrator_envmap_and_shapes(gpu_ctx, oracle):
     from mitsuba_amd.scene import DirectIntegrator
     for sc, _ in (_c3_small(area_light=True), scenes.build('C1', width=32, height=32, spp=4, materials='shapes')):
