@@ -118,6 +118,19 @@ __device__ __forceinline__ uint64_t sobol_lookup(const MtsgLookup &L, uint32_t f
     return index | ((uint64_t)jhi << m);
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs, each with its own L2.
+// Renumber them so that XCD x runs the x-th contiguous eighth of the grid: the
+// items (pixels in 8x8 tiles) the lanes of one XCD hold at a time are then
+// neighbours, and their rays share BVH nodes and triangles in that XCD's L2.
+__device__ __forceinline__ uint32_t xcd_block() {
+#ifdef MTSG_NO_XCD_REMAP
+    return blockIdx.x;
+#else
+    const uint32_t nb = gridDim.x;
+    return (nb % 8u == 0) ? (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u : blockIdx.x;
+#endif
+}
+
 struct SamplerState {
     uint64_t sobolIndex;
     uint32_t sampleIndex;
@@ -826,7 +839,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     unsigned long long cHits = 0, cNee = 0, cSobol = 0;
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    uint64_t item = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+    uint64_t item = (uint64_t)xcd_block() * BLOCK + threadIdx.x;
     bool active = false, done = false;
     int px = 0, py = 0;
     uint32_t j = 0, pix = 0;
@@ -1511,7 +1524,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
     };
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t it = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; it < L.num_items; it += lanes) {
+    for (uint64_t it = (uint64_t)xcd_block() * BLOCK + threadIdx.x; it < L.num_items; it += lanes) {
         const uint32_t jj = (uint32_t)(it / L.num_pixels);
         const uint32_t pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
         int px, py;
