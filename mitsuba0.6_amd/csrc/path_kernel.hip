@@ -1069,7 +1069,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                             f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
                             float pdf = 0.0f, dist = 0.0f;
                             f3 vlp = mk(0, 0, 0);   // dRec.p where it does not define dRec.d exactly (volpath)
-                            bool vrecomp = false, vsurf = true;
+                            bool vrecomp = false;
                             if (ENV && e.type != MTSG_EMITTER_AREA) {
 #ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
                                 glb_env *E = (glb_env *)S.env;
@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                                                  : env_sample_direct(E, P.its.p, ex, ey);
                                 value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
                                 vlp = add(P.its.p, mul(dd, dist));   // dRec.p = ray(farT) (envmap.cpp:536, constant.cpp:254)
-                                vrecomp = true; vsurf = false;
+                                vrecomp = true;
 #endif
                             } else if (ANA && S.shapes[e.shape].analytic >= 0) {
                                 const AnaSample as =
@@ -1150,12 +1150,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                 sd = dd;
                                 smaxt = dist * (1 - D_SHADOW_EPSILON);
                                 if (L.integrator == MTSG_INTEGRATOR_VOLPATH && vrecomp) {
-                                    // Scene::evalTransmittance (scene.cpp:619-679): the segment to dRec.p,
-                                    // re-normalised; no shadow epsilon towards an emitter not on a surface
+                                    // Scene::evalTransmittance (scene.cpp:619-679, 890): the segment to dRec.p,
+                                    // re-normalised; every supported emitter is EOnSurface (envmap.cpp:107,
+                                    // constant.cpp:48, area lights), so the shadow epsilon always applies
                                     const f3 v = sub(vlp, P.its.p);
                                     const float rem = dsqrt(len2(v));
                                     sd = divs(v, rem);
-                                    smaxt = vsurf ? rem * (1 - D_SHADOW_EPSILON) : rem;
+                                    smaxt = rem * (1 - D_SHADOW_EPSILON);
                                 }
                                 haveShadow = true;
                             }
@@ -1411,6 +1412,20 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
     return bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
 }
 
+// direct_kernel's shadow rays: the any-hit traversal as a separate (not
+// inlined) function.  Inlined into direct_kernel's nested divergent loops at
+// -O3, hipcc (ROCm 7.2, gfx950) produced wrong occlusion answers for 15% of the
+// samples of the analytic-shape scene; the same source is exact at -O1, as a
+// call, with the NaN-aware (closest-hit) form of the sphere predicate, and
+// inlined into path_kernel / trace_kernel (DESIGN.md 4 has the bisection)
+template <bool ANA, typename NodeT, typename TriT>
+__device__ __noinline__ bool shadow_any(NodeT *nodes, TriT *tris, f3 o, f3 d, float mint, float maxt,
+                                        lds_stk_n *stkN, lds_stk_d *stkD, unsigned long long &cN,
+                                        unsigned long long &cT, const MtsgAnalytic *ana) {
+    uint32_t sl = 0;
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    return traverse<true, false, ANA>(nodes, tris, o, d, mint, maxt, stkN, stkD, sl, a0, a1, a2, cN, cT, ana);
+}
 template <bool SCENE_LDS, int FEAT>
 __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLaunch L) {
     constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
@@ -1506,21 +1521,17 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         }
         return hit;
     };
-    // Shadow rays run the closest-hit traversal: the same occlusion answer as
-    // the any-hit instantiation, which hipcc (ROCm 7.2) miscompiles inside
-    // this kernel ("direct integrator")
     auto occluded = [&](f3 o, f3 d, float dist) -> bool {   // Ray(ref, d, Epsilon, dist*(1-ShadowEpsilon))
         cShadow++;
         float mint, maxt;
         if (!ray_interval(S, o, d, D_EPSILON, dist * (1 - D_SHADOW_EPSILON), true, mint, maxt)) return false;
-        uint32_t sl; float a0, a1, a2;
-        if (SCENE_LDS && L.scan)
-            return scan_tris<false, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, sl, a0, a1, a2, cT);
-        if (SCENE_LDS)
-            return traverse<false, false, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, sl, a0, a1, a2, cN, cT,
-                                               S.analytic);
-        return traverse<false, false, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD, sl, a0,
-                                           a1, a2, cN, cT, S.analytic);
+        if (SCENE_LDS && L.scan) {
+            uint32_t sl; float a0, a1, a2;
+            return scan_tris<true, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, sl, a0, a1, a2, cT);
+        }
+        if (SCENE_LDS) return shadow_any<ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, cN, cT, S.analytic);
+        return shadow_any<ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD, cN, cT,
+                               S.analytic);
     };
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;

@@ -3012,12 +3012,13 @@ static V3 sample_emitter_direct(const Scene *S, DRec *dRec, float sx, float sy, 
         if (volpath && (env || S->meshes[e->mesh].kind != MTSGPU_SHAPE_TRIMESH)) {
             /* Scene::sampleAttenuatedEmitterDirect -> evalTransmittance (scene.cpp:619-679, 876-898):
              * the segment to dRec.p (= ray(farT) for the environment, envmap.cpp:536, constant.cpp:254),
-             * re-normalised; no shadow epsilon towards an emitter that is not on a surface */
+             * re-normalised; every supported emitter is EOnSurface (area.cpp, envmap.cpp:107,
+             * constant.cpp:48), so lengthFactor = 1 - ShadowEpsilon on every segment (scene.cpp:624) */
             const V3 lp = env ? vadd(dRec->ref, vmul(dRec->d, dRec->dist)) : dRec->p;
             const V3 v = vsub(lp, dRec->ref);
             const float rem = sqrtf(vlen2(v));
             ray_set_dir(&sray, vdiv(v, rem));
-            sray.maxt = env ? rem : rem * (1 - SHADOW_EPSILON);
+            sray.maxt = rem * (1 - SHADOW_EPSILON);
         }
         if (scene_occluded(S, &sray, C)) return zero;
         dRec->emitter = (int)index;

@@ -19,12 +19,17 @@ def _bits(a):
     return np.ascontiguousarray(a, np.float32).view(np.uint32)
 
 
-def _compare(film_g, smp_g, film_o, smp_o):
+def _assert_records_equal(smp_g, smp_o, what=''):
+    """Every per-sample record (Li, alpha, position, depth, flags) bit-identical."""
     assert smp_g.shape == smp_o.shape
     same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
     bad = np.nonzero(~same)[0]
-    assert same.all(), 'per-sample mismatch at %d records, first: %s vs %s' % (
-        bad.size, smp_g[bad[:3]].tolist(), smp_o[bad[:3]].tolist())
+    assert same.all(), '%s: per-sample mismatch at %d of %d records, first %s: %s vs %s' % (
+        what, bad.size, same.size, bad[:3].tolist(), smp_g[bad[:3]].tolist(), smp_o[bad[:3]].tolist())
+
+
+def _compare(film_g, smp_g, film_o, smp_o):
+    _assert_records_equal(smp_g, smp_o)
     np.testing.assert_allclose(film_g, film_o, rtol=1e-6, atol=1e-7)
     frac = np.mean(_bits(film_g) == _bits(film_o))
     assert frac > 0.999, frac
@@ -84,8 +89,7 @@ def test_rough_bsdfs_all_materials(gpu_ctx, oracle):
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
         film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, (mi, same.mean())
+        _assert_records_equal(smp_g, smp_o, repr(mi))
 
 
 def _c3_small(**kw):
@@ -114,8 +118,7 @@ def test_envmap_variants(gpu_ctx, oracle):
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
         film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, (kw, hide, same.mean())
+        _assert_records_equal(smp_g, smp_o, repr((kw, hide)))
 
 
 def test_atrium_bitexact(gpu_ctx, oracle):
@@ -184,8 +187,7 @@ def test_smooth_bsdfs_all_materials(gpu_ctx, oracle):
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
         film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, (mi, same.mean())
+        _assert_records_equal(smp_g, smp_o, repr(mi))
 
 
 def test_analytic_shapes_bitexact(gpu_ctx, oracle):
@@ -213,8 +215,7 @@ def test_analytic_shapes_under_envmap(gpu_ctx, oracle):
     gpu_ctx.upload(sc)
     film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
     film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
-    same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-    assert same.mean() > 0.999, same.mean()
+    _assert_records_equal(smp_g, smp_o)
 
 
 def test_constant_emitter_bitexact(gpu_ctx, oracle):
@@ -259,14 +260,13 @@ def test_independent_sampler_bitexact(gpu_ctx, oracle, materials):
                                 bsdfSamples=2)):
         film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
         film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, same.mean()
+        _assert_records_equal(smp_g, smp_o)
         assert st_g['rays'] == st_o['rays']
 
 
 def test_volpath_bitexact(gpu_ctx, oracle):
-    """volpath without media: evalTransmittance shadow segments (env without
-    shadow epsilon, re-normalised sphere-light directions), strictNormals and
+    """volpath without media: evalTransmittance shadow segments (shadow epsilon on
+    every emitter, re-normalised env / sphere-light directions), strictNormals and
     path-length accounting, on the envmap scene and the analytic-shape box."""
     from mitsuba_amd.scene import VolpathIntegrator
     for sc, _ in (_c3_small(area_light=True), scenes.build('C1', width=32, height=32, spp=8, materials='shapes')):
@@ -274,8 +274,7 @@ def test_volpath_bitexact(gpu_ctx, oracle):
         gpu_ctx.upload(sc)
         film_g, smp_g, st_g = gpu_ctx.render(v, samples=True)
         film_o, smp_o, st_o = oracle.render(sc, v, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, same.mean()
+        _assert_records_equal(smp_g, smp_o)
         assert st_g['path_length_sum'] == st_o['path_length_sum']
 
 
@@ -286,8 +285,7 @@ def test_direct_integrator_envmap_and_shapes(gpu_ctx, oracle):
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(d, samples=True)
         film_o, smp_o, _ = oracle.render(sc, d, samples=True, libm_mode=1)
-        same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
-        assert same.mean() > 0.999, same.mean()
+        _assert_records_equal(smp_g, smp_o)
 
 
 def _random_rays(sc, n, seed):
