@@ -4,35 +4,35 @@
 Workload (BASELINE.json configs[1]): Cornell box, 1280x720, 512 spp, sobol,
 path maxDepth=-1 rrDepth=5, box filter.  One step = one full frame
 (471,859,200 samples = one pass of the hot path over the frame) rendered into
-an HBM-resident film; with N GPUs the frame's rows are sharded (8-row blocks,
-interleaved over ranks) and the films are reduced to rank 0 with one RCCL
-reduce over xGMI (the reference's Film::put merge, renderproc.cpp:142-149).
-Total work is fixed as N grows: scaling "strong".
+an HBM-resident film; with N GPUs the frame's rows are sharded (row blocks
+interleaved over ranks, sized so every rank gets the same number of rows) and
+the films are summed onto rank 0 with one RCCL reduce over xGMI (the
+reference's Film::put merge, renderproc.cpp:142-149).  Total work is fixed as
+N grows: scaling "strong".
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 through
-torch.distributed.run (one process per GPU, RCCL backend).
+Launch: `python bench.py [--gpus N --steps K --warmup W]`.  With N > 1 and no
+torch.distributed environment, this process starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py` as a child
+(one process per GPU, RCCL backend) before touching the GPU, and exits with
+its status; under torch.distributed.run WORLD_SIZE must equal N.
+
+`--device cpu-oracle` is a launcher rehearsal for machines without a GPU (the
+CPU test suite): each rank renders its rows with the CPU oracle and the films
+are reduced over gloo.  It is never selected implicitly; the GPU path fails
+loudly when the HIP library or the GPU is missing.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, REPO)
-
-import torch  # noqa: E402  (loads the HIP runtime first; libmtsgpu shares it)
-import torch.distributed as dist  # noqa: E402
-
-from pkgimport import mitsuba_amd  # noqa: E402
-
-mitsuba_amd()
-from mitsuba_amd import film_border, scenes  # noqa: E402
-from mitsuba_amd.distributed import ROW_BLOCK, RowSharding  # noqa: E402
-from mitsuba_amd.integrator import Context  # noqa: E402
-
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BASELINE_METRIC = 'Msamples/s (and s/frame) at 512 spp, 1280×720; 1/2/4/8 MI355X + CPU ref'
 WORKLOADS = {
     'C1': 'C1: Cornell box 512x512 64 spp (plumbing config)',
     'C2': 'C2: Cornell box (32 tris, diffuse, area light), path maxDepth=-1 rrDepth=5, sobol, box filter',
@@ -44,6 +44,51 @@ WORKLOADS = {
           '2D rough-transmittance slice (50 alpha x 100 theta) per shading point, 1024x512 envmap, 1024 spp, '
           'path maxDepth=-1 rrDepth=5, sobol, box filter',
 }
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='C2')
+    ap.add_argument('--size', default=None, help='WxHxSPP override (launcher rehearsals and tests only)')
+    ap.add_argument('--device', default='gpu', choices=['gpu', 'cpu-oracle'])
+    ap.add_argument('--save-film', default=None, help='rank 0 writes the reduced film (.npy) after the last step')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-threads', type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args):
+    """Start one process per GPU through torch.distributed.run (as a child: this
+    process has not touched the GPU and never execs) and return its exit code;
+    None when this process is already a rank or N == 1."""
+    world_env = os.environ.get('WORLD_SIZE')
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.exit('bench.py: --gpus %d but WORLD_SIZE=%s; launch with --nproc-per-node %d' %
+                     (args.gpus, world_env, args.gpus))
+        return None
+    if args.gpus == 1:
+        return None
+    if args.gpus < 1:
+        sys.exit('bench.py: --gpus must be >= 1')
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '1')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args.gpus),
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    return subprocess.call(cmd, env=env)
 
 
 def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
@@ -61,136 +106,233 @@ def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
     return b / n
 
 
+def measured_profile(kind, cfg):
+    """The newest committed summary profiles/<round>_<kind>_<cfg>.json (traffic:
+    HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
+    tools/traffic_summary.py; valu: VALU-busy / issue fractions from SQ counters,
+    tools/valu_summary.py); None when none exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_%s_%s.json' % (kind, cfg))))
+    if not files:
+        return None
+    t = json.load(open(files[-1]))
+    t['source'] = os.path.basename(files[-1])
+    return t
+
+
+def host_info():
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
+
+
+def cpu_baseline(scene, integ, threads):
+    """The CPU restatement (oracle, OpenMP, glibc transcendentals as the
+    reference) on a bounded sample of the same workload: the full frame at a
+    reduced spp (the first spp Sobol samples of every pixel).  Threads: all
+    cores this job may use -- OMP_NUM_THREADS when the host sets it (the GPU
+    boxes give a job a 16-CPU share of a larger machine), else the affinity
+    mask."""
+    import copy
+    import oracle.binding as ob
+    model, ncpu, avail = host_info()
+    omp = os.environ.get('OMP_NUM_THREADS')
+    if not threads:
+        threads = int(omp) if omp and omp.isdigit() and int(omp) > 0 else avail
+    it = copy.copy(integ)
+    it.sampleCount = min(integ.sampleCount, 256)
+    t0 = time.perf_counter()
+    _, _, st = ob.render(scene, it, libm_mode=0, threads=threads)
+    dt = time.perf_counter() - t0
+    return {'value': round(st['samples'] / dt / 1e6, 3), 'unit': 'Msamples/s', 'cores': threads, 'kind': 'port',
+            'sample': '%dx%d at %d spp (%d samples, %.1f s)' % (scene.sensor.width, scene.sensor.height,
+                                                                it.sampleCount, st['samples'], dt),
+            'cpu_model': model, 'host_cpus': ncpu, 'affinity_cpus': avail, 'omp_num_threads': omp}
+
+
+def build_scene(args):
+    sys.path.insert(0, REPO)
+    from pkgimport import mitsuba_amd
+    mitsuba_amd()
+    from mitsuba_amd import scenes
+    kw = {'rfilter': 'box'}
+    if args.size:
+        w, h, spp = (int(v) for v in args.size.lower().split('x'))
+        kw.update(width=w, height=h, spp=spp)
+    return scenes.build(args.config, **kw)
+
+
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=3)
-    ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--config', default='C2')
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-threads', type=int, default=0)
-    args = ap.parse_args()
+    args = parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+
+    import torch  # loads the HIP runtime first; libmtsgpu shares it
+    import torch.distributed as dist
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.cuda.current_device()
-
-    scene, integ = scenes.build(args.config, rfilter='box')
+    scene, integ = build_scene(args)
+    from mitsuba_amd import film_border
+    from mitsuba_amd.distributed import RowSharding
     W, H, spp = scene.sensor.width, scene.sensor.height, integ.sampleCount
-    ctx = Context(dev)
-    t_up = time.time()
-    ctx.upload(scene)
-    upload_s = time.time() - t_up
     b = film_border(integ.rfilter, integ.rfilterParam)
-    film = torch.zeros(((H + 2 * b) * (W + 2 * b) * 5,), dtype=torch.float32, device='cuda')
-    stream = torch.cuda.current_stream().cuda_stream
-    shard = RowSharding(rank, world, ROW_BLOCK)
+    shard = RowSharding.for_frame(rank, world, H)
     row = shard.row_params()
+    gpu = args.device == 'gpu'
 
-    def step():
-        st = ctx.render_device(integ, film.data_ptr(), stream, row=row)
-        shard.reduce(film, dist)
-        return st
+    if gpu:
+        if not torch.cuda.is_available():
+            sys.exit('bench.py: no GPU visible (the HIP path has no CPU fallback; --device cpu-oracle is the '
+                     'launcher rehearsal)')
+        torch.cuda.set_device(local)
+        if world > 1:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        from mitsuba_amd.integrator import Context
+        ctx = Context(torch.cuda.current_device())
+        t_up = time.time()
+        ctx.upload(scene)
+        upload_s = time.time() - t_up
+        film = torch.zeros(((H + 2 * b) * (W + 2 * b) * 5,), dtype=torch.float32, device='cuda')
+        stream = torch.cuda.current_stream().cuda_stream
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(max(args.steps, 1))]
+
+        def step(k=None):   # mtsgpu_render_device clears the film on the stream
+            st = ctx.render_device(integ, film.data_ptr(), stream, row=row)
+            if k is not None:
+                ev[k][0].record()
+            shard.reduce(film, dist)
+            if k is not None:
+                ev[k][1].record()
+            return st
+
+        def sync():
+            torch.cuda.synchronize()
+    else:
+        if world > 1:
+            dist.init_process_group('gloo')
+        import oracle.binding as ob
+        upload_s = 0.0
+        film = torch.zeros(((H + 2 * b) * (W + 2 * b) * 5,), dtype=torch.float32)
+        threads = max(1, (os.cpu_count() or 1) // world)
+
+        def step(k=None):
+            f, _, st = ob.render(scene, integ, row=row, threads=threads)
+            film.copy_(torch.from_numpy(f.reshape(-1)))
+            t = time.perf_counter()
+            shard.reduce(film, dist)
+            st['reduce_s'] = time.perf_counter() - t
+            st['kernel_ms'] = 0.0
+            return st
+
+        def sync():
+            pass
+
+    if world > 1:
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
-    kernel_ms = []
+    kernel_ms, reduce_s = [], []
     samples_rank = 0
-    for _ in range(args.steps):
-        st = step()
+    for k in range(args.steps):
+        st = step(k)
         kernel_ms.append(st['kernel_ms'])
+        if 'reduce_s' in st:
+            reduce_s.append(st['reduce_s'])
         samples_rank += st['samples']
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
-    s = torch.tensor([samples_rank], dtype=torch.float64, device='cuda')
+    if gpu:
+        reduce_s = [ev[k][0].elapsed_time(ev[k][1]) / 1e3 for k in range(args.steps)]
+    dev = 'cuda' if gpu else 'cpu'
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    s = torch.tensor([samples_rank], dtype=torch.float64, device=dev)
+    r = torch.tensor([max(reduce_s) if reduce_s else 0.0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        dist.all_reduce(r, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
     total_samples = float(s.item())
     frame_samples = W * H * spp
     assert int(total_samples) == frame_samples * args.steps, (total_samples, frame_samples)
 
     if rank == 0:
+        if args.save_film:
+            import numpy as np
+            np.save(args.save_film, film.cpu().numpy().reshape(H + 2 * b, W + 2 * b, 5))
         value = total_samples / elapsed_max / 1e6
-        # roofline: traversal counters from a bounded stats pass (1/16 of the rows), always
-        # through the BVH: tiny scenes' linear TriAccel scan (an implementation choice that
-        # reads every record from the scalar cache) must not inflate the workload's bytes
-        os.environ['MTSGPU_NO_SCAN'] = '1'
-        try:
-            _, _, sst = ctx.render(integ, row=(ROW_BLOCK, 16, 0), traversal_stats=True)
-        finally:
-            os.environ.pop('MTSGPU_NO_SCAN', None)
-        bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
-        avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
-        per_launch_samples = samples_rank / max(1, len(kernel_ms))
-        achieved = bps * per_launch_samples / avg_kernel_s / 1e9
-        roofline = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
-                    'frac': round(achieved / HBM_PEAK_GBPS, 5), 'traffic': measured_traffic(args.config),
-                    'algorithmic_bytes_per_sample': round(bps, 1),
-                    'kernel_ms_avg': round(avg_kernel_s * 1e3, 3)}
+        roofline = None
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(scene, integ, args.cpu_threads)
+        if gpu:
+            # roofline: traversal counters from a bounded stats pass (1/16 of the rows), always
+            # through the BVH: tiny scenes' linear TriAccel scan (an implementation choice that
+            # reads every record from the scalar cache) must not inflate the workload's bytes
+            os.environ['MTSGPU_NO_SCAN'] = '1'
+            try:
+                _, _, sst = ctx.render(integ, row=(8, 16, 0), traversal_stats=True)
+            finally:
+                os.environ.pop('MTSGPU_NO_SCAN', None)
+            bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
+            avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
+            per_launch_samples = samples_rank / max(1, len(kernel_ms))
+            achieved = bps * per_launch_samples / avg_kernel_s / 1e9
+            traffic = measured_profile('traffic', args.config)
+            roofline = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+                        'frac': round(achieved / HBM_PEAK_GBPS, 5),
+                        'traffic': traffic and {'bytes_per_launch': traffic['hbm_bytes_per_launch'], 'unit': 'B',
+                                                'write_bytes_per_sample': traffic.get('write_bytes_per_sample'),
+                                                'source': traffic['source']},
+                        'valu': measured_profile('valu', args.config),
+                        'algorithmic_bytes_per_sample': round(bps, 1),
+                        'kernel_ms_avg': round(avg_kernel_s * 1e3, 3)}
+            if not args.no_cpu_baseline and world == 1:
+                cpu = cpu_baseline(scene, integ, args.cpu_threads)
+        metric = BASELINE_METRIC if args.config == 'C2' and not args.size else \
+            'Msamples/s (and s/frame) at %d spp, %dx%d' % (spp, W, H)
         out = {
-            'metric': 'Msamples/s (and s/frame) at 512 spp, 1280x720', 'value': round(value, 2),
+            'metric': metric, 'value': round(value, 2),
             'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed_max / args.steps * 1e3, 2), 'higher_is_better': True,
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': WORKLOADS.get(args.config, args.config), 'width': W, 'height': H, 'spp': spp,
-                       'samples_per_frame': frame_samples, 'parallelism': 'rows sharded x%d + RCCL film reduce' % world,
+                       'samples_per_frame': frame_samples,
+                       'parallelism': 'rows sharded x%d (row block %d) + %s film reduce' % (
+                           world, shard.row_block, 'RCCL' if gpu else 'gloo'),
+                       'world_size_reported': dist.get_world_size() if world > 1 else 1,
+                       'reduce_ms_max': round(float(r.item()) * 1e3, 3),
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},
             'roofline': roofline,
             'cpu_baseline': cpu,
         }
-        print(json.dumps(out))
+        if not gpu:
+            out['device'] = 'cpu-oracle launcher rehearsal (not a GPU measurement)'
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def measured_traffic(cfg):
-    """HBM bytes per launch of the path kernel on this workload from the committed
-    PMC passes (profiles/<round>_traffic_<cfg>.json, written by
-    tools/traffic_summary.py from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md); None when no summary exists."""
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', '*_traffic_%s.json' % cfg)))
-    if not files:
-        return None
-    t = json.load(open(files[-1]))
-    return {'bytes_per_launch': t['hbm_bytes_per_launch'], 'unit': 'B', 'source': os.path.basename(files[-1])}
-
-
-def cpu_baseline(scene, integ, threads):
-    """The CPU restatement (oracle, OpenMP over host cores) on a bounded sample of
-    the same workload: the full 1280x720 frame at 256 spp (first 256 Sobol samples
-    of every pixel)."""
-    import oracle.binding as ob
-    import copy
-    threads = threads or min(16, os.cpu_count() or 1)
-    it = copy.copy(integ)
-    it.sampleCount = 256
-    t0 = time.perf_counter()
-    _, _, st = ob.render(scene, it, libm_mode=0, threads=threads)
-    dt = time.perf_counter() - t0
-    return {'value': round(st['samples'] / dt / 1e6, 3), 'unit': 'Msamples/s', 'cores': threads, 'kind': 'port',
-            'sample': '%dx%d at 256 spp (%d samples, %.1f s)' % (scene.sensor.width, scene.sensor.height,
-                                                                 st['samples'], dt)}
 
 
 if __name__ == '__main__':

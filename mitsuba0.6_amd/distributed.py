@@ -13,11 +13,27 @@ filter-border splats, which the reference also accumulates by addition.
 ROW_BLOCK = 8
 
 
+def balanced_row_block(height, world, preferred=ROW_BLOCK):
+    """The largest row block <= `preferred` (8, 4, 2, 1) whose block count divides
+    evenly over the ranks, so that every rank renders the same number of rows
+    (720 rows: 8 for 1-2 ranks, 4 for 4, 2 for 8); 1 when none does."""
+    b = preferred
+    while b > 1:
+        if -(-height // b) % world == 0:
+            return b
+        b //= 2
+    return 1
+
+
 class RowSharding:
     def __init__(self, rank=0, world=1, row_block=ROW_BLOCK):
         if world < 1 or not (0 <= rank < world) or row_block < 1:
             raise ValueError('bad sharding rank=%r world=%r row_block=%r' % (rank, world, row_block))
         self.rank, self.world, self.row_block = rank, world, row_block
+
+    @classmethod
+    def for_frame(cls, rank, world, height):
+        return cls(rank, world, balanced_row_block(height, world))
 
     def row_params(self):
         """(row_block, row_stride, row_phase) of mtsgpu_render_params."""
