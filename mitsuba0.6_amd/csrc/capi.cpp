@@ -65,7 +65,7 @@ struct mtsgpu_ctx {
     HostScene host;
     MtsgDeviceScene dscene;
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
-    DevBuf env, env_texels, env_rows, env_cols, env_weights;
+    DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
     DevBuf film_own, film_spill, samples, counters, contrib;
@@ -178,6 +178,14 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         H.env.cdf_rows = (const float *)ctx->env_rows.p;
         H.env.cdf_cols = (const float *)ctx->env_cols.p;
         H.env.row_weights = (const float *)ctx->env_weights.p;
+        H.env.guide_rows = H.env.guide_cols = nullptr;
+        if (!H.env_guide_rows.empty()) {
+            if ((e = upload(ctx->env_grows, H.env_guide_rows, s)) != hipSuccess ||
+                (e = upload(ctx->env_gcols, H.env_guide_cols, s)) != hipSuccess)
+                return hip_fail(ctx, e, "envmap upload");
+            H.env.guide_rows = (const uint16_t *)ctx->env_grows.p;
+            H.env.guide_cols = (const uint16_t *)ctx->env_gcols.p;
+        }
         if ((e = ctx->env.ensure(sizeof(MtsgEnv))) != hipSuccess ||
             (e = hipMemcpyAsync(ctx->env.p, &H.env, sizeof(MtsgEnv), hipMemcpyHostToDevice, s)) != hipSuccess)
             return hip_fail(ctx, e, "envmap upload");
@@ -495,7 +503,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
-                      &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights,
+                      &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out};
     for (DevBuf *b : bufs) b->release();

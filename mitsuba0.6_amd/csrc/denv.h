@@ -197,9 +197,17 @@ __device__ __forceinline__ bool env_bsphere(glb_env *E, f3 ro, f3 d, float &near
     return true;
 }
 
-// sampleReuse of the envmap's float CDFs (envmap.cpp:687-692)
-__device__ __forceinline__ uint32_t env_sample_reuse(glb_f32 *__restrict__ cdf, uint32_t size, float &sample) {
-    uint32_t lo = 0, hi = size + 1;                        // std::lower_bound
+// sampleReuse of the envmap's float CDFs (envmap.cpp:687-692): std::lower_bound
+// over [lo, hi), narrowed by the guide table when there is one (MtsgEnv::guide_*:
+// the same index as the full-range search)
+typedef __attribute__((address_space(1))) const uint16_t glb_u16;
+__device__ __forceinline__ uint32_t env_sample_reuse(glb_f32 *__restrict__ cdf, glb_u16 *guide, uint32_t gbits,
+                                                     uint32_t size, float &sample) {
+    uint32_t lo = 0, hi = size + 1;
+    if (guide) {
+        const uint32_t k = (uint32_t)(sample * (float)(1u << gbits));   // exact scaling, floor
+        if (k < (1u << gbits)) { lo = guide[k]; hi = guide[k + 1]; }
+    }
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (cdf[mid] < sample) lo = mid + 1; else hi = mid;
@@ -221,8 +229,11 @@ __device__ __forceinline__ float interval_to_tent(float s) {   // warp.cpp:143-1
 // (envmap.cpp:567-603): returns value/pdf; pdf = 0 on failure
 __device__ __forceinline__ f3 env_sample_direct_impl(glb_env *E, f3 ref, float sx, float sy, f3 &dOut, float &dist, float &pdfOut) {
     const uint32_t W = (uint32_t)E->w0, H = (uint32_t)E->h0;
-    const uint32_t row = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_rows, H, sy);
-    const uint32_t col = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_cols + (size_t)row * (W + 1), W, sx);
+    glb_u16 *gr = (glb_u16 *)(uintptr_t)E->guide_rows, *gc = (glb_u16 *)(uintptr_t)E->guide_cols;
+    const uint32_t row = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_rows, gr, E->guide_rbits, H, sy);
+    const uint32_t col = env_sample_reuse((glb_f32 *)(uintptr_t)E->cdf_cols + (size_t)row * (W + 1),
+                                          gc ? gc + (size_t)row * ((1u << E->guide_cbits) + 1) : nullptr,
+                                          E->guide_cbits, W, sx);
     const float posx = (float)col + interval_to_tent(sx), posy = (float)row + interval_to_tent(sy);
     const int xPos = (int)floorf(posx), yPos = (int)floorf(posy);
     const float dx1 = posx - (float)xPos, dx2 = 1.0f - dx1, dy1 = posy - (float)yPos, dy2 = 1.0f - dy1;

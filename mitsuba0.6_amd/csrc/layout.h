@@ -155,6 +155,11 @@ struct MtsgEnv {
     const float *cdf_rows;          // h0 + 1
     const float *cdf_cols;          // h0 * (w0 + 1)
     const float *row_weights;       // h0
+    // guide tables of the two CDF searches (cutpoint method): for u in [k/G, (k+1)/G)
+    // std::lower_bound(cdf, u) lies in [guide[k], guide[k+1]]; null: full-range search
+    const uint16_t *guide_rows;     // (1 << guide_rbits) + 1
+    const uint16_t *guide_cols;     // h0 * ((1 << guide_cbits) + 1)
+    uint32_t guide_rbits, guide_cbits;
 };
 
 struct MtsgDeviceScene {

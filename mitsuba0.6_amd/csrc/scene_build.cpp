@@ -805,6 +805,45 @@ std::vector<float> resample_level(const std::vector<float> &src, int w, int h, i
 
 // EnvironmentMap ctor (envmap.cpp:105-185: TMIPMap with EEWA, anisotropy 10,
 // mipmap.h:155-301) and configure() (envmap.cpp:261-321)
+// Guide tables for the envmap's two CDF searches (the cutpoint method): with
+// G = 2^bits buckets, guide[k] = lower_bound(cdf, k / G).  For u in [k/G,
+// (k+1)/G) the reference's std::lower_bound(cdf, u) (envmap.cpp:687-692) lies
+// in [guide[k], guide[k+1]] because the CDF is non-decreasing, so the device
+// searches that range only and lands on the same index.  A CDF that is not
+// non-decreasing (negative or NaN texels) keeps the full-range search: its
+// lower_bound depends on the search path.
+static uint32_t guide_bits(uint32_t size) {
+    uint32_t b = 0;
+    while ((1u << b) < size && b < 12) ++b;
+    return b;
+}
+static void build_guide(const float *cdf, uint32_t size, uint32_t bits, uint16_t *g) {
+    const uint32_t G = 1u << bits;
+    bool mono = true;
+    for (uint32_t i = 0; i < size; ++i) mono &= cdf[i] <= cdf[i + 1];
+    for (uint32_t k = 0; k <= G; ++k) {
+        if (!mono) { g[k] = (uint16_t)(k == 0 ? 0 : size + 1); continue; }
+        const float u = (float)k * (1.0f / (float)G);   // exact: G is a power of two
+        g[k] = (uint16_t)(std::lower_bound(cdf, cdf + size + 1, u) - cdf);
+    }
+}
+static void build_env_guides(HostScene &S, int W, int H) {
+    S.env_guide_rows.clear();
+    S.env_guide_cols.clear();
+    MtsgEnv &E = S.env;
+    E.guide_rbits = E.guide_cbits = 0;
+    if (W + 1 > 65535 || H + 1 > 65535 || std::getenv("MTSGPU_NO_ENV_GUIDE")) return;
+    E.guide_rbits = guide_bits((uint32_t)H);
+    E.guide_cbits = guide_bits((uint32_t)W);
+    const uint32_t gr = (1u << E.guide_rbits) + 1, gc = (1u << E.guide_cbits) + 1;
+    S.env_guide_rows.assign(gr, 0);
+    S.env_guide_cols.assign((size_t)gc * H, 0);
+    build_guide(S.env_cdf_rows.data(), (uint32_t)H, E.guide_rbits, S.env_guide_rows.data());
+    for (int y = 0; y < H; ++y)
+        build_guide(S.env_cdf_cols.data() + (size_t)y * (W + 1), (uint32_t)W, E.guide_cbits,
+                    S.env_guide_cols.data() + (size_t)y * gc);
+}
+
 int build_envmap(const mtsgpu_emitter_desc &e, int index, HostScene &S, std::string &err) {
     const int W = (int)e.env_width, H = (int)e.env_height;
     if (!e.env_rgb || W <= 0 || H <= 0) { err = "envmap: missing image data"; return MTSGPU_EINVAL; }
@@ -885,6 +924,7 @@ int build_envmap(const mtsgpu_emitter_desc &e, int index, HostScene &S, std::str
         err = "The environment map contains an invalid floating point value (nan/inf) -- giving up.";
         return MTSGPU_EINVAL;
     }
+    build_env_guides(S, W, H);
     E.normalization = 1.0f / (rowSum * (2 * kPi / (float)W) * (kPi / (float)H));
     E.pixel_x = 2 * kPi / (float)W;
     E.pixel_y = kPi / (float)H;

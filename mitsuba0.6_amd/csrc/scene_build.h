@@ -42,6 +42,7 @@ struct HostScene {
     MtsgEnv env;
     std::vector<uint16_t> env_texels;
     std::vector<float> env_cdf_rows, env_cdf_cols, env_row_weights;
+    std::vector<uint16_t> env_guide_rows, env_guide_cols;   // MtsgEnv::guide_* (empty: no guide)
     // roughplastic tables (MtsgBsdf::rt_ext / rt_int offsets) and per-vertex UVs
     std::vector<float> rtrans, texcoords;
     bool ext = false;   // roughplastic or textured BSDFs: the MTSG_FEAT_EXT kernel variant

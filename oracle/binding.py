@@ -9,22 +9,34 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, '_build', 'liboracle.so')
+# the same source built with the reference's release flags (Makefile REFFLAGS)
+LIB_REFFLAGS = os.path.join(HERE, '_build', 'liboracle_refflags.so')
 _lib = None
+_libs = {}
 
 
-def _stale():
-    if not os.path.exists(LIB):
+def _stale(path=LIB):
+    if not os.path.exists(path):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(path)
     srcs = [os.path.join(HERE, f) for f in ('mts_oracle.c', 'mts_oracle.h', 'Makefile')]
     srcs.append(os.path.join(os.path.dirname(HERE), 'include', 'mtsgpu.h'))
     return any(os.path.getmtime(f) > t for f in srcs if os.path.exists(f))
 
 
-def lib():
+def lib(variant='strict'):
+    """The oracle library: 'strict' (source order, the parity checker) or
+    'refflags' (the reference's -funsafe-math-optimizations release flags)."""
     global _lib
-    if _lib is None:
-        if _stale():   # a stale checker silently compares against old semantics: rebuild it
+    path = LIB if variant == 'strict' else LIB_REFFLAGS
+    if variant != 'strict' and variant != 'refflags':
+        raise ValueError('unknown oracle variant %r' % variant)
+    if variant == 'strict' and _lib is not None:
+        return _lib
+    if variant in _libs:
+        return _libs[variant]
+    if True:
+        if _stale(path):   # a stale checker silently compares against old semantics: rebuild it
             import subprocess
             subprocess.run(['make', '-s', '-C', HERE], check=True)
         import sys
@@ -32,7 +44,7 @@ def lib():
         from pkgimport import mitsuba_amd
         m = mitsuba_amd()
         abi = m.abi
-        L = C.CDLL(LIB)
+        L = C.CDLL(path)
         L.oracle_sobol_init.argtypes = [C.c_char_p]
         L.oracle_render.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(abi.RenderParams),
                                     C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(abi.Stats),
@@ -58,8 +70,10 @@ def lib():
         rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
         if rc != 0:
             raise RuntimeError('oracle_sobol_init failed: %d' % rc)
-        _lib = L
-    return _lib
+        _libs[variant] = L
+        if variant == 'strict':
+            _lib = L
+    return L
 
 
 def trace_rays(scene, o, d, mint=1e-4, maxt=np.inf, shadow=False):
@@ -84,13 +98,14 @@ def configure_rc(scene):
     return lib().oracle_configure(C.byref(d))
 
 
-def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0)):
-    """Render with the oracle; returns (film (H+2b, W+2b, 5), samples or None, stats dict)."""
+def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0), variant='strict'):
+    """Render with the oracle; returns (film (H+2b, W+2b, 5), samples or None, stats dict).
+    variant='refflags' renders with the reference-flags build (lib())."""
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     from pkgimport import mitsuba_amd
     m = mitsuba_amd()
-    L = lib()
+    L = lib(variant)
     W, H = scene.sensor.width, scene.sensor.height
     x0, y0, w, h = window if window else (getattr(integ, 'crop', None) or (0, 0, W, H))
     p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])

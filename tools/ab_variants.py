@@ -39,7 +39,7 @@ sc, it = scenes.build(cfg, rfilter='box')
 ctxs = {}
 for name, path in variants:
     c = Context(0, lib_path=path)
-    c.upload(sc)
+    with_env(name, lambda: c.upload(sc))
     with_env(name, lambda: c.render(it, row=(8, stride, 0)))   # warm up
     ctxs[name] = c
 res = {n: [] for n, _ in variants}

@@ -27,15 +27,25 @@ def counter(path_glob, name):
     return vals
 
 
+# samples per profiled launch (one full frame; C5's 1024 spp renders as two 512-spp launches)
+SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 512}
+
 for cfg in ('C2', 'C3', 'C4', 'C5'):
     fetch = counter(os.path.join(src, 'pmc_%s_FETCH_SIZE' % cfg, '**', '*counter_collection.csv'), 'FETCH_SIZE')
     write = counter(os.path.join(src, 'pmc_%s_WRITE_SIZE' % cfg, '**', '*counter_collection.csv'), 'WRITE_SIZE')
     if fetch and write:
         f, w = sum(fetch) / len(fetch), sum(write) / len(write)
+        samples = SAMPLES.get(cfg)
         out = {'config': cfg, 'kernel': 'path_kernel', 'launches': len(fetch), 'FETCH_SIZE_KiB': f, 'WRITE_SIZE_KiB': w,
                'hbm_bytes_per_launch': 2 * f * 1024 + w * 1024,
-               'note': 'one full frame (tools/prof_run.py %s 1 1); FETCH_SIZE doubled (gfx950 counts half of wide '
-                       'reads), WRITE_SIZE as reported' % cfg}
+               'hbm_bytes_per_launch_fetch_raw': f * 1024 + w * 1024,
+               'write_bytes_per_sample': w * 1024 / samples if samples else None,
+               'read_bytes_per_sample_raw': f * 1024 / samples if samples else None,
+               'note': 'one full frame (tools/prof_run.py %s 1 1). hbm_bytes_per_launch doubles FETCH_SIZE '
+                       '(MI355X_MICROARCH.md: gfx950 counts half of 16 B/lane streaming reads), an upper bound '
+                       'for the scattered node/triangle reads whose width is uncalibrated; '
+                       'hbm_bytes_per_launch_fetch_raw is the undoubled lower bound. WRITE_SIZE as reported '
+                       '(exact for 16 B/lane stores and float atomics)' % cfg}
         json.dump(out, open(os.path.join(prof, '%s_traffic_%s.json' % (rnd, cfg)), 'w'), indent=1)
         print(cfg, out)
     for f in glob.glob(os.path.join(src, 'bench_%s' % cfg, '**', '*kernel_stats.csv'), recursive=True):
