@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 4
+#define MTSGPU_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -215,6 +215,11 @@ enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1 };
 
 /* render flags */
 #define MTSGPU_FLAG_TRAVERSAL_STATS 1u  /* count BVH node visits / TriAccel tests   */
+/* execution engine of the path / volpath integrators (same per-sample results):
+   the persistent megakernel or the wavefront pipeline (per-bounce ray queues);
+   neither flag: the library's per-scene default */
+#define MTSGPU_FLAG_WAVEFRONT 2u
+#define MTSGPU_FLAG_MEGAKERNEL 4u
 
 /* Film layout produced by mtsgpu_render: an ImageBlock of the full crop
  * (film_width+2b) x (film_height+2b) pixels, 5 floats each {R,G,B,alpha,w},
@@ -300,6 +305,10 @@ int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */
 int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *out, int n);
 int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4);
+/* the 16 raw device counters of the last render (samples, rays, shadow rays,
+   path lengths, node visits, TriAccel tests, dimension errors, hits, -, NEE
+   samples, Sobol HBM words, diagnostic section cycles 11-15) */
+int mtsgpu_debug_counters(mtsgpu_ctx *ctx, uint64_t *out16);
 /* Host-only (no device needed): configure `scene` and return its environment
  * emitter's tables -- params[64] = {levels, w0, h0, normalization, pixel_x,
  * pixel_y, scale, center xyz, radius, total texels, .., lw[l] at 16+l, lh[l] at

@@ -27,6 +27,13 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
 hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32_t n, float *out, bool shadow,
                              uint32_t stackDepth, int numCUs, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
+hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
+                                bool instr, hipStream_t s);
+hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
+                                bool stats, hipStream_t s);
+hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters,
+                                hipStream_t s);
+int mtsg_wf_occupancy(const MtsgLaunch &L, int *shadeBpc, int *traceBpc);
 hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
                                hipStream_t s);
 int mtsg_develop_channels(int pixel_format);
@@ -70,6 +77,11 @@ struct mtsgpu_ctx {
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
+    // wavefront pipeline: path slots, ray queues and results, counters
+    DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_cnt, wf_cursor, wf_part;
+    uint32_t *wf_live_host = nullptr;   // pinned: live-slot counts read back while the pipeline runs
+    hipEvent_t wf_ev[8] = {};
+    unsigned long long last_counters[16] = {};
 };
 
 namespace {
@@ -243,6 +255,68 @@ int mtsgpu_film_border(int32_t rfilter, float rfilter_param) {
     return f.border;
 }
 
+// The wavefront pipeline for one chunk of samples: bounce after bounce,
+// wf_shade (consume results, shade, regenerate, append the next rays) then
+// wf_trace (both queues), until no path slot is live.  The live count of every
+// POLL-th bounce is read back asynchronously; the host stays at most LAG polls
+// ahead of the GPU, so the queue never drains and the overshoot (empty bounces)
+// stays small.
+static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, bool stats, hipStream_t stream,
+                           int shadeGrid, int traceGrid, uint32_t slots, const volatile int *cancel) {
+    hipError_t e;
+    MtsgWave W;
+    std::memset(&W, 0, sizeof W);
+    W.state = (float4 *)ctx->wf_state.p;
+    W.qray = (float4 *)ctx->wf_qray.p;
+    W.sray = (float4 *)ctx->wf_sray.p;
+    W.hit = (float4 *)ctx->wf_hit.p;
+    W.occl = (uint32_t *)ctx->wf_occl.p;
+    W.cnt = (uint32_t *)ctx->wf_cnt.p;
+    W.cursor = (unsigned long long *)ctx->wf_cursor.p;
+    W.slots = slots;
+    const uint32_t tiles = L.num_pixels / 64;
+    for (int b = 0; b <= 8; ++b) W.band_tiles[b] = (uint32_t)((uint64_t)tiles * b / 8);
+    unsigned long long *part = (unsigned long long *)ctx->wf_part.p;
+    const int partBlocks = std::max(shadeGrid, traceGrid);
+    if ((e = hipMemsetAsync((char *)ctx->wf_state.p + (size_t)7 * slots * 16, 0, (size_t)slots * 16, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->wf_cnt.p, 0, 8 * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->wf_cursor.p, 0, 8 * 8, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(part, 0, (size_t)partBlocks * 16 * 8, stream)) != hipSuccess)
+        return hip_fail(ctx, e, "wavefront reset");
+    constexpr int POLL = 4, LAG = 2, RING = 8;
+    int polls = 0, checked = 0;
+    const uint64_t maxBounces = (uint64_t)1 << 24;
+    for (uint64_t it = 0;; ++it) {
+        if (it >= maxBounces) return fail(ctx, MTSGPU_EHIP, "wavefront: no convergence");
+        W.parity = (uint32_t)(it & 1);
+        if ((e = mtsg_launch_wf_shade(L, W, part, shadeGrid, instr, stream)) != hipSuccess)
+            return hip_fail(ctx, e, "wf_shade launch");
+        if (it % POLL == 0) {
+            const int r = polls % RING;
+            if ((e = hipMemcpyAsync(ctx->wf_live_host + r, W.cnt + W.parity * 4 + 2, 4, hipMemcpyDeviceToHost,
+                                    stream)) != hipSuccess ||
+                (e = hipEventRecord(ctx->wf_ev[r], stream)) != hipSuccess)
+                return hip_fail(ctx, e, "wavefront poll");
+            ++polls;
+        }
+        if ((e = mtsg_launch_wf_trace(L, W, part, traceGrid, stats, stream)) != hipSuccess)
+            return hip_fail(ctx, e, "wf_trace launch");
+        bool finished = false;
+        while (!finished && polls > checked) {
+            const int r = checked % RING;
+            if (polls - checked <= LAG && hipEventQuery(ctx->wf_ev[r]) != hipSuccess) break;   // not yet, and not far ahead
+            if ((e = hipEventSynchronize(ctx->wf_ev[r])) != hipSuccess) return hip_fail(ctx, e, "wavefront");
+            ++checked;
+            finished = ctx->wf_live_host[r] == 0;
+        }
+        if (finished) break;
+        if (cancel && *cancel) break;
+    }
+    if ((e = mtsg_launch_wf_flush(part, (uint32_t)partBlocks, L.counters, stream)) != hipSuccess)
+        return hip_fail(ctx, e, "wf_flush launch");
+    return MTSGPU_OK;
+}
+
 static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *film_host, float *film_dev,
                        float *samples_host, hipStream_t stream, mtsgpu_stats *stats) {
     if (!ctx || !P) return MTSGPU_EINVAL;
@@ -395,15 +469,55 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
+    // execution engine (same per-sample results): the wavefront pipeline or the megakernel
+    bool wave = pathLike && !L.scene_lds;   // default: wavefront for scenes whose BVH lives in HBM
+    if (const char *env = std::getenv("MTSGPU_ENGINE")) wave = pathLike && std::strcmp(env, "wavefront") == 0;
+    if (P->flags & MTSGPU_FLAG_WAVEFRONT) wave = pathLike;
+    if (P->flags & MTSGPU_FLAG_MEGAKERNEL) wave = false;
+    int shadeGrid = 0, traceGrid = 0;
+    uint32_t slots = 0;
+    if (wave) {
+        int sb = 0, tb = 0;
+        mtsg_wf_occupancy(L, &sb, &tb);
+        if (sb <= 0 || tb <= 0) return fail(ctx, MTSGPU_EHIP, "wavefront kernels do not fit the device");
+        shadeGrid = std::max(8, ctx->num_cus * sb / 8 * 8);   // a multiple of 8: one pixel band per XCD
+        traceGrid = ctx->num_cus * tb;
+        const uint64_t lanes = (uint64_t)shadeGrid * BLOCK_THREADS;
+        uint64_t target = (uint64_t)1 << 20;
+        if (const char *env = std::getenv("MTSGPU_WF_SLOTS")) target = std::max<uint64_t>(1, std::strtoull(env, nullptr, 10));
+        const uint64_t items = (uint64_t)std::min(chunk, P->spp) * L.num_pixels;
+        target = std::min(target, items);
+        slots = (uint32_t)(std::max<uint64_t>(1, (target + lanes - 1) / lanes) * lanes);
+        if ((e = ctx->wf_state.ensure((size_t)MTSG_WF_STATE_VECS * slots * 16)) != hipSuccess ||
+            (e = ctx->wf_qray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
+            (e = ctx->wf_sray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
+            (e = ctx->wf_hit.ensure((size_t)slots * 16)) != hipSuccess ||
+            (e = ctx->wf_occl.ensure((size_t)slots * 4)) != hipSuccess || (e = ctx->wf_cnt.ensure(8 * 4)) != hipSuccess ||
+            (e = ctx->wf_cursor.ensure(8 * 8)) != hipSuccess ||
+            (e = ctx->wf_part.ensure((size_t)std::max(shadeGrid, traceGrid) * 16 * 8)) != hipSuccess)
+            return hip_fail(ctx, e, "wavefront buffers");
+        if (!ctx->wf_live_host) {
+            if ((e = hipHostMalloc((void **)&ctx->wf_live_host, 8 * sizeof(uint32_t))) != hipSuccess)
+                return hip_fail(ctx, e, "wavefront pinned buffer");
+            for (hipEvent_t &ev : ctx->wf_ev)
+                if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return hip_fail(ctx, e, "event");
+        }
+    }
     if ((e = hipEventRecord(ctx->ev0, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
     for (uint32_t j0 = 0; j0 < P->spp; j0 += chunk) {
         if (P->cancel && *P->cancel) break;
         L.j0 = j0;
         L.chunk_spp = std::min(chunk, P->spp - j0);
         L.num_items = (uint64_t)L.chunk_spp * L.num_pixels;
-        const uint64_t blocksNeeded = (L.num_items + 255) / 256;
-        const int grid = (int)std::min<uint64_t>((uint64_t)ctx->num_cus * bpc, std::max<uint64_t>(1, blocksNeeded));
-        if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
+        if (wave) {
+            const int rc = wf_render_chunk(ctx, L, nsamp != 0 || stats_mode, stats_mode, stream, shadeGrid, traceGrid,
+                                           slots, P->cancel);
+            if (rc != MTSGPU_OK) return rc;
+        } else {
+            const uint64_t blocksNeeded = (L.num_items + 255) / 256;
+            const int grid = (int)std::min<uint64_t>((uint64_t)ctx->num_cus * bpc, std::max<uint64_t>(1, blocksNeeded));
+            if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
+        }
         if ((e = mtsg_launch_reduce(L, stream)) != hipSuccess) return hip_fail(ctx, e, "reduce launch");
     }
     if ((e = hipEventRecord(ctx->ev1, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
@@ -415,6 +529,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (nsamp && (e = hipMemcpyAsync(samples_host, ctx->samples.p, nsamp * 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
         return hip_fail(ctx, e, "sample copy");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel");
+    std::memcpy(ctx->last_counters, hc, sizeof hc);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     if (stats) {
@@ -505,8 +620,12 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
-                      &ctx->dev_in, &ctx->dev_out};
+                      &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_qray, &ctx->wf_sray, &ctx->wf_hit,
+                      &ctx->wf_occl, &ctx->wf_cnt, &ctx->wf_cursor, &ctx->wf_part, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
+    for (hipEvent_t &e : ctx->wf_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->wf_live_host) (void)hipHostFree(ctx->wf_live_host);
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -554,6 +673,12 @@ int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *o
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 32, hipMemcpyDeviceToHost);
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
     return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "arith probe");
+}
+
+int mtsgpu_debug_counters(mtsgpu_ctx *ctx, uint64_t *out16) {
+    if (!ctx || !out16) return MTSGPU_EINVAL;
+    for (int k = 0; k < 16; ++k) out16[k] = ctx->last_counters[k];
+    return MTSGPU_OK;
 }
 
 // diagnostics: BVH statistics of the uploaded scene

@@ -12,6 +12,7 @@
 //   vertices  positions / shading normals (zero-filled where a shape has none)
 #pragma once
 #include <stdint.h>
+#include <hip/hip_vector_types.h>   // float4 of MtsgWave (host and device)
 
 #define MTSG_MAX_STACK 64     // BVH builder keeps depth < MTSG_MAX_STACK
 #define MTSG_LEAF_MAX 8       // primitives per leaf
@@ -191,6 +192,24 @@ struct MtsgLookup {
     uint32_t m;                 // log2 resolution (0: identity enumeration)
     uint32_t inv[32];
     uint32_t ycol[64];
+};
+
+// The wavefront pipeline (path_kernel.hip: wf_shade / wf_trace):
+// per-path state in SoA slots, the two ray queues of one bounce and their
+// results.  Queue positions are handed out per wave (one atomic per wave).
+#define MTSG_WF_STATE_VECS 8          // float4 state vectors per slot
+#define MTSG_WF_NONE 0xffffffffu      // no queue entry (ray skipped or outside the scene box)
+struct MtsgWave {
+    float4 *state;                    // [MTSG_WF_STATE_VECS][slots]
+    float4 *qray;                     // [2 * slots] closest-hit rays {o, mint}, {d, maxt}
+    float4 *sray;                     // [2 * slots] shadow rays
+    float4 *hit;                      // [slots] {t, u, v, slot bits (MTSG_WF_NONE: miss)}
+    uint32_t *occl;                   // [slots] shadow results
+    uint32_t *cnt;                    // [2][4] per parity: closest count, shadow count, live slots, -
+    unsigned long long *cursor;       // [8] item cursors of the 8 pixel bands (one per XCD)
+    uint32_t slots;                   // multiple of the shade grid's lanes
+    uint32_t parity;                  // bounce index & 1
+    uint32_t band_tiles[9];           // tile ranges of the 8 pixel bands
 };
 
 struct MtsgLaunch {

@@ -751,25 +751,53 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
     return index | ((uint64_t)jhi << m);
 }
 
-// One loop iteration = one bounce of Li() for every lane: trace the lane's
-// pending shadow ray (NEE of the previous vertex) and its closest-hit ray
-// (camera or BSDF-sampled), then shade the new vertex: add the NEE estimate if
-// unoccluded, the MIS-weighted emission of the hit, Russian roulette, then at
-// the new vertex draw the NEE sample and the BSDF sample, which produce the
-// next iteration's two rays.  Sampler dimensions are consumed in the
-// reference's order (NEE 2D, BSDF 2D [+1D], RR 1D), and radiance is
+// ---------------------------------------------------------------------------
+// Li() as a per-path state machine, one bounce per step.  One step traces the
+// path's pending shadow ray (NEE of the previous vertex) and its closest-hit
+// ray (camera or BSDF-sampled), then shades the new vertex: add the NEE
+// estimate if unoccluded, the MIS-weighted emission of the hit, Russian
+// roulette, then at the new vertex draw the NEE sample and the BSDF sample,
+// which produce the next step's two rays.  Sampler dimensions are consumed in
+// the reference's order (NEE 2D, BSDF 2D [+1D], RR 1D), and radiance is
 // accumulated in the reference's order (NEE term before the BSDF-hit term).
-// INSTR: traversal statistics + optional per-sample records (tests, roofline
-// pass); SCENE_LDS: BVH + TriAccel staged in LDS; FEAT: MTSG_FEAT_ENV (scene
-// has an envmap) | MTSG_FEAT_EXT (roughplastic or textured BSDFs)
-template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
-__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
-    constexpr bool STATS = INSTR;
-    constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
-                   ANA = (FEAT & MTSG_FEAT_ANA) != 0;
-    extern __shared__ uint32_t lds[];
+// PathShader holds the three pieces both execution models share: start (the
+// renderBlock loop body up to Li's prologue), shade (the rest of one bounce)
+// and finish (block->put).  The persistent megakernel (path_kernel) runs them
+// with both traversals inline; the wavefront pipeline (wf_shade / wf_trace)
+// runs the traversals as separate kernels over compacted ray queues.
+// ---------------------------------------------------------------------------
+struct PathState {
+    bool active;
+    int px, py;
+    uint32_t j, pix;
+    float sx, sy;
+    SamplerState smp;
+    PathVars P;
+    // rays of the next trace step: closest (camera / extension) and shadow (NEE)
+    bool haveRay, primary, haveShadow;
+    f3 ro, rd, sd;
+    float rmint, rmaxt, smaxt;
+};
+
+struct PathCounters {
+    unsigned long long rays, shadow, len, samples, nodes, tests, err, hits, nee, sobol;
+};
+
+// LDS of path_kernel / wf_shade: [Sobol nibble tables][look_up column tables]
+// [BVH + TriAccel + hit data (SCENE_LDS)][traversal stacks]
+template <bool SCENE_LDS>
+struct LdsView {
+    lds_u32 *ycolTab;
+    lds_node *nodes;
+    lds_tri *tris;
+    HitSrc<SCENE_LDS> hs;
+    SobolCtx SC;
+    uint32_t stackBase;   // word offset of the traversal stacks
+};
+
+template <bool SCENE_LDS>
+__device__ __forceinline__ LdsView<SCENE_LDS> stage_lds(const MtsgLaunch &L, uint32_t *lds) {
     const MtsgDeviceScene &S = L.scene;
-    // LDS: [Sobol nibble tables][look_up column tables][BVH + TriAccel (small scenes)][stacks]
     const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
     for (uint32_t i = threadIdx.x; i < tabWords; i += BLOCK) {
         const uint32_t d = i / (L.nibbles * 16), r = i % (L.nibbles * 16);
@@ -804,441 +832,833 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
         }
     }
     __syncthreads();
-    lds_u32 *ycolTab = (lds_u32 *)(lds + tabWords);
+    LdsView<SCENE_LDS> v;
+    v.ycolTab = (lds_u32 *)(lds + tabWords);
     // base2 and the node array size are multiples of 4 words: 16-byte aligned (ds_read_b128)
-    lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
-    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
+    v.nodes = (lds_node *)__builtin_assume_aligned((const void *)(lds + base2), 16);
+    v.tris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + base2 + L.num_nodes * 16), 16);
     // triangle data of hit records and emitter samples (HitSrc)
-    HitSrc<SCENE_LDS> hs;
     if constexpr (SCENE_LDS) {
         const uint32_t np = S.num_prims, nv = L.num_verts;
         lds_u32 *b = (lds_u32 *)(lds + base2 + L.num_nodes * 16 + np * 12);
-        hs.pv = b;
-        hs.dpdu = (lds_f32 *)(b + 4 * np);
-        hs.pos = (lds_f32 *)(b + 7 * np);
-        hs.nrm = (lds_f32 *)(b + 7 * np + 3 * nv);
-        hs.shapes = (lds_shape *)(b + 7 * np + 6 * nv);
+        v.hs.pv = b;
+        v.hs.dpdu = (lds_f32 *)(b + 4 * np);
+        v.hs.pos = (lds_f32 *)(b + 7 * np);
+        v.hs.nrm = (lds_f32 *)(b + 7 * np + 3 * nv);
+        v.hs.shapes = (lds_shape *)(b + 7 * np + 6 * nv);
     } else {
-        hs.pv = (glb_u32 *)S.prim_vtx;
-        hs.dpdu = (glb_f32 *)S.dpdu;
-        hs.pos = (glb_f32 *)S.positions;
-        hs.nrm = (glb_f32 *)S.normals;
-        hs.shapes = (glb_shape *)S.shapes;
+        v.hs.pv = (glb_u32 *)S.prim_vtx;
+        v.hs.dpdu = (glb_f32 *)S.dpdu;
+        v.hs.pos = (glb_f32 *)S.positions;
+        v.hs.nrm = (glb_f32 *)S.normals;
+        v.hs.shapes = (glb_shape *)S.shapes;
     }
-    SobolCtx SC;
-    SC.lds = (lds_u32 *)lds;
-    SC.glob = (glb_u32 *)L.sobol_nib;
-    SC.lds_dims = L.lds_dims;
-    SC.nibbles = L.nibbles;
-    SC.scramble = L.scramble;
-    SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
-    lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
-    lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
+    v.SC.lds = (lds_u32 *)lds;
+    v.SC.glob = (glb_u32 *)L.sobol_nib;
+    v.SC.lds_dims = L.lds_dims;
+    v.SC.nibbles = L.nibbles;
+    v.SC.scramble = L.scramble;
+    v.SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
+    v.stackBase = base2 + sceneWords;
+    return v;
+}
 
-    unsigned long long cRays = 0, cShadow = 0, cLen = 0, cSamples = 0, cNodes = 0, cTests = 0, cErr = 0;
-    unsigned long long cHits = 0, cNee = 0, cSobol = 0;
+// INSTR: traversal statistics + optional per-sample records (tests, roofline
+// pass); SCENE_LDS: BVH + TriAccel staged in LDS; FEAT: MTSG_FEAT_ENV (scene
+// has an environment emitter) | MTSG_FEAT_EXT (roughplastic, textures, smooth
+// BSDFs, twosided) | MTSG_FEAT_ANA (analytic shapes)
+template <bool INSTR, bool SCENE_LDS, int FEAT>
+struct PathShader {
+    static constexpr bool STATS = INSTR;
+    static constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
+                          ANA = (FEAT & MTSG_FEAT_ANA) != 0;
+    const MtsgLaunch &L;
+    const HitSrc<SCENE_LDS> &hs;
+    const SobolCtx &SC;
+    lds_u32 *ycolTab;
+    PathCounters &c;
+
+    // the renderBlock loop body for item `it` up to Li()'s prologue
+    // (integrator.cpp:165-186, path.cpp:119-133); false for a padding pixel
+    __device__ __forceinline__ bool start(PathState &st, uint64_t it) const {
+        const MtsgDeviceScene &S = L.scene;
+        SamplerState &smp = st.smp;
+        PathVars &P = st.P;
+        const uint32_t jj = (uint32_t)(it / L.num_pixels);
+        st.pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
+        if (!pixel_of(L, st.pix, st.px, st.py)) return false;
+        const int px = st.px, py = st.py;
+        uint32_t &j = st.j;
+        float &sx = st.sx, &sy = st.sy;
+        bool &haveRay = st.haveRay, &primary = st.primary, &haveShadow = st.haveShadow;
+        f3 &ro = st.ro, &rd = st.rd;
+        float &rmint = st.rmint, &rmaxt = st.rmaxt;
+        j = L.j0 + jj;
+        smp.dim = 0;
+        smp.sampleIndex = j;
+        smp.err = false;
+        if (SC.indep)
+            smp.sobolIndex = indep_key((uint32_t)px, (uint32_t)py, j);
+        else if (L.lut.m > 1)
+            smp.sobolIndex = sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py, L.scramble64);
+        else
+            smp.sobolIndex = j;
+        float u, v;
+        next2d(SC, L.resolution, smp, px, py, u, v);
+        sx = (float)px + u;
+        sy = (float)py + v;
+        // PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298)
+        const MtsgCamera &cam = S.cam;
+        const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+        const f3 dl = normalize(nearP);
+        const float invZ = 1.0f / dl.z;
+        rmint = cam.near_clip * invZ;
+        rmaxt = cam.far_clip * invZ;
+        const float *W = cam.to_world;
+        ro = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
+                W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);
+        rd = mk(W[0] * dl.x + W[1] * dl.y + W[2] * dl.z, W[4] * dl.x + W[5] * dl.y + W[6] * dl.z,
+                W[8] * dl.x + W[9] * dl.y + W[10] * dl.z);
+        // Li() prologue (path.cpp:119-133)
+        P.L = mk(0, 0, 0);
+        P.thr = mk(1.0f, 1.0f, 1.0f);
+        P.eta = 1.0f;
+        P.depth = 1;
+        P.scattered = false;
+        P.emitted = true;
+        haveRay = true;
+        primary = true;
+        haveShadow = false;
+        st.active = true;
+        return true;
+    }
+
+    // the rest of one bounce, given the step's trace results: returns true
+    // when the path ends (path.cpp:135-292)
+    __device__ __forceinline__ bool shade(PathState &st, bool occluded, bool hit, uint32_t slot, uint32_t prim,
+                                          float hu, float hv, float ht) const {
+        const MtsgDeviceScene &S = L.scene;
+        PathVars &P = st.P;
+        SamplerState &smp = st.smp;
+        const int px = st.px, py = st.py;
+        const float sx = st.sx, sy = st.sy;
+        bool &haveRay = st.haveRay, &primary = st.primary, &haveShadow = st.haveShadow;
+        f3 &ro = st.ro, &rd = st.rd, &sd = st.sd;
+        float &rmint = st.rmint, &rmaxt = st.rmaxt, &smaxt = st.smaxt;
+        bool endPath = false;
+        // NEE of the previous vertex (scene.cpp:838-842, path.cpp:176-199)
+        if (haveShadow && !occluded) P.L = add(P.L, P.neeC);
+        haveShadow = false;
+        bool vertex = false;
+        if (!haveRay) {
+            endPath = true;   // the BSDF sample at the previous vertex failed
+        } else {
+            // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
+            // a miss overwrites the whole record: no field of the previous vertex stays
+            // live across the next traversal except through an explicit use
+            if (hit) {
+                fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, ro, rd, P.its);
+            } else {
+                P.its = Hit{};
+            }
+            if (STATS && hit) c.hits++;
+            if (primary) {
+                P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
+                vertex = true;
+            } else if (!P.its.valid) {
+                // missed: the environment emitter, if any (path.cpp:233-247)
+                if (ENV && !(L.hide_emitters && !P.scattered)) {
+                    glb_env *E = (glb_env *)S.env;
+                    const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : env_eval(E, rd);
+                    float nT, fT;
+                    // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
+                    if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
+                        float lumPdf = 0;
+                        if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
+                            lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : env_pdf_direction(E, rd)) *
+                                     (S.emitters[S.env_emitter].weight * S.em_norm);
+                        const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                        P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
+                    }
+                }
+                // volpath.cpp:326-336: the miss still passes the RR step before the loop ends
+                if (L.integrator == MTSG_INTEGRATOR_VOLPATH && P.depth++ >= L.rr_depth) (void)next1d(SC, smp);
+                endPath = true;   // !its.isValid(): break after the environment term
+            } else {
+                auto &sh = hs.shapes[P.its.shape];
+                if (sh.emitter >= 0) {
+                    const f3 value = area_Le(S, P.its, neg(rd));
+                    float lumPdf = 0;
+                    if (!(P.sampledType & MTSG_F_DELTA)) {
+                        // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
+                        // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
+                        const MtsgEmitter &e = S.emitters[sh.emitter];
+                        const f3 dn = P.its.sh.n;
+                        float pdf = 0.0f;
+                        if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0) {
+                            if (ANA && S.shapes[P.its.shape].analytic >= 0)   // dRec.ref = the previous vertex
+                                pdf = ana_pdf_direct(((GAna *)S.analytic)[S.shapes[P.its.shape].analytic], ro, rd,
+                                                     dn, P.its.t);
+                            else
+                                pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
+                        }
+                        lumPdf = pdf * (e.weight * S.em_norm);
+                    }
+                    const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
+                    P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
+                }
+                P.emitted = false;
+                if (P.depth++ >= L.rr_depth) {
+                    const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
+                    if (next1d(SC, smp) >= q) endPath = true;
+                    else P.thr = divs(P.thr, q);
+                }
+                if (smp.err) endPath = true;
+                vertex = !endPath;
+            }
+        }
+        haveRay = false;
+        primary = false;
+
+        if (vertex) {
+            // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
+            if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
+                endPath = true;
+            } else if (!P.its.valid) {
+                // camera ray missed: scene->evalEnvironment(ray) with the sensor's ray
+                // differentials (path.cpp:136-142, perspective.cpp:271-298, integrator.cpp:181)
+                if (ENV && P.emitted && (!L.hide_emitters || P.scattered)) {
+                    const MtsgCamera &cam = S.cam;
+                    const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
+                    const f3 rxl = normalize(add(nearP, ld3(cam.dx))), ryl = normalize(add(nearP, ld3(cam.dy)));
+                    const float *W = cam.to_world;
+                    f3 rxd = mk(W[0] * rxl.x + W[1] * rxl.y + W[2] * rxl.z, W[4] * rxl.x + W[5] * rxl.y + W[6] * rxl.z,
+                                W[8] * rxl.x + W[9] * rxl.y + W[10] * rxl.z);
+                    f3 ryd = mk(W[0] * ryl.x + W[1] * ryl.y + W[2] * ryl.z, W[4] * ryl.x + W[5] * ryl.y + W[6] * ryl.z,
+                                W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
+                    rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
+                    ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
+                    glb_env *E = (glb_env *)S.env;
+                    if (E->constant) {   // ConstantBackgroundEmitter::evalEnvironment (constant.cpp:241-243)
+                        P.L = add(P.L, mulv(P.thr, mk(E->radiance[0], E->radiance[1], E->radiance[2])));
+                    } else {
+#ifdef MTSG_ABL_BILINEAR_PRIMARY   // timing ablation only
+                    P.L = add(P.L, mulv(P.thr, env_eval(E, rd)));
+#else
+                    P.L = add(P.L, mulv(P.thr, env_eval_diff(E, rd, rxd, ryd)));
+#endif
+                    }
+                }
+                endPath = true;
+            } else {
+                auto &sh = hs.shapes[P.its.shape];
+                GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
+                if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
+                    P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
+                // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
+                const float snp = dot(rd, P.its.geoN) * P.its.wi.z;
+                if ((P.depth >= L.max_depth && L.max_depth > 0) ||
+                    (L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
+                    endPath = true;
+                } else {
+                    P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
+                    if (bsdf.flags & MTSG_F_SMOOTH) {
+                        // Scene::sampleEmitterDirect (scene.cpp:828-852)
+                        float ex, ey;
+                        next2d(SC, L.resolution, smp, px, py, ex, ey);
+                        float emPdf;
+                        const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
+                        if (STATS) c.nee++;
+                        const MtsgEmitter &e = S.emitters[ei];
+                        f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
+                        float pdf = 0.0f, dist = 0.0f;
+                        f3 vlp = mk(0, 0, 0);   // dRec.p where it does not define dRec.d exactly (volpath)
+                        bool vrecomp = false;
+                        if (ENV && e.type != MTSG_EMITTER_AREA) {
+#ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
+                            glb_env *E = (glb_env *)S.env;
+                            const EnvSample es = E->constant ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
+                                                             : env_sample_direct(E, P.its.p, ex, ey);
+                            value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
+                            vlp = add(P.its.p, mul(dd, dist));   // dRec.p = ray(farT) (envmap.cpp:536, constant.cpp:254)
+                            vrecomp = true;
+#endif
+                        } else if (ANA && S.shapes[e.shape].analytic >= 0) {
+                            const AnaSample as =
+                                ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], P.its.p, ex, ey);
+                            dd = as.d; dist = as.dist; pdf = as.pdf;
+                            vlp = as.p; vrecomp = true;
+                            // AreaLight::sampleDirect (area.cpp:158-173)
+                            if (dot(dd, P.refN) >= 0 && dot(dd, as.n) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+                            else pdf = 0.0f;
+                        } else {
+                        // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
+                        float py2 = ey;
+                        const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
+                        const uint32_t prim = e.tri_first + lt;
+                        const uint4 pv = make_uint4(hs.pv[4 * prim], hs.pv[4 * prim + 1], hs.pv[4 * prim + 2],
+                                                    hs.pv[4 * prim + 3]);
+                        const float a = safe_sqrt(1.0f - ex);
+                        const float bx = 1 - a, by = a * py2;
+                        const f3 p0 = ldp3(hs.pos + 3 * (size_t)pv.x), p1 = ldp3(hs.pos + 3 * (size_t)pv.y),
+                                 p2 = ldp3(hs.pos + 3 * (size_t)pv.z);
+                        const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
+                        const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
+                        f3 ln;
+                        if (hs.shapes[e.shape].has_normals) {
+                            const f3 n0 = ldp3(hs.nrm + 3 * (size_t)pv.x), n1 = ldp3(hs.nrm + 3 * (size_t)pv.y),
+                                     n2 = ldp3(hs.nrm + 3 * (size_t)pv.z);
+                            ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
+                        } else {
+                            ln = normalize(cross(sideA, sideB));
+                        }
+                        pdf = e.inv_area;
+                        // Shape::sampleDirect (shape.cpp:102-115)
+                        dd = sub(lp, P.its.p);
+                        const float distSquared = len2(dd);
+                        dist = dsqrt(distSquared);
+                        dd = divs(dd, dist);
+                        const float dp = absdot(dd, ln);
+                        pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
+                        // AreaLight::sampleDirect (area.cpp:158-173)
+                        if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
+                        else pdf = 0.0f;
+                        }
+                        if (pdf != 0) {
+                            // the NEE estimate but for visibility (path.cpp:176-199)
+                            const float dpdf = pdf * emPdf;
+                            value = divs(value, emPdf);
+                            f3 c = mk(0, 0, 0);
+                            if (!is_zero(value)) {
+                                const f3 wo = to_local(P.its.sh, dd);
+                                // twosided (twosided.cpp:105-131): the nested BSDF of the side wi is on
+                                f3 qwi = P.its.wi, qwo = wo;
+                                GBsdf *qb = &bsdf;
+                                if constexpr (EXT) {
+                                    if (bsdf.type == BSDF_TWOSIDED) {
+                                        const bool flip = !(qwi.z > 0);
+                                        qb = &((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
+                                        if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
+                                    }
+                                }
+                                const f3 bsdfVal = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
+                                    const float bsdfPdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                    const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
+                                    const float weight = pa / (pa + pb);
+                                    c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
+                                }
+                            }
+                            // Ray(dRec.ref, dRec.d, Epsilon, dRec.dist*(1-ShadowEpsilon)) (scene.cpp:839-840)
+                            P.neeC = c;
+                            sd = dd;
+                            smaxt = dist * (1 - D_SHADOW_EPSILON);
+                            if (L.integrator == MTSG_INTEGRATOR_VOLPATH && vrecomp) {
+                                // Scene::evalTransmittance (scene.cpp:619-679, 890): the segment to dRec.p,
+                                // re-normalised; every supported emitter is EOnSurface (envmap.cpp:107,
+                                // constant.cpp:48, area lights), so the shadow epsilon always applies
+                                const f3 v = sub(vlp, P.its.p);
+                                const float rem = dsqrt(len2(v));
+                                sd = divs(v, rem);
+                                smaxt = rem * (1 - D_SHADOW_EPSILON);
+                            }
+                            haveShadow = true;
+                        }
+                    }
+                    // BSDF sampling (path.cpp:206-226)
+                    float bx2, by2;
+                    next2d(SC, L.resolution, smp, px, py, bx2, by2);
+                    float u1d = 0.0f;
+                    if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
+                    BSample bs;
+                    if (EXT && bsdf.type == BSDF_TWOSIDED) {
+                        // TwoSidedBRDF::sample(bRec, pdf, sample) (twosided.cpp:151-172)
+                        const bool flip = P.its.wi.z < 0;
+                        f3 qwi = P.its.wi;
+                        if (flip) qwi.z = -qwi.z;
+                        bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
+                                              bx2, by2, u1d, P.its.u, P.its.v);
+                        if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
+                    } else {
+                        bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                    }
+                    if (!is_zero(bs.weight) && !smp.err) {
+                        P.scattered |= bs.sampledType != MTSG_F_NULL;
+                        const f3 wo = to_world(P.its.sh, bs.wo);
+                        if (!L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
+                            // throughput *= bsdfWeight; eta *= bRec.eta (path.cpp:256-257): the same
+                            // products as after the hit, formed now so they need not stay live
+                            P.thr = mulv(P.thr, bs.weight);
+                            P.bsdfPdf = bs.pdf;
+                            P.eta *= bs.eta;
+                            P.sampledType = bs.sampledType;
+                            ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
+                            rd = wo;
+                            rmint = D_EPSILON;
+                            rmaxt = INFINITY;
+                            haveRay = true;
+                        }
+                    }
+                    // no next ray: the path ends once the pending shadow ray is resolved
+                    if (!haveRay && !haveShadow) endPath = true;
+                }
+            }
+        }
+        return endPath;
+    }
+
+    // block->put(samplePos, spec, alpha) (integrator.cpp:184) and the sample's records
+    __device__ __forceinline__ void finish(PathState &st) const {
+        PathVars &P = st.P;
+        SamplerState &smp = st.smp;
+        const int px = st.px, py = st.py;
+        const uint32_t j = st.j, pix = st.pix;
+        const float sx = st.sx, sy = st.sy;
+        bool &haveRay = st.haveRay, &haveShadow = st.haveShadow;
+        // block->put(samplePos, spec, alpha) (integrator.cpp:184): the own-pixel
+        // splat is stored as {L.rgb, w} (alpha in {0,1} in the sign bit of w) and
+        // film_reduce re-forms weight * value[k] -- the same products
+        const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
+        float ownW = 0.0f;
+        const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
+        float4 rec4;
+        if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha == 0.0f ? -ownW : ownW);
+        else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
+        if (INSTR && L.samples) {
+            const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
+            float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
+            rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
+            rec[4] = sx; rec[5] = sy; rec[6] = (float)P.depth; rec[7] = smp.err ? 1.0f : 0.0f;
+        }
+        c.len += (unsigned long long)P.depth;
+        c.samples++;
+        if (STATS) c.sobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
+        if (smp.err) c.err++;
+        st.active = false;
+        haveRay = haveShadow = false;
+    }
+};
+
+template <bool STATS>
+__device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const PathCounters &c) {
+    atomicAdd(L.counters + 0, c.samples);
+    atomicAdd(L.counters + 1, c.rays);
+    atomicAdd(L.counters + 2, c.shadow);
+    atomicAdd(L.counters + 3, c.len);
+    if (STATS) {
+        atomicAdd(L.counters + 4, c.nodes);
+        atomicAdd(L.counters + 5, c.tests);
+        atomicAdd(L.counters + 7, c.hits);
+        atomicAdd(L.counters + 9, c.nee);
+        atomicAdd(L.counters + 10, c.sobol);
+    }
+    if (c.err) atomicAdd(L.counters + 6, c.err);
+}
+
+// The persistent megakernel: grid = CUs x resident blocks; every lane runs
+// PathShader steps with both traversals inline
+template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
+    constexpr bool STATS = INSTR;
+    constexpr bool ANA = (FEAT & MTSG_FEAT_ANA) != 0;
+    extern __shared__ uint32_t lds[];
+    const MtsgDeviceScene &S = L.scene;
+    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
+    lds_node *ldsNodes = V.nodes;
+    lds_tri *ldsTris = V.tris;
+    lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
+    PathCounters c = {};
+    const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
     uint64_t item = (uint64_t)xcd_block() * BLOCK + threadIdx.x;
-    bool active = false, done = false;
-    int px = 0, py = 0;
-    uint32_t j = 0, pix = 0;
-    SamplerState smp;
-    smp.sobolIndex = 0; smp.sampleIndex = 0; smp.dim = 0; smp.err = false;
-    PathVars P;
-    float sx = 0, sy = 0;
-    // rays of this iteration: closest (camera / extension) and shadow (NEE)
-    bool haveRay = false, primary = false, haveShadow = false;
-    f3 ro = mk(0, 0, 0), rd = mk(0, 0, 1), sd = mk(0, 0, 1);
-    float rmint = 0, rmaxt = 0, smaxt = 0;
+    bool done = false;
+    PathState st;
+    st.active = false;
+    st.px = st.py = 0;
+    st.j = st.pix = 0;
+    st.smp.sobolIndex = 0; st.smp.sampleIndex = 0; st.smp.dim = 0; st.smp.err = false;
+    st.sx = st.sy = 0;
+    st.haveRay = st.primary = st.haveShadow = false;
+    st.ro = mk(0, 0, 0); st.rd = mk(0, 0, 1); st.sd = mk(0, 0, 1);
+    st.rmint = st.rmaxt = st.smaxt = 0;
 
     while (true) {
-        // ---- A: start the next sample (renderBlock loop body, integrator.cpp:165-186)
-        while (!active && !done) {
+        // ---- A: start the next sample
+        while (!st.active && !done) {
             if (item >= L.num_items) { done = true; break; }
             const uint64_t it = item;
             item += lanes;
-            const uint32_t jj = (uint32_t)(it / L.num_pixels);
-            pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
-            if (!pixel_of(L, pix, px, py)) continue;
-            j = L.j0 + jj;
-            // sampler->generate(offset) + setSampleIndex(j) (sobol.cpp:187-217)
-            smp.dim = 0;
-            smp.sampleIndex = j;
-            smp.err = false;
-            if (SC.indep)
-                smp.sobolIndex = indep_key((uint32_t)px, (uint32_t)py, j);
-            else if (L.lut.m > 1)
-                smp.sobolIndex = sobol_lookup_lds(L.lut, ycolTab, L.nibbles, j, (uint32_t)px, (uint32_t)py, L.scramble64);
-            else
-                smp.sobolIndex = j;
-            float u, v;
-            next2d(SC, L.resolution, smp, px, py, u, v);
-            sx = (float)px + u;
-            sy = (float)py + v;
-            // PerspectiveCameraImpl::sampleRayDifferential (perspective.cpp:271-298)
-            const MtsgCamera &cam = S.cam;
-            const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
-            const f3 dl = normalize(nearP);
-            const float invZ = 1.0f / dl.z;
-            rmint = cam.near_clip * invZ;
-            rmaxt = cam.far_clip * invZ;
-            const float *W = cam.to_world;
-            ro = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
-                    W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);
-            rd = mk(W[0] * dl.x + W[1] * dl.y + W[2] * dl.z, W[4] * dl.x + W[5] * dl.y + W[6] * dl.z,
-                    W[8] * dl.x + W[9] * dl.y + W[10] * dl.z);
-            // Li() prologue (path.cpp:119-133)
-            P.L = mk(0, 0, 0);
-            P.thr = mk(1.0f, 1.0f, 1.0f);
-            P.eta = 1.0f;
-            P.depth = 1;
-            P.scattered = false;
-            P.emitted = true;
-            haveRay = true;
-            primary = true;
-            haveShadow = false;
-            active = true;
+            sh.start(st, it);
         }
         if (__all(done)) break;
 
         // ---- B: trace the shadow ray, then the closest-hit ray ---------------
         bool occluded = false;
-        if (active && haveShadow) {
-            cShadow++;
+        if (st.active && st.haveShadow) {
+            c.shadow++;
             float mint, maxt;
             // a shadow ray whose estimate is zero cannot change Li: skip its traversal
 #ifdef MTSG_ABL_NO_SHADOW
             if (false) {
 #else
-            if (!is_zero(P.neeC) && ray_interval(S, P.its.p, sd, D_EPSILON, smaxt, true, mint, maxt)) {
+            if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
 #endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS && L.scan)
-                    occluded = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, P.its.p, sd, mint, maxt, sl, a0, a1, a2, cTests);
+                    occluded = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, st.P.its.p, st.sd, mint, maxt,
+                                                      sl, a0, a1, a2, c.tests);
                 else if (SCENE_LDS)
-                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
+                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
+                                                          sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
                 else
-                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, P.its.p, sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, cNodes, cTests, S.analytic);
+                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
+                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
+                                                          S.analytic);
             }
         }
         bool hit = false;
-        uint32_t slot = 0;
+        uint32_t slot = 0, prim = 0;
         float hu = 0, hv = 0, ht = 0;
-        if (active && haveRay) {
-            cRays++;
+        if (st.active && st.haveRay) {
+            c.rays++;
             float mint, maxt;
-            if (ray_interval(S, ro, rd, rmint, rmaxt, false, mint, maxt)) {
+            if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS && L.scan)
-                    hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, ro, rd, mint, maxt, slot, hu, hv, ht, cTests);
+                    hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, st.ro, st.rd, mint, maxt, slot, hu,
+                                                  hv, ht, c.tests);
                 else if (SCENE_LDS)
-                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
+                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
+                                                      hu, hv, ht, c.nodes, c.tests, S.analytic);
                 else
-                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, ro, rd, mint, maxt, stkN, stkD, slot, hu, hv, ht, cNodes, cTests, S.analytic);
+                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
+                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
+                                                      S.analytic);
             }
+            if (hit) prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
         }
 
         // ---- C: shade -------------------------------------------------------
-        bool endPath = false;
-        if (active) {
-            // NEE of the previous vertex (scene.cpp:838-842, path.cpp:176-199)
-            if (haveShadow && !occluded) P.L = add(P.L, P.neeC);
-            haveShadow = false;
-            bool vertex = false;
-            if (!haveRay) {
-                endPath = true;   // the BSDF sample at the previous vertex failed
-            } else {
-                // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
-                // a miss overwrites the whole record: no field of the previous vertex stays
-                // live across the next traversal except through an explicit use
-                if (hit) {
-                    const uint32_t prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
-                    fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, ro, rd, P.its);
-                } else {
-                    P.its = Hit{};
-                }
-                if (STATS && hit) cHits++;
-                if (primary) {
-                    P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
-                    vertex = true;
-                } else if (!P.its.valid) {
-                    // missed: the environment emitter, if any (path.cpp:233-247)
-                    if (ENV && !(L.hide_emitters && !P.scattered)) {
-                        glb_env *E = (glb_env *)S.env;
-                        const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : env_eval(E, rd);
-                        float nT, fT;
-                        // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
-                        if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
-                            float lumPdf = 0;
-                            if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
-                                lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : env_pdf_direction(E, rd)) *
-                                         (S.emitters[S.env_emitter].weight * S.em_norm);
-                            const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
-                            P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
-                        }
-                    }
-                    // volpath.cpp:326-336: the miss still passes the RR step before the loop ends
-                    if (L.integrator == MTSG_INTEGRATOR_VOLPATH && P.depth++ >= L.rr_depth) (void)next1d(SC, smp);
-                    endPath = true;   // !its.isValid(): break after the environment term
-                } else {
-                    auto &sh = hs.shapes[P.its.shape];
-                    if (sh.emitter >= 0) {
-                        const f3 value = area_Le(S, P.its, neg(rd));
-                        float lumPdf = 0;
-                        if (!(P.sampledType & MTSG_F_DELTA)) {
-                            // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
-                            // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
-                            const MtsgEmitter &e = S.emitters[sh.emitter];
-                            const f3 dn = P.its.sh.n;
-                            float pdf = 0.0f;
-                            if (dot(rd, P.refN) >= 0 && dot(rd, dn) < 0) {
-                                if (ANA && S.shapes[P.its.shape].analytic >= 0)   // dRec.ref = the previous vertex
-                                    pdf = ana_pdf_direct(((GAna *)S.analytic)[S.shapes[P.its.shape].analytic], ro, rd,
-                                                         dn, P.its.t);
-                                else
-                                    pdf = e.inv_area * (P.its.t * P.its.t) / absdot(rd, dn);
-                            }
-                            lumPdf = pdf * (e.weight * S.em_norm);
-                        }
-                        const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
-                        P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
-                    }
-                    P.emitted = false;
-                    if (P.depth++ >= L.rr_depth) {
-                        const float q = smin(smaxc(P.thr) * P.eta * P.eta, (float)0.95f);
-                        if (next1d(SC, smp) >= q) endPath = true;
-                        else P.thr = divs(P.thr, q);
-                    }
-                    if (smp.err) endPath = true;
-                    vertex = !endPath;
-                }
-            }
-            haveRay = false;
-            primary = false;
+        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
+    }
+    path_counters_flush<STATS>(L, c);
+}
 
-            if (vertex) {
-                // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
-                if (!(P.depth <= L.max_depth || L.max_depth < 0)) {
-                    endPath = true;
-                } else if (!P.its.valid) {
-                    // camera ray missed: scene->evalEnvironment(ray) with the sensor's ray
-                    // differentials (path.cpp:136-142, perspective.cpp:271-298, integrator.cpp:181)
-                    if (ENV && P.emitted && (!L.hide_emitters || P.scattered)) {
-                        const MtsgCamera &cam = S.cam;
-                        const f3 nearP = xf_point(cam.sample_to_camera, mk(sx * cam.inv_res_x, sy * cam.inv_res_y, 0.0f));
-                        const f3 rxl = normalize(add(nearP, ld3(cam.dx))), ryl = normalize(add(nearP, ld3(cam.dy)));
-                        const float *W = cam.to_world;
-                        f3 rxd = mk(W[0] * rxl.x + W[1] * rxl.y + W[2] * rxl.z, W[4] * rxl.x + W[5] * rxl.y + W[6] * rxl.z,
-                                    W[8] * rxl.x + W[9] * rxl.y + W[10] * rxl.z);
-                        f3 ryd = mk(W[0] * ryl.x + W[1] * ryl.y + W[2] * ryl.z, W[4] * ryl.x + W[5] * ryl.y + W[6] * ryl.z,
-                                    W[8] * ryl.x + W[9] * ryl.y + W[10] * ryl.z);
-                        rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
-                        ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
-                        glb_env *E = (glb_env *)S.env;
-                        if (E->constant) {   // ConstantBackgroundEmitter::evalEnvironment (constant.cpp:241-243)
-                            P.L = add(P.L, mulv(P.thr, mk(E->radiance[0], E->radiance[1], E->radiance[2])));
-                        } else {
-#ifdef MTSG_ABL_BILINEAR_PRIMARY   // timing ablation only
-                        P.L = add(P.L, mulv(P.thr, env_eval(E, rd)));
+// ===========================================================================
+// The wavefront pipeline (north star: per-bounce SoA ray queues in HBM,
+// ballot-compacted).  One bounce = wf_shade (every path slot: consume the
+// previous trace results, run PathShader::shade / finish, regenerate ended
+// paths from the pixel bands, append the next closest-hit and shadow rays to
+// the queues with one atomic per wave) + wf_trace (both queues, dense, at the
+// traversal's own occupancy).  Same PathShader code, same per-sample results
+// as the megakernel; the traversals no longer run with the shading's register
+// budget, and a shadow traversal no longer idles the lanes without one.
+// ===========================================================================
+#ifndef MTSG_WF_SHADE_WAVES
+#define MTSG_WF_SHADE_WAVES 3
+#endif
+#ifndef MTSG_WF_TRACE_WAVES
+#define MTSG_WF_TRACE_WAVES 8
+#endif
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// diagnostic section stamps (guide: in-kernel stamps; shares only, never timing)
+#ifdef MTSG_WF_STAMPS
+#define WF_STAMP(t)                                                                                   \
+    do {                                                                                              \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                                            \
+    } while (0)
 #else
-                        P.L = add(P.L, mulv(P.thr, env_eval_diff(E, rd, rxd, ryd)));
+#define WF_STAMP(t) (void)(t = 0)
 #endif
-                        }
-                    }
-                    endPath = true;
-                } else {
-                    auto &sh = hs.shapes[P.its.shape];
-                    GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
-                    if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
-                        P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
-                    // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
-                    const float snp = dot(rd, P.its.geoN) * P.its.wi.z;
-                    if ((P.depth >= L.max_depth && L.max_depth > 0) ||
-                        (L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
-                        endPath = true;
-                    } else {
-                        P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
-                        if (bsdf.flags & MTSG_F_SMOOTH) {
-                            // Scene::sampleEmitterDirect (scene.cpp:828-852)
-                            float ex, ey;
-                            next2d(SC, L.resolution, smp, px, py, ex, ey);
-                            float emPdf;
-                            const uint32_t ei = dd_sample_reuse(S.em_cdf, S.num_emitters, ex, &emPdf);
-                            if (STATS) cNee++;
-                            const MtsgEmitter &e = S.emitters[ei];
-                            f3 value = mk(0, 0, 0), dd = mk(0, 0, 1);
-                            float pdf = 0.0f, dist = 0.0f;
-                            f3 vlp = mk(0, 0, 0);   // dRec.p where it does not define dRec.d exactly (volpath)
-                            bool vrecomp = false;
-                            if (ENV && e.type != MTSG_EMITTER_AREA) {
-#ifndef MTSG_ABL_NO_ENV_NEE   // timing ablation only
-                                glb_env *E = (glb_env *)S.env;
-                                const EnvSample es = E->constant ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
-                                                                 : env_sample_direct(E, P.its.p, ex, ey);
-                                value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
-                                vlp = add(P.its.p, mul(dd, dist));   // dRec.p = ray(farT) (envmap.cpp:536, constant.cpp:254)
-                                vrecomp = true;
-#endif
-                            } else if (ANA && S.shapes[e.shape].analytic >= 0) {
-                                const AnaSample as =
-                                    ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], P.its.p, ex, ey);
-                                dd = as.d; dist = as.dist; pdf = as.pdf;
-                                vlp = as.p; vrecomp = true;
-                                // AreaLight::sampleDirect (area.cpp:158-173)
-                                if (dot(dd, P.refN) >= 0 && dot(dd, as.n) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
-                                else pdf = 0.0f;
-                            } else {
-                            // TriMesh::samplePosition (trimesh.cpp:412-425), Triangle::sample (triangle.cpp:24-58)
-                            float py2 = ey;
-                            const uint32_t lt = dd_sample_reuse(S.area_cdf + e.cdf_offset, e.tri_count, py2, nullptr);
-                            const uint32_t prim = e.tri_first + lt;
-                            const uint4 pv = make_uint4(hs.pv[4 * prim], hs.pv[4 * prim + 1], hs.pv[4 * prim + 2],
-                                                        hs.pv[4 * prim + 3]);
-                            const float a = safe_sqrt(1.0f - ex);
-                            const float bx = 1 - a, by = a * py2;
-                            const f3 p0 = ldp3(hs.pos + 3 * (size_t)pv.x), p1 = ldp3(hs.pos + 3 * (size_t)pv.y),
-                                     p2 = ldp3(hs.pos + 3 * (size_t)pv.z);
-                            const f3 sideA = sub(p1, p0), sideB = sub(p2, p0);
-                            const f3 lp = add(add(p0, mul(sideA, bx)), mul(sideB, by));
-                            f3 ln;
-                            if (hs.shapes[e.shape].has_normals) {
-                                const f3 n0 = ldp3(hs.nrm + 3 * (size_t)pv.x), n1 = ldp3(hs.nrm + 3 * (size_t)pv.y),
-                                         n2 = ldp3(hs.nrm + 3 * (size_t)pv.z);
-                                ln = normalize(add(add(mul(n0, 1.0f - bx - by), mul(n1, bx)), mul(n2, by)));
-                            } else {
-                                ln = normalize(cross(sideA, sideB));
-                            }
-                            pdf = e.inv_area;
-                            // Shape::sampleDirect (shape.cpp:102-115)
-                            dd = sub(lp, P.its.p);
-                            const float distSquared = len2(dd);
-                            dist = dsqrt(distSquared);
-                            dd = divs(dd, dist);
-                            const float dp = absdot(dd, ln);
-                            pdf *= dp != 0 ? (distSquared / dp) : 0.0f;
-                            // AreaLight::sampleDirect (area.cpp:158-173)
-                            if (dot(dd, P.refN) >= 0 && dot(dd, ln) < 0 && pdf != 0) value = divs(ld3(e.radiance), pdf);
-                            else pdf = 0.0f;
-                            }
-                            if (pdf != 0) {
-                                // the NEE estimate but for visibility (path.cpp:176-199)
-                                const float dpdf = pdf * emPdf;
-                                value = divs(value, emPdf);
-                                f3 c = mk(0, 0, 0);
-                                if (!is_zero(value)) {
-                                    const f3 wo = to_local(P.its.sh, dd);
-                                    // twosided (twosided.cpp:105-131): the nested BSDF of the side wi is on
-                                    f3 qwi = P.its.wi, qwo = wo;
-                                    GBsdf *qb = &bsdf;
-                                    if constexpr (EXT) {
-                                        if (bsdf.type == BSDF_TWOSIDED) {
-                                            const bool flip = !(qwi.z > 0);
-                                            qb = &((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
-                                            if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
-                                        }
-                                    }
-                                    const f3 bsdfVal = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
-                                    if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                        const float bsdfPdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
-                                        const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
-                                        const float weight = pa / (pa + pb);
-                                        c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
-                                    }
-                                }
-                                // Ray(dRec.ref, dRec.d, Epsilon, dRec.dist*(1-ShadowEpsilon)) (scene.cpp:839-840)
-                                P.neeC = c;
-                                sd = dd;
-                                smaxt = dist * (1 - D_SHADOW_EPSILON);
-                                if (L.integrator == MTSG_INTEGRATOR_VOLPATH && vrecomp) {
-                                    // Scene::evalTransmittance (scene.cpp:619-679, 890): the segment to dRec.p,
-                                    // re-normalised; every supported emitter is EOnSurface (envmap.cpp:107,
-                                    // constant.cpp:48, area lights), so the shadow epsilon always applies
-                                    const f3 v = sub(vlp, P.its.p);
-                                    const float rem = dsqrt(len2(v));
-                                    sd = divs(v, rem);
-                                    smaxt = rem * (1 - D_SHADOW_EPSILON);
-                                }
-                                haveShadow = true;
-                            }
-                        }
-                        // BSDF sampling (path.cpp:206-226)
-                        float bx2, by2;
-                        next2d(SC, L.resolution, smp, px, py, bx2, by2);
-                        float u1d = 0.0f;
-                        if (bsdf.type == BSDF_ROUGHDIELECTRIC) u1d = next1d(SC, smp);   // roughdielectric.cpp:554
-                        BSample bs;
-                        if (EXT && bsdf.type == BSDF_TWOSIDED) {
-                            // TwoSidedBRDF::sample(bRec, pdf, sample) (twosided.cpp:151-172)
-                            const bool flip = P.its.wi.z < 0;
-                            f3 qwi = P.its.wi;
-                            if (flip) qwi.z = -qwi.z;
-                            bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
-                                                  bx2, by2, u1d, P.its.u, P.its.v);
-                            if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
-                        } else {
-                            bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
-                        }
-                        if (!is_zero(bs.weight) && !smp.err) {
-                            P.scattered |= bs.sampledType != MTSG_F_NULL;
-                            const f3 wo = to_world(P.its.sh, bs.wo);
-                            if (!L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
-                                // throughput *= bsdfWeight; eta *= bRec.eta (path.cpp:256-257): the same
-                                // products as after the hit, formed now so they need not stay live
-                                P.thr = mulv(P.thr, bs.weight);
-                                P.bsdfPdf = bs.pdf;
-                                P.eta *= bs.eta;
-                                P.sampledType = bs.sampledType;
-                                ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
-                                rd = wo;
-                                rmint = D_EPSILON;
-                                rmaxt = INFINITY;
-                                haveRay = true;
-                            }
-                        }
-                        // no next ray: the path ends once the pending shadow ray is resolved
-                        if (!haveRay && !haveShadow) endPath = true;
-                    }
+
+// per-wave queue append: one atomic for the wave, positions in lane order
+__device__ __forceinline__ uint32_t wave_append(uint32_t *counter, bool pred) {
+    const unsigned long long m = __ballot(pred);
+    if (m == 0) return MTSG_WF_NONE;
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    return pred ? base + rank : MTSG_WF_NONE;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// per-block partial counters: [block][16] (MtsgLaunch::counters indices), summed by wf_flush
+__device__ __forceinline__ void block_counters(unsigned long long *part, const uint32_t *v, uint32_t *red) {
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t s = wave_sum(v[k]);
+        if (lane == 0) red[w * 16 + k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        unsigned long long t = 0;
+        for (uint32_t i = 0; i < BLOCK / 64; ++i) t += red[i * 16 + threadIdx.x];
+        if (t) part[(size_t)blockIdx.x * 16 + threadIdx.x] += t;
+    }
+}
+
+// path state <-> SoA slot s: [0] L, eta  [1] thr, bsdfPdf  [2] neeC, alpha
+// [3] refN, sx  [4] ro, sy  [5] rd, depth  [6] pix, j, sobol index
+// [7] flags | dim << 16, sampledType, closest queue pos, shadow queue pos
+enum { WF_ACTIVE = 1, WF_RAY = 2, WF_PRIMARY = 4, WF_SHADOW = 8, WF_SCATTERED = 16, WF_EMITTED = 32, WF_ERR = 64 };
+__device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, uint32_t s, PathState &st,
+                                        uint32_t &qpos, uint32_t &spos) {
+    const size_t n = W.slots;
+    // all eight vectors in flight at once (an inactive slot's are simply unused)
+    const uint4 f = reinterpret_cast<const uint4 *>(W.state)[7 * n + s];
+    const float4 a = W.state[s], b = W.state[n + s], c = W.state[2 * n + s], d = W.state[3 * n + s],
+                 e = W.state[4 * n + s], g = W.state[5 * n + s];
+    const uint4 h = reinterpret_cast<const uint4 *>(W.state)[6 * n + s];
+    st.active = (f.x & WF_ACTIVE) != 0;
+    qpos = f.z;
+    spos = f.w;
+    if (!st.active) return false;
+    st.P.L = mk(a.x, a.y, a.z); st.P.eta = a.w;
+    st.P.thr = mk(b.x, b.y, b.z); st.P.bsdfPdf = b.w;
+    st.P.neeC = mk(c.x, c.y, c.z); st.P.alpha = c.w;
+    st.P.refN = mk(d.x, d.y, d.z); st.sx = d.w;
+    st.ro = mk(e.x, e.y, e.z); st.sy = e.w;
+    st.rd = mk(g.x, g.y, g.z); st.P.depth = __float_as_int(g.w);
+    st.pix = h.x; st.j = h.y;
+    st.smp.sobolIndex = (uint64_t)h.z | ((uint64_t)h.w << 32);
+    st.smp.sampleIndex = h.y;
+    st.smp.dim = f.x >> 16;
+    st.smp.err = (f.x & WF_ERR) != 0;
+    st.P.sampledType = (int)f.y;
+    st.haveRay = (f.x & WF_RAY) != 0;
+    st.primary = (f.x & WF_PRIMARY) != 0;
+    st.haveShadow = (f.x & WF_SHADOW) != 0;
+    st.P.scattered = (f.x & WF_SCATTERED) != 0;
+    st.P.emitted = (f.x & WF_EMITTED) != 0;
+    pixel_of(L, st.pix, st.px, st.py);
+    return true;
+}
+
+__device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const PathState &st, uint32_t qpos,
+                                         uint32_t spos) {
+    const size_t n = W.slots;
+    uint4 f;
+    f.x = (st.active ? WF_ACTIVE : 0) | (st.haveRay ? WF_RAY : 0) | (st.primary ? WF_PRIMARY : 0) |
+          (st.haveShadow ? WF_SHADOW : 0) | (st.P.scattered ? WF_SCATTERED : 0) | (st.P.emitted ? WF_EMITTED : 0) |
+          (st.smp.err ? WF_ERR : 0) | (st.smp.dim << 16);
+    f.y = (uint32_t)st.P.sampledType;
+    f.z = qpos;
+    f.w = spos;
+    reinterpret_cast<uint4 *>(W.state)[7 * n + s] = f;
+    if (!st.active) return;
+    W.state[s] = make_float4(st.P.L.x, st.P.L.y, st.P.L.z, st.P.eta);
+    W.state[n + s] = make_float4(st.P.thr.x, st.P.thr.y, st.P.thr.z, st.P.bsdfPdf);
+    W.state[2 * n + s] = make_float4(st.P.neeC.x, st.P.neeC.y, st.P.neeC.z, st.P.alpha);
+    W.state[3 * n + s] = make_float4(st.P.refN.x, st.P.refN.y, st.P.refN.z, st.sx);
+    W.state[4 * n + s] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.sy);
+    W.state[5 * n + s] = make_float4(st.rd.x, st.rd.y, st.rd.z, __int_as_float(st.P.depth));
+    reinterpret_cast<uint4 *>(W.state)[6 * n + s] =
+        make_uint4(st.pix, st.j, (uint32_t)st.smp.sobolIndex, (uint32_t)(st.smp.sobolIndex >> 32));
+}
+
+template <bool INSTR, bool SCENE_LDS, int FEAT>
+__global__ __launch_bounds__(BLOCK, MTSG_WF_SHADE_WAVES) void wf_shade(MtsgLaunch L, MtsgWave W,
+                                                                       unsigned long long *part) {
+    extern __shared__ uint32_t lds[];
+    __shared__ uint32_t red[BLOCK / 64 * 16];
+    const MtsgDeviceScene &S = L.scene;
+    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
+    PathCounters c = {};
+    const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
+    uint32_t *cnt = W.cnt + W.parity * 4;
+    const uint32_t lanes = gridDim.x * BLOCK;
+    // the pixel band of this block's XCD (blocks are dealt round-robin over the 8 XCDs),
+    // then the other bands once it is exhausted
+    uint32_t band = blockIdx.x % 8u;
+    uint32_t tried = 0, live = 0;
+    uint32_t stamp[5] = {0, 0, 0, 0, 0};
+    for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < W.slots; s += lanes) {   // same trip count in a wave
+        unsigned long long t0, t1, t2, t3, t4, t5;
+        WF_STAMP(t0);
+        PathState st;
+        uint32_t qpos, spos;
+        const bool was = wf_load(L, W, s, st, qpos, spos);
+        bool occluded = false, hit = false;
+        uint32_t slot = 0, prim = 0;
+        float hu = 0, hv = 0, ht = 0;
+        if (st.active) {
+            occluded = st.haveShadow && spos != MTSG_WF_NONE && W.occl[spos] != 0;
+            if (st.haveRay && qpos != MTSG_WF_NONE) {
+                // the hit record's 4th word: the TriAccel slot with analytic shapes (fill_hit reads
+                // the slot's record), else the primitive index itself
+                const float4 h = W.hit[qpos];
+                const uint32_t w = __float_as_uint(h.w);
+                hit = w != MTSG_WF_NONE;
+                if (hit) {
+                    ht = h.x; hu = h.y; hv = h.z;
+                    if ((FEAT & MTSG_FEAT_ANA) != 0) { slot = w; prim = S.tris[slot].prim; }
+                    else prim = w;
                 }
             }
         }
-
-        if (endPath) {
-            // block->put(samplePos, spec, alpha) (integrator.cpp:184): the own-pixel
-            // splat is stored as {L.rgb, w} (alpha in {0,1} in the sign bit of w) and
-            // film_reduce re-forms weight * value[k] -- the same products
-            const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
-            float ownW = 0.0f;
-            const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
-            float4 rec4;
-            if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha == 0.0f ? -ownW : ownW);
-            else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
-            if (INSTR && L.samples) {
-                const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
-                float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
-                rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
-                rec[4] = sx; rec[5] = sy; rec[6] = (float)P.depth; rec[7] = smp.err ? 1.0f : 0.0f;
+        WF_STAMP(t1);
+        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
+        WF_STAMP(t2);
+        // regeneration: ended and empty slots take the next items of the bands
+        while (tried < 8) {
+            const unsigned long long m = __ballot(!st.active);
+            if (m == 0) break;
+            const uint32_t n = (uint32_t)__popcll(m);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const int leader = __builtin_ctzll(m);
+            unsigned long long base = 0;
+            if ((int)lane_id() == leader) base = atomicAdd(W.cursor + band, (unsigned long long)n);
+            base = __shfl(base, leader);
+            const uint64_t npx = (uint64_t)(W.band_tiles[band + 1] - W.band_tiles[band]) * 64u;
+            const uint64_t limit = npx * L.chunk_spp;
+            if (!st.active) {
+                const uint64_t k = base + rank;
+                if (k < limit) {
+                    const uint64_t jj = k / npx;
+                    sh.start(st, jj * L.num_pixels + (uint64_t)W.band_tiles[band] * 64u + (k - jj * npx));
+                }
             }
-            cLen += (unsigned long long)P.depth;
-            cSamples++;
-            if (STATS) cSobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
-            if (smp.err) cErr++;
-            active = false;
-            haveRay = haveShadow = false;
+            if (base + n > limit) { band = (band + 1) % 8u; ++tried; }
+        }
+        WF_STAMP(t3);
+        // the next bounce's rays (megakernel step B's intervals and counts)
+        float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, s0 = r0, s1 = r0;
+        bool ps = false, pr = false;
+        if (st.active && st.haveShadow) {
+            c.shadow++;
+            float mint, maxt;
+            if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
+                ps = true;
+                s0 = make_float4(st.P.its.p.x, st.P.its.p.y, st.P.its.p.z, mint);
+                s1 = make_float4(st.sd.x, st.sd.y, st.sd.z, maxt);
+            }
+        }
+        if (st.active && st.haveRay) {
+            c.rays++;
+            float mint, maxt;
+            if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
+                pr = true;
+                r0 = make_float4(st.ro.x, st.ro.y, st.ro.z, mint);
+                r1 = make_float4(st.rd.x, st.rd.y, st.rd.z, maxt);
+            }
+        }
+        spos = wave_append(cnt + 1, ps);
+        qpos = wave_append(cnt + 0, pr);
+        if (ps) { W.sray[2 * (size_t)spos] = s0; W.sray[2 * (size_t)spos + 1] = s1; }
+        if (pr) { W.qray[2 * (size_t)qpos] = r0; W.qray[2 * (size_t)qpos + 1] = r1; }
+        WF_STAMP(t4);
+        live += st.active ? 1u : 0u;
+        if (st.active || was) wf_store(W, s, st, qpos, spos);
+        WF_STAMP(t5);
+#ifdef MTSG_WF_STAMPS
+        stamp[0] += (uint32_t)(t1 - t0); stamp[1] += (uint32_t)(t2 - t1); stamp[2] += (uint32_t)(t3 - t2);
+        stamp[3] += (uint32_t)(t4 - t3); stamp[4] += (uint32_t)(t5 - t4);
+#endif
+    }
+    const uint32_t lv = wave_sum(live);
+    if (lane_id() == 0 && lv) atomicAdd(cnt + 2, lv);
+    uint32_t v[16] = {};
+    v[0] = (uint32_t)c.samples; v[1] = (uint32_t)c.rays; v[2] = (uint32_t)c.shadow; v[3] = (uint32_t)c.len;
+    v[6] = (uint32_t)c.err;
+    if (INSTR) { v[7] = (uint32_t)c.hits; v[9] = (uint32_t)c.nee; v[10] = (uint32_t)c.sobol; }
+#ifdef MTSG_WF_STAMPS   // diagnostic build: cycles per section, summed over waves (counters 11-15)
+    if (lane_id() == 0)
+        for (int k = 0; k < 5; ++k) v[11 + k] = stamp[k] >> 4;
+#endif
+    (void)stamp;
+    block_counters(part, v, red);
+}
+
+// both queues of one bounce: entries [0, nc) closest hit, [nc, nc + ns) shadow;
+// block 0 also clears the other parity's counters for the next wf_shade
+template <bool STATS, bool SCENE_LDS, bool ANA>
+__global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunch L, MtsgWave W,
+                                                                       unsigned long long *part) {
+    extern __shared__ uint32_t lds[];
+    __shared__ uint32_t red[BLOCK / 64 * 16];
+    const MtsgDeviceScene &S = L.scene;
+    if (blockIdx.x == 0 && threadIdx.x < 4) W.cnt[(W.parity ^ 1u) * 4 + threadIdx.x] = 0;
+    const uint32_t nc = W.cnt[W.parity * 4 + 0], ns = W.cnt[W.parity * 4 + 1];
+    if (blockIdx.x * BLOCK >= nc + ns) return;   // block-uniform
+    uint32_t stackBase = 0;
+    if (SCENE_LDS && !L.scan) {
+        const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
+        const uint32_t *gn = reinterpret_cast<const uint32_t *>(S.nodes);
+        const uint32_t *gt = reinterpret_cast<const uint32_t *>(S.tris);
+        for (uint32_t i = threadIdx.x; i < nodeWords; i += BLOCK) lds[i] = gn[i];
+        for (uint32_t i = threadIdx.x; i < triWords; i += BLOCK) lds[nodeWords + i] = gt[i];
+        stackBase = nodeWords + triWords;
+        __syncthreads();
+    }
+    lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)lds, 16);
+    lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + L.num_nodes * 16), 16);
+    lds_stk_n *stkN = (lds_stk_n *)(lds + stackBase) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + stackBase + L.stack_depth * BLOCK) + threadIdx.x;
+    unsigned long long cN = 0, cT = 0;
+    const uint32_t n = nc + ns;
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const bool shadow = i >= nc;
+        const uint32_t k = shadow ? i - nc : i;
+        const float4 *q = shadow ? W.sray : W.qray;
+        const float4 a = q[2 * (size_t)k], b = q[2 * (size_t)k + 1];
+        const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
+        const float mint = a.w, maxt = b.w;
+        uint32_t slot = 0;
+        float hu = 0, hv = 0, ht = 0;
+        if (shadow) {
+            bool occ;
+            if (SCENE_LDS && L.scan)
+                occ = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+            else if (SCENE_LDS)
+                occ = traverse<true, STATS, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht, cN,
+                                                 cT, S.analytic);
+            else
+                occ = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
+                                                 slot, hu, hv, ht, cN, cT, S.analytic);
+            W.occl[k] = occ ? 1u : 0u;
+        } else {
+            bool hit;
+            if (SCENE_LDS && L.scan)
+                hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+            else if (SCENE_LDS)
+                hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht,
+                                                  cN, cT, S.analytic);
+            else
+                hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
+                                                  slot, hu, hv, ht, cN, cT, S.analytic);
+            const uint32_t w = !hit ? MTSG_WF_NONE : ANA ? slot
+                             : (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+            W.hit[k] = make_float4(ht, hu, hv, __uint_as_float(w));
         }
     }
-    atomicAdd(L.counters + 0, cSamples);
-    atomicAdd(L.counters + 1, cRays);
-    atomicAdd(L.counters + 2, cShadow);
-    atomicAdd(L.counters + 3, cLen);
     if (STATS) {
-        atomicAdd(L.counters + 4, cNodes);
-        atomicAdd(L.counters + 5, cTests);
-        atomicAdd(L.counters + 7, cHits);
-        atomicAdd(L.counters + 9, cNee);
-        atomicAdd(L.counters + 10, cSobol);
+        uint32_t v[16] = {};
+        v[4] = (uint32_t)cN;
+        v[5] = (uint32_t)cT;
+        block_counters(part, v, red);
     }
-    if (cErr) atomicAdd(L.counters + 6, cErr);
+}
+
+// the per-block partial counters of a chunk -> MtsgLaunch::counters
+__global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters) {
+    const uint32_t k = threadIdx.x & 15u;   // 256 threads: counter k, blocks b = threadIdx / 16 (mod 16)
+    unsigned long long t = 0;
+    for (uint32_t b = threadIdx.x >> 4; b < blocks; b += 16) t += part[(size_t)b * 16 + k];
+    if (t) atomicAdd(counters + k, t);
 }
 
 // ===========================================================================
@@ -1824,6 +2244,93 @@ hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream) {
     hipLaunchKernelGGL(arith_probe, dim3((n + 255) / 256), dim3(256), 0, stream, a, b, out, n);
     return hipGetLastError();
+}
+
+// wavefront launchers: wf_shade needs no traversal stacks; wf_trace stages
+// the BVH of SCENE_LDS scenes (not the linear-scan ones) and holds the stacks
+size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) {
+    const size_t scene = L.scene_lds ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * (12 + 7) +
+                                        (size_t)L.num_verts * 6 + (size_t)L.num_shapes * (sizeof(MtsgShape) / 4))
+                                     : 0;
+    return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene) * 4;
+}
+size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
+    const bool scan = L.scene_lds && L.scan;
+    const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
+    const size_t stack = scan ? 0 : ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2;
+    return (scene + stack) * 4 + 16;
+}
+
+template <int FEAT>
+static void launch_wf_shade_f(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid, bool instr,
+                              hipStream_t s) {
+    const size_t lds = mtsg_wf_shade_lds_bytes(L);
+#define MTSG_SHADE(I, SL) hipLaunchKernelGGL((wf_shade<I, SL, FEAT>), dim3(grid), dim3(BLOCK), lds, s, L, W, part)
+    if (L.scene_lds) { if (instr) MTSG_SHADE(true, true); else MTSG_SHADE(false, true); }
+    else { if (instr) MTSG_SHADE(true, false); else MTSG_SHADE(false, false); }
+#undef MTSG_SHADE
+}
+
+hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
+                                bool instr, hipStream_t s) {
+    switch (mtsg_path_features(L)) {
+        case 0: launch_wf_shade_f<0>(L, W, part, grid, instr, s); break;
+        case MTSG_FEAT_ENV: launch_wf_shade_f<MTSG_FEAT_ENV>(L, W, part, grid, instr, s); break;
+        case MTSG_FEAT_EXT: launch_wf_shade_f<MTSG_FEAT_EXT>(L, W, part, grid, instr, s); break;
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: launch_wf_shade_f<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, W, part, grid, instr, s); break;
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: launch_wf_shade_f<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, W, part, grid, instr, s); break;
+        default: launch_wf_shade_f<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, W, part, grid, instr, s); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
+                                bool stats, hipStream_t s) {
+    const size_t lds = mtsg_wf_trace_lds_bytes(L);
+#define MTSG_WFT(ST, SL, A) hipLaunchKernelGGL((wf_trace<ST, SL, A>), dim3(grid), dim3(BLOCK), lds, s, L, W, part)
+    const bool ana = L.ana != 0;
+    if (stats) {
+        if (L.scene_lds) { if (ana) MTSG_WFT(true, true, true); else MTSG_WFT(true, true, false); }
+        else { if (ana) MTSG_WFT(true, false, true); else MTSG_WFT(true, false, false); }
+    } else {
+        if (L.scene_lds) { if (ana) MTSG_WFT(false, true, true); else MTSG_WFT(false, true, false); }
+        else { if (ana) MTSG_WFT(false, false, true); else MTSG_WFT(false, false, false); }
+    }
+#undef MTSG_WFT
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(wf_flush, dim3(1), dim3(256), 0, s, part, blocks, counters);
+    return hipGetLastError();
+}
+
+// resident blocks per CU of the two wavefront kernels (their grids)
+int mtsg_wf_occupancy(const MtsgLaunch &L, int *shadeBpc, int *traceBpc) {
+    *shadeBpc = *traceBpc = 0;
+    const size_t ls = mtsg_wf_shade_lds_bytes(L), lt = mtsg_wf_trace_lds_bytes(L);
+    int r = 0;
+    switch (mtsg_path_features(L)) {   // the instrumented variants run on the same grid
+#define MTSG_OCC(F) \
+        r = L.scene_lds ? (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(shadeBpc, wf_shade<false, true, F>, BLOCK, ls) \
+                        : (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(shadeBpc, wf_shade<false, false, F>, BLOCK, ls); \
+        break;
+        case 0: MTSG_OCC(0)
+        case MTSG_FEAT_ENV: MTSG_OCC(MTSG_FEAT_ENV)
+        case MTSG_FEAT_EXT: MTSG_OCC(MTSG_FEAT_EXT)
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: MTSG_OCC(MTSG_FEAT_ENV | MTSG_FEAT_EXT)
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: MTSG_OCC(MTSG_FEAT_EXT | MTSG_FEAT_ANA)
+        default: MTSG_OCC(MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA)
+#undef MTSG_OCC
+    }
+    if (r) return r;
+    const bool ana = L.ana != 0;
+    if (L.scene_lds) r = ana ? (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(traceBpc, wf_trace<false, true, true>, BLOCK, lt)
+                             : (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(traceBpc, wf_trace<false, true, false>, BLOCK, lt);
+    else r = ana ? (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(traceBpc, wf_trace<false, false, true>, BLOCK, lt)
+                 : (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(traceBpc, wf_trace<false, false, false>, BLOCK, lt);
+    return r;
 }
 
 template <bool SCENE_LDS, int FEAT, int WAVES>

@@ -27,7 +27,7 @@ class MtsgpuError(RuntimeError):
 
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
-           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
            'mtsgpu_trace_rays']
 
 _lib = None
@@ -60,6 +60,7 @@ def load_library(path=None):
     L.mtsgpu_destroy.argtypes = [C.c_void_p]
     L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
+    L.mtsgpu_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     L.mtsgpu_trace_rays.argtypes = [C.c_void_p, P(C.c_float), C.c_uint32, C.c_int, P(C.c_float), P(C.c_double)]
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
@@ -103,19 +104,37 @@ class Context:
         self._check(self.L.mtsgpu_upload_scene(self.h, C.byref(d)))
         self.scene = scene
 
+    def debug_counters(self):
+        """The 16 raw device counters of the last render (include/mtsgpu.h)."""
+        out = (C.c_uint64 * 16)()
+        self._check(self.L.mtsgpu_debug_counters(self.h, out))
+        return list(out)
+
     def scene_info(self):
         info = (C.c_uint32 * 4)()
         self._check(self.L.mtsgpu_debug_scene_info(self.h, info))
         return {'nodes': info[0], 'prims': info[1], 'depth': info[2], 'cus': info[3]}
 
-    def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False):
-        """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict)."""
+    @staticmethod
+    def _engine_flags(engine):
+        if engine is None:
+            return 0
+        if engine == 'wavefront':
+            return abi.FLAG_WAVEFRONT
+        if engine == 'megakernel':
+            return abi.FLAG_MEGAKERNEL
+        raise ValueError('engine must be None, "wavefront" or "megakernel"')
+
+    def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False, engine=None):
+        """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict).
+        engine: None (the library's default), 'wavefront' or 'megakernel'."""
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
         x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
         if traversal_stats:
             p.flags |= abi.FLAG_TRAVERSAL_STATS
+        p.flags |= self._engine_flags(engine)
         b = film_border(integ.rfilter, integ.rfilterParam)
         film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
         smp = np.zeros((w * h * integ.sampleCount, abi.SAMPLE_RECORD_FLOATS), np.float32) if samples else None
@@ -125,11 +144,12 @@ class Context:
                                           C.byref(st)))
         return film, smp, st.as_dict()
 
-    def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0)):
+    def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0), engine=None):
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
         x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+        p.flags |= self._engine_flags(engine)
         st = abi.Stats()
         self._check(self.L.mtsgpu_render_device(self.h, C.byref(p), C.c_void_p(film_ptr),
                                                  C.c_void_p(stream_ptr) if stream_ptr else None, C.byref(st)))
