@@ -78,7 +78,7 @@ struct mtsgpu_ctx {
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
     // wavefront pipeline: path slots, ray queues and results, counters
-    DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_cnt, wf_cursor, wf_part;
+    DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_rcnt, wf_live, wf_ovf, wf_part;
     uint32_t *wf_live_host = nullptr;   // pinned: live-slot counts read back while the pipeline runs
     hipEvent_t wf_ev[8] = {};
     unsigned long long last_counters[16] = {};
@@ -271,16 +271,18 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     W.sray = (float4 *)ctx->wf_sray.p;
     W.hit = (float4 *)ctx->wf_hit.p;
     W.occl = (uint32_t *)ctx->wf_occl.p;
-    W.cnt = (uint32_t *)ctx->wf_cnt.p;
-    W.cursor = (unsigned long long *)ctx->wf_cursor.p;
+    W.rcnt = (uint32_t *)ctx->wf_rcnt.p;
+    W.live = (uint32_t *)ctx->wf_live.p;
+    W.ovf = (uint2 *)ctx->wf_ovf.p;
     W.slots = slots;
-    const uint32_t tiles = L.num_pixels / 64;
-    for (int b = 0; b <= 8; ++b) W.band_tiles[b] = (uint32_t)((uint64_t)tiles * b / 8);
+    W.regions = (uint32_t)shadeGrid;
+    W.rounds = slots / (uint32_t)(shadeGrid * BLOCK_THREADS);
+    W.split = (uint32_t)(traceGrid / shadeGrid);
+    W.ovf_depth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
     unsigned long long *part = (unsigned long long *)ctx->wf_part.p;
     const int partBlocks = std::max(shadeGrid, traceGrid);
     if ((e = hipMemsetAsync((char *)ctx->wf_state.p + (size_t)7 * slots * 16, 0, (size_t)slots * 16, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(ctx->wf_cnt.p, 0, 8 * 4, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(ctx->wf_cursor.p, 0, 8 * 8, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->wf_live.p, 0, 2 * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(part, 0, (size_t)partBlocks * 16 * 8, stream)) != hipSuccess)
         return hip_fail(ctx, e, "wavefront reset");
     constexpr int POLL = 4, LAG = 2, RING = 8;
@@ -293,7 +295,7 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
             return hip_fail(ctx, e, "wf_shade launch");
         if (it % POLL == 0) {
             const int r = polls % RING;
-            if ((e = hipMemcpyAsync(ctx->wf_live_host + r, W.cnt + W.parity * 4 + 2, 4, hipMemcpyDeviceToHost,
+            if ((e = hipMemcpyAsync(ctx->wf_live_host + r, W.live + W.parity, 4, hipMemcpyDeviceToHost,
                                     stream)) != hipSuccess ||
                 (e = hipEventRecord(ctx->wf_ev[r], stream)) != hipSuccess)
                 return hip_fail(ctx, e, "wavefront poll");
@@ -470,7 +472,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (bpc <= 0) bpc = 1;
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
     // execution engine (same per-sample results): the wavefront pipeline or the megakernel
-    bool wave = pathLike && !L.scene_lds;   // default: wavefront for scenes whose BVH lives in HBM
+    bool wave = false;   // default: the megakernel (DESIGN.md 4 has the engine A/B)
     if (const char *env = std::getenv("MTSGPU_ENGINE")) wave = pathLike && std::strcmp(env, "wavefront") == 0;
     if (P->flags & MTSGPU_FLAG_WAVEFRONT) wave = pathLike;
     if (P->flags & MTSGPU_FLAG_MEGAKERNEL) wave = false;
@@ -480,20 +482,24 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         int sb = 0, tb = 0;
         mtsg_wf_occupancy(L, &sb, &tb);
         if (sb <= 0 || tb <= 0) return fail(ctx, MTSGPU_EHIP, "wavefront kernels do not fit the device");
-        shadeGrid = std::max(8, ctx->num_cus * sb / 8 * 8);   // a multiple of 8: one pixel band per XCD
-        traceGrid = ctx->num_cus * tb;
+        shadeGrid = std::max(8, ctx->num_cus * sb / 8 * 8);   // a multiple of 8: XCD-aware slot lanes
+        const int split = std::max(1, (ctx->num_cus * tb + shadeGrid - 1) / shadeGrid);
+        traceGrid = shadeGrid * split;
         const uint64_t lanes = (uint64_t)shadeGrid * BLOCK_THREADS;
-        uint64_t target = (uint64_t)1 << 20;
+        uint64_t target = (uint64_t)1 << 21;
         if (const char *env = std::getenv("MTSGPU_WF_SLOTS")) target = std::max<uint64_t>(1, std::strtoull(env, nullptr, 10));
         const uint64_t items = (uint64_t)std::min(chunk, P->spp) * L.num_pixels;
         target = std::min(target, items);
         slots = (uint32_t)(std::max<uint64_t>(1, (target + lanes - 1) / lanes) * lanes);
+        const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
         if ((e = ctx->wf_state.ensure((size_t)MTSG_WF_STATE_VECS * slots * 16)) != hipSuccess ||
             (e = ctx->wf_qray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
             (e = ctx->wf_sray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
             (e = ctx->wf_hit.ensure((size_t)slots * 16)) != hipSuccess ||
-            (e = ctx->wf_occl.ensure((size_t)slots * 4)) != hipSuccess || (e = ctx->wf_cnt.ensure(8 * 4)) != hipSuccess ||
-            (e = ctx->wf_cursor.ensure(8 * 8)) != hipSuccess ||
+            (e = ctx->wf_occl.ensure((size_t)slots * 4)) != hipSuccess ||
+            (e = ctx->wf_rcnt.ensure((size_t)4 * shadeGrid * 4)) != hipSuccess ||
+            (e = ctx->wf_live.ensure(2 * 4)) != hipSuccess ||
+            (e = ctx->wf_ovf.ensure((size_t)traceGrid * BLOCK_THREADS * ovfDepth * 8)) != hipSuccess ||
             (e = ctx->wf_part.ensure((size_t)std::max(shadeGrid, traceGrid) * 16 * 8)) != hipSuccess)
             return hip_fail(ctx, e, "wavefront buffers");
         if (!ctx->wf_live_host) {
@@ -621,7 +627,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_qray, &ctx->wf_sray, &ctx->wf_hit,
-                      &ctx->wf_occl, &ctx->wf_cnt, &ctx->wf_cursor, &ctx->wf_part, &ctx->env_grows, &ctx->env_gcols};
+                      &ctx->wf_occl, &ctx->wf_rcnt, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
     for (hipEvent_t &e : ctx->wf_ev)
         if (e) (void)hipEventDestroy(e);

@@ -196,20 +196,26 @@ struct MtsgLookup {
 
 // The wavefront pipeline (path_kernel.hip: wf_shade / wf_trace):
 // per-path state in SoA slots, the two ray queues of one bounce and their
-// results.  Queue positions are handed out per wave (one atomic per wave).
+// results.  wf_shade block b owns queue region [b * rounds * 256, ...) and
+// appends to it densely (one LDS atomic per wave); wf_trace block t works on
+// region t / split.  No global atomics on the data path.
 #define MTSG_WF_STATE_VECS 8          // float4 state vectors per slot
 #define MTSG_WF_NONE 0xffffffffu      // no queue entry (ray skipped or outside the scene box)
+#ifndef MTSG_WF_LDS_STACK
+#define MTSG_WF_LDS_STACK 12          // wf_trace: traversal stack entries per lane in LDS (deeper: HBM)
+#endif
 struct MtsgWave {
     float4 *state;                    // [MTSG_WF_STATE_VECS][slots]
     float4 *qray;                     // [2 * slots] closest-hit rays {o, mint}, {d, maxt}
     float4 *sray;                     // [2 * slots] shadow rays
-    float4 *hit;                      // [slots] {t, u, v, slot bits (MTSG_WF_NONE: miss)}
+    float4 *hit;                      // [slots] {t, u, v, prim (TriAccel slot with analytic shapes) | MTSG_WF_NONE}
     uint32_t *occl;                   // [slots] shadow results
-    uint32_t *cnt;                    // [2][4] per parity: closest count, shadow count, live slots, -
-    unsigned long long *cursor;       // [8] item cursors of the 8 pixel bands (one per XCD)
-    uint32_t slots;                   // multiple of the shade grid's lanes
+    uint32_t *rcnt;                   // [2 parities][2 queues][regions] entries per region
+    uint32_t *live;                   // [2 parities] live slots after wf_shade
+    uint2 *ovf;                       // wf_trace stack overflow: [trace lanes][ovf_depth]
+    uint32_t slots;                   // = regions * rounds * 256
     uint32_t parity;                  // bounce index & 1
-    uint32_t band_tiles[9];           // tile ranges of the 8 pixel bands
+    uint32_t regions, rounds, split, ovf_depth;
 };
 
 struct MtsgLaunch {

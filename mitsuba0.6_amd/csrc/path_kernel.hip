@@ -168,11 +168,14 @@ __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float(
 // leaf parks it and keeps descending until every lane of the wave holds a
 // leaf; then all lanes test their parked leaves together.  Same closest hit
 // (tie rule included) as a plain depth-first traversal.
-template <bool ANY, bool STATS, bool ANA = false, typename NodeT, typename TriT>
+// LDSK > 0: the first LDSK stack entries live in LDS, deeper ones in a per-lane
+// global array `ovf` ({node, distance} pairs): a short LDS stack keeps the
+// traversal kernel's LDS per lane small (wf_trace occupancy); 0: all in LDS
+template <bool ANY, bool STATS, bool ANA = false, int LDSK = 0, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
                                          float &bt, unsigned long long &nodes, unsigned long long &tests,
-                                         const MtsgAnalytic *anaArr = nullptr) {
+                                         const MtsgAnalytic *anaArr = nullptr, uint2 *ovf = nullptr) {
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
@@ -188,7 +191,12 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     auto pop = [&]() -> int {
         while (sp > 0) {
             --sp;
-            if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
+            if (LDSK == 0 || sp < LDSK) {
+                if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
+            } else {
+                const uint2 e = ovf[sp - LDSK];
+                if (ANY || dist_up16((uint16_t)e.y) <= bt) return (int)e.x;
+            }
         }
         return DONE;
     };
@@ -217,8 +225,12 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 int nearC = e.x, farC = e.y;
                 float farT = n1;
                 if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
-                stkN[sp * BLOCK] = farC;
-                stkD[sp * BLOCK] = dist_down16(farT);
+                if (LDSK == 0 || sp < LDSK) {
+                    stkN[sp * BLOCK] = farC;
+                    stkD[sp * BLOCK] = dist_down16(farT);
+                } else {
+                    ovf[sp - LDSK] = make_uint2((uint32_t)farC, dist_down16(farT));
+                }
                 ++sp;
                 node = nearC;
             } else if (h0) {
@@ -1395,8 +1407,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// per-block partial counters: [block][16] (MtsgLaunch::counters indices), summed by wf_flush
-__device__ __forceinline__ void block_counters(unsigned long long *part, const uint32_t *v, uint32_t *red) {
+// per-block partial counters: [block][16] (MtsgLaunch::counters indices), summed by wf_flush;
+// counter `atomicK` (if any) is instead added to *atomicDst (one atomic per block)
+__device__ __forceinline__ void block_counters(unsigned long long *part, const uint32_t *v, uint32_t *red,
+                                               int atomicK = -1, uint32_t *atomicDst = nullptr) {
     const uint32_t w = threadIdx.x >> 6, lane = lane_id();
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -1407,7 +1421,11 @@ __device__ __forceinline__ void block_counters(unsigned long long *part, const u
     if (threadIdx.x < 16) {
         unsigned long long t = 0;
         for (uint32_t i = 0; i < BLOCK / 64; ++i) t += red[i * 16 + threadIdx.x];
-        if (t) part[(size_t)blockIdx.x * 16 + threadIdx.x] += t;
+        if ((int)threadIdx.x == atomicK) {
+            if (t) atomicAdd(atomicDst, (uint32_t)t);
+        } else if (t) {
+            part[(size_t)blockIdx.x * 16 + threadIdx.x] += t;
+        }
     }
 }
 
@@ -1416,7 +1434,7 @@ __device__ __forceinline__ void block_counters(unsigned long long *part, const u
 // [7] flags | dim << 16, sampledType, closest queue pos, shadow queue pos
 enum { WF_ACTIVE = 1, WF_RAY = 2, WF_PRIMARY = 4, WF_SHADOW = 8, WF_SCATTERED = 16, WF_EMITTED = 32, WF_ERR = 64 };
 __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, uint32_t s, PathState &st,
-                                        uint32_t &qpos, uint32_t &spos) {
+                                        uint32_t &qpos, uint32_t &spos, uint32_t &flags) {
     const size_t n = W.slots;
     // all eight vectors in flight at once (an inactive slot's are simply unused)
     const uint4 f = reinterpret_cast<const uint4 *>(W.state)[7 * n + s];
@@ -1426,6 +1444,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     st.active = (f.x & WF_ACTIVE) != 0;
     qpos = f.z;
     spos = f.w;
+    flags = f.x;
     if (!st.active) return false;
     st.P.L = mk(a.x, a.y, a.z); st.P.eta = a.w;
     st.P.thr = mk(b.x, b.y, b.z); st.P.bsdfPdf = b.w;
@@ -1449,10 +1468,10 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
 }
 
 __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const PathState &st, uint32_t qpos,
-                                         uint32_t spos) {
+                                         uint32_t spos, uint32_t extra) {
     const size_t n = W.slots;
     uint4 f;
-    f.x = (st.active ? WF_ACTIVE : 0) | (st.haveRay ? WF_RAY : 0) | (st.primary ? WF_PRIMARY : 0) |
+    f.x = extra | (st.active ? WF_ACTIVE : 0) | (st.haveRay ? WF_RAY : 0) | (st.primary ? WF_PRIMARY : 0) |
           (st.haveShadow ? WF_SHADOW : 0) | (st.P.scattered ? WF_SCATTERED : 0) | (st.P.emitted ? WF_EMITTED : 0) |
           (st.smp.err ? WF_ERR : 0) | (st.smp.dim << 16);
     f.y = (uint32_t)st.P.sampledType;
@@ -1470,28 +1489,38 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
         make_uint4(st.pix, st.j, (uint32_t)st.smp.sobolIndex, (uint32_t)(st.smp.sobolIndex >> 32));
 }
 
+// Slot s of wf_shade runs items v, v + slots, v + 2 slots, ... (v = the slot's
+// XCD-aware lane index: each XCD's slots hold neighbouring pixels, as the
+// megakernel's xcd_block), regenerating as soon as a path ends; flag WF_DONE
+// marks a slot whose items are used up.
+enum { WF_DONE = 128 };
+__device__ __forceinline__ uint64_t wf_lane_index(uint32_t s) {
+    const uint32_t G = gridDim.x, t = s % BLOCK, b = (s / BLOCK) % G, r = s / (BLOCK * G);
+    const uint32_t pb = (G % 8u == 0) ? (b % 8u) * (G / 8u) + b / 8u : b;
+    return ((uint64_t)r * G + pb) * BLOCK + t;
+}
+
 template <bool INSTR, bool SCENE_LDS, int FEAT>
 __global__ __launch_bounds__(BLOCK, MTSG_WF_SHADE_WAVES) void wf_shade(MtsgLaunch L, MtsgWave W,
                                                                        unsigned long long *part) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t red[BLOCK / 64 * 16];
+    __shared__ uint32_t qcnt[2];   // this block's region: closest, shadow entries
+    if (threadIdx.x < 2) qcnt[threadIdx.x] = 0;
     const MtsgDeviceScene &S = L.scene;
-    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
+    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);   // ends with a barrier
     PathCounters c = {};
     const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
-    uint32_t *cnt = W.cnt + W.parity * 4;
     const uint32_t lanes = gridDim.x * BLOCK;
-    // the pixel band of this block's XCD (blocks are dealt round-robin over the 8 XCDs),
-    // then the other bands once it is exhausted
-    uint32_t band = blockIdx.x % 8u;
-    uint32_t tried = 0, live = 0;
+    const uint32_t region = blockIdx.x * W.rounds * BLOCK;
+    uint32_t live = 0;
     uint32_t stamp[5] = {0, 0, 0, 0, 0};
-    for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < W.slots; s += lanes) {   // same trip count in a wave
+    for (uint32_t s = blockIdx.x * BLOCK + threadIdx.x; s < W.slots; s += lanes) {   // same trip count in a block
         unsigned long long t0, t1, t2, t3, t4, t5;
         WF_STAMP(t0);
         PathState st;
-        uint32_t qpos, spos;
-        const bool was = wf_load(L, W, s, st, qpos, spos);
+        uint32_t qpos, spos, flags;
+        const bool was = wf_load(L, W, s, st, qpos, spos, flags);
         bool occluded = false, hit = false;
         uint32_t slot = 0, prim = 0;
         float hu = 0, hv = 0, ht = 0;
@@ -1511,28 +1540,18 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_SHADE_WAVES) void wf_shade(MtsgLaunc
             }
         }
         WF_STAMP(t1);
-        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
+        bool ended = false;
+        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) { sh.finish(st); ended = true; }
         WF_STAMP(t2);
-        // regeneration: ended and empty slots take the next items of the bands
-        while (tried < 8) {
-            const unsigned long long m = __ballot(!st.active);
-            if (m == 0) break;
-            const uint32_t n = (uint32_t)__popcll(m);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const int leader = __builtin_ctzll(m);
-            unsigned long long base = 0;
-            if ((int)lane_id() == leader) base = atomicAdd(W.cursor + band, (unsigned long long)n);
-            base = __shfl(base, leader);
-            const uint64_t npx = (uint64_t)(W.band_tiles[band + 1] - W.band_tiles[band]) * 64u;
-            const uint64_t limit = npx * L.chunk_spp;
-            if (!st.active) {
-                const uint64_t k = base + rank;
-                if (k < limit) {
-                    const uint64_t jj = k / npx;
-                    sh.start(st, jj * L.num_pixels + (uint64_t)W.band_tiles[band] * 64u + (k - jj * npx));
-                }
+        // regeneration: the slot's next item (static stride, no atomics)
+        bool done = (flags & WF_DONE) != 0;
+        if (!st.active && !done) {
+            uint64_t it = (ended || was) ? (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots : wf_lane_index(s);
+            while (true) {
+                if (it >= L.num_items) { done = true; break; }
+                if (sh.start(st, it)) break;
+                it += W.slots;   // padding pixel of a partial tile
             }
-            if (base + n > limit) { band = (band + 1) % 8u; ++tried; }
         }
         WF_STAMP(t3);
         // the next bounce's rays (megakernel step B's intervals and counts)
@@ -1556,44 +1575,49 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_SHADE_WAVES) void wf_shade(MtsgLaunc
                 r1 = make_float4(st.rd.x, st.rd.y, st.rd.z, maxt);
             }
         }
-        spos = wave_append(cnt + 1, ps);
-        qpos = wave_append(cnt + 0, pr);
-        if (ps) { W.sray[2 * (size_t)spos] = s0; W.sray[2 * (size_t)spos + 1] = s1; }
-        if (pr) { W.qray[2 * (size_t)qpos] = r0; W.qray[2 * (size_t)qpos + 1] = r1; }
+        spos = wave_append(qcnt + 1, ps);
+        qpos = wave_append(qcnt + 0, pr);
+        if (ps) { spos += region; W.sray[2 * (size_t)spos] = s0; W.sray[2 * (size_t)spos + 1] = s1; }
+        if (pr) { qpos += region; W.qray[2 * (size_t)qpos] = r0; W.qray[2 * (size_t)qpos + 1] = r1; }
         WF_STAMP(t4);
         live += st.active ? 1u : 0u;
-        if (st.active || was) wf_store(W, s, st, qpos, spos);
+        if (st.active || was || ended || done != ((flags & WF_DONE) != 0))
+            wf_store(W, s, st, qpos, spos, done ? WF_DONE : 0u);
         WF_STAMP(t5);
 #ifdef MTSG_WF_STAMPS
         stamp[0] += (uint32_t)(t1 - t0); stamp[1] += (uint32_t)(t2 - t1); stamp[2] += (uint32_t)(t3 - t2);
         stamp[3] += (uint32_t)(t4 - t3); stamp[4] += (uint32_t)(t5 - t4);
 #endif
     }
-    const uint32_t lv = wave_sum(live);
-    if (lane_id() == 0 && lv) atomicAdd(cnt + 2, lv);
     uint32_t v[16] = {};
     v[0] = (uint32_t)c.samples; v[1] = (uint32_t)c.rays; v[2] = (uint32_t)c.shadow; v[3] = (uint32_t)c.len;
     v[6] = (uint32_t)c.err;
+    v[8] = live;   // (slot 8 is otherwise unused) live slots: this block's region count below
     if (INSTR) { v[7] = (uint32_t)c.hits; v[9] = (uint32_t)c.nee; v[10] = (uint32_t)c.sobol; }
 #ifdef MTSG_WF_STAMPS   // diagnostic build: cycles per section, summed over waves (counters 11-15)
     if (lane_id() == 0)
         for (int k = 0; k < 5; ++k) v[11 + k] = stamp[k] >> 4;
 #endif
     (void)stamp;
-    block_counters(part, v, red);
+    block_counters(part, v, red, 8, W.live + W.parity);   // ends with a barrier: qcnt is final
+    if (threadIdx.x < 2) W.rcnt[(W.parity * 2 + threadIdx.x) * W.regions + blockIdx.x] = qcnt[threadIdx.x];
 }
 
-// both queues of one bounce: entries [0, nc) closest hit, [nc, nc + ns) shadow;
-// block 0 also clears the other parity's counters for the next wf_shade
+// both queues of one bounce, region by region: block t works on wf_shade
+// region t / split, entries [0, nc) closest hit then [nc, nc + ns) shadow, in
+// steps of split x 256; block 0 also clears the other parity's live count
 template <bool STATS, bool SCENE_LDS, bool ANA>
 __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunch L, MtsgWave W,
                                                                        unsigned long long *part) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t red[BLOCK / 64 * 16];
     const MtsgDeviceScene &S = L.scene;
-    if (blockIdx.x == 0 && threadIdx.x < 4) W.cnt[(W.parity ^ 1u) * 4 + threadIdx.x] = 0;
-    const uint32_t nc = W.cnt[W.parity * 4 + 0], ns = W.cnt[W.parity * 4 + 1];
-    if (blockIdx.x * BLOCK >= nc + ns) return;   // block-uniform
+    if (blockIdx.x == 0 && threadIdx.x == 0) W.live[W.parity ^ 1u] = 0;
+    const uint32_t region = blockIdx.x / W.split, part0 = blockIdx.x % W.split;
+    if (region >= W.regions) return;
+    const uint32_t nc = W.rcnt[(W.parity * 2 + 0) * W.regions + region];
+    const uint32_t ns = W.rcnt[(W.parity * 2 + 1) * W.regions + region];
+    if (part0 * BLOCK >= nc + ns) return;   // block-uniform
     uint32_t stackBase = 0;
     if (SCENE_LDS && !L.scan) {
         const uint32_t nodeWords = L.num_nodes * 16, triWords = S.num_prims * 12;
@@ -1604,15 +1628,17 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
         stackBase = nodeWords + triWords;
         __syncthreads();
     }
+    const uint32_t K = L.stack_depth < MTSG_WF_LDS_STACK ? L.stack_depth : MTSG_WF_LDS_STACK;
     lds_node *ldsNodes = (lds_node *)__builtin_assume_aligned((const void *)lds, 16);
     lds_tri *ldsTris = (lds_tri *)__builtin_assume_aligned((const void *)(lds + L.num_nodes * 16), 16);
     lds_stk_n *stkN = (lds_stk_n *)(lds + stackBase) + threadIdx.x;
-    lds_stk_d *stkD = (lds_stk_d *)(lds + stackBase + L.stack_depth * BLOCK) + threadIdx.x;
+    lds_stk_d *stkD = (lds_stk_d *)(lds + stackBase + K * BLOCK) + threadIdx.x;
+    uint2 *ovf = W.ovf + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * W.ovf_depth;
     unsigned long long cN = 0, cT = 0;
-    const uint32_t n = nc + ns;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    const uint32_t n = nc + ns, base = region * W.rounds * BLOCK;
+    for (uint32_t i = part0 * BLOCK + threadIdx.x; i < n; i += W.split * BLOCK) {
         const bool shadow = i >= nc;
-        const uint32_t k = shadow ? i - nc : i;
+        const uint32_t k = base + (shadow ? i - nc : i);
         const float4 *q = shadow ? W.sray : W.qray;
         const float4 a = q[2 * (size_t)k], b = q[2 * (size_t)k + 1];
         const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
@@ -1624,22 +1650,24 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
             if (SCENE_LDS && L.scan)
                 occ = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
-                occ = traverse<true, STATS, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht, cN,
-                                                 cT, S.analytic);
+                occ = traverse<true, STATS, ANA, MTSG_WF_LDS_STACK>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD,
+                                                                    slot, hu, hv, ht, cN, cT, S.analytic, ovf);
             else
-                occ = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
-                                                 slot, hu, hv, ht, cN, cT, S.analytic);
+                occ = traverse<true, STATS, ANA, MTSG_WF_LDS_STACK>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint,
+                                                                    maxt, stkN, stkD, slot, hu, hv, ht, cN, cT,
+                                                                    S.analytic, ovf);
             W.occl[k] = occ ? 1u : 0u;
         } else {
             bool hit;
             if (SCENE_LDS && L.scan)
                 hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
-                hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht,
-                                                  cN, cT, S.analytic);
+                hit = traverse<false, STATS, ANA, MTSG_WF_LDS_STACK>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD,
+                                                                     slot, hu, hv, ht, cN, cT, S.analytic, ovf);
             else
-                hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD,
-                                                  slot, hu, hv, ht, cN, cT, S.analytic);
+                hit = traverse<false, STATS, ANA, MTSG_WF_LDS_STACK>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d,
+                                                                     mint, maxt, stkN, stkD, slot, hu, hv, ht, cN, cT,
+                                                                     S.analytic, ovf);
             const uint32_t w = !hit ? MTSG_WF_NONE : ANA ? slot
                              : (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
             W.hit[k] = make_float4(ht, hu, hv, __uint_as_float(w));
@@ -2257,7 +2285,8 @@ size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) {
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
     const bool scan = L.scene_lds && L.scan;
     const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
-    const size_t stack = scan ? 0 : ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2;
+    const size_t K = std::min<size_t>(L.stack_depth, MTSG_WF_LDS_STACK);
+    const size_t stack = scan ? 0 : (K * 3 * BLOCK + 1) / 2;
     return (scene + stack) * 4 + 16;
 }
 
