@@ -211,7 +211,16 @@ typedef struct {
 } mtsgpu_render_params;
 
 enum { MTSGPU_INTEGRATOR_PATH = 0, MTSGPU_INTEGRATOR_DIRECT = 1, MTSGPU_INTEGRATOR_VOLPATH = 2 };
-enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1 };
+enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1,
+       /* the reference's own independent sampler, replayed: SFMT19937 streams
+          (random.cpp) cloned from Random(5489) as RenderJob does
+          (renderjob.cpp:58-66), the crop's 32x32 blocks in BlockedImageProcess's
+          spiral order (imageproc.cpp:43-80) and each block's pixels on its Hilbert
+          curve (sfcurve.h, renderproc.cpp:79-81).  SFMT_REPLAY: one worker renders
+          every block (`mitsuba -p 1`, sequential: for parity, not speed);
+          SFMT_BLOCKS: block k is rendered by clone k (blocks in parallel).
+          Whole crop only (row_stride 1); no direct-integrator sample arrays */
+       MTSGPU_SAMPLER_SFMT_REPLAY = 2, MTSGPU_SAMPLER_SFMT_BLOCKS = 3 };
 
 /* render flags */
 #define MTSGPU_FLAG_TRAVERSAL_STATS 1u  /* count BVH node visits / TriAccel tests   */
@@ -309,6 +318,9 @@ int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4);
    path lengths, node visits, TriAccel tests, dimension errors, hits, -, NEE
    samples, Sobol HBM words, diagnostic section cycles 11-15) */
 int mtsgpu_debug_counters(mtsgpu_ctx *ctx, uint64_t *out16);
+/* n nextULong draws of the device's SFMT19937 (the SFMT replay samplers' generator)
+   from Random(seed), or from the clone-th Random(&master) clone of it */
+int mtsgpu_debug_sfmt(mtsgpu_ctx *ctx, uint64_t seed, int clone, uint64_t *out, int n);
 /* Host-only (no device needed): configure `scene` and return its environment
  * emitter's tables -- params[64] = {levels, w0, h0, normalization, pixel_x,
  * pixel_y, scale, center xyz, radius, total texels, .., lw[l] at 16+l, lh[l] at

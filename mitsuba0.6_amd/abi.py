@@ -21,7 +21,7 @@ SHAPE_TRIMESH, SHAPE_RECTANGLE, SHAPE_DISK, SHAPE_SPHERE = 0, 1, 2, 3
 FOV_X, FOV_Y, FOV_DIAGONAL, FOV_SMALLER, FOV_LARGER = 0, 1, 2, 3, 4
 RFILTER_BOX, RFILTER_GAUSSIAN = 0, 1
 INTEGRATOR_PATH, INTEGRATOR_DIRECT, INTEGRATOR_VOLPATH = 0, 1, 2
-SAMPLER_SOBOL, SAMPLER_INDEPENDENT = 0, 1
+SAMPLER_SOBOL, SAMPLER_INDEPENDENT, SAMPLER_SFMT_REPLAY, SAMPLER_SFMT_BLOCKS = 0, 1, 2, 3
 SAMPLE_RECORD_FLOATS = 8
 PIX_LUMINANCE, PIX_LUMINANCE_ALPHA, PIX_RGB, PIX_RGBA, PIX_XYZ, PIX_XYZA = 0, 1, 2, 3, 4, 5
 COMP_FLOAT16, COMP_FLOAT32, COMP_UINT32 = 0, 1, 2

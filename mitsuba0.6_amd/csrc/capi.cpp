@@ -19,6 +19,7 @@
 #include "../../include/mtsgpu.h"
 #include "layout.h"
 #include "scene_build.h"
+#include "sfmt.h"
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
@@ -34,6 +35,7 @@ hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned
 hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters,
                                 hipStream_t s);
 int mtsg_wf_occupancy(const MtsgLaunch &L, int *shadeBpc, int *traceBpc);
+hipError_t mtsg_launch_sfmt_probe(uint32_t *w, unsigned long long *out, int n, hipStream_t s);
 hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
                                hipStream_t s);
 int mtsg_develop_channels(int pixel_format);
@@ -79,6 +81,7 @@ struct mtsgpu_ctx {
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
     // wavefront pipeline: path slots, ray queues and results, counters
     DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_rcnt, wf_live, wf_ovf, wf_part;
+    DevBuf rp_order, rp_start, rp_sfmt;   // SFMT replay: render order, unit starts, streams
     uint32_t *wf_live_host = nullptr;   // pinned: live-slot counts read back while the pipeline runs
     hipEvent_t wf_ev[8] = {};
     unsigned long long last_counters[16] = {};
@@ -319,6 +322,129 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     return MTSGPU_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The `independent` sampler replay (MTSGPU_SAMPLER_SFMT_*): stream seeding and
+// the reference's render order
+// ---------------------------------------------------------------------------
+static void sfmt_period_certification(uint32_t *w) {   // random.cpp:322-347
+    const uint32_t parity[4] = {0x00000001u, 0x00000000u, 0x00000000u, 0x13c9e684u};
+    uint32_t inner = 0;
+    for (int i = 0; i < 4; ++i) inner ^= w[i] & parity[i];
+    for (int i = 16; i > 0; i >>= 1) inner ^= inner >> i;
+    if (inner & 1) return;
+    for (int i = 0; i < 4; ++i)
+        for (uint32_t work = 1, j = 0; j < 32; ++j, work <<= 1)
+            if (work & parity[i]) { w[i] ^= work; return; }
+}
+
+static void mtsg_sfmt_seed(uint32_t *w, uint64_t seed) {   // init_gen_rand (random.cpp:397-406)
+    uint64_t v = seed;
+    w[0] = (uint32_t)v;
+    w[1] = (uint32_t)(v >> 32);
+    for (int i = 1; i < MTSG_SFMT_N64; ++i) {
+        v = 6364136223846793005ull * (v ^ (v >> 62)) + (uint64_t)i;
+        w[2 * i] = (uint32_t)v;
+        w[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    w[MTSG_SFMT_N32] = MTSG_SFMT_N32;
+    sfmt_period_certification(w);
+}
+
+// Random(Random *parent): init_by_array over 312 of the parent's outputs as
+// 624 little-endian words (random.cpp:408-471, 528-548)
+static void mtsg_sfmt_clone(uint32_t *w, uint32_t *parent) {
+    uint32_t key[MTSG_SFMT_N32];
+    for (int i = 0; i < MTSG_SFMT_N64; ++i) {
+        const uint64_t v = sfmt_next_ulong(parent);
+        key[2 * i] = (uint32_t)v;
+        key[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    const int n = MTSG_SFMT_N32, lag = 11, mid = (n - lag) / 2, len = MTSG_SFMT_N32;
+    auto f1 = [](uint32_t x) { return (x ^ (x >> 27)) * 1664525u; };
+    auto f2 = [](uint32_t x) { return (x ^ (x >> 27)) * 1566083941u; };
+    std::memset(w, 0x8b, MTSG_SFMT_N32 * 4);
+    int count = std::max(len + 1, n);
+    uint32_t r = f1(w[0] ^ w[mid] ^ w[n - 1]);
+    w[mid] += r;
+    r += (uint32_t)len;
+    w[mid + lag] += r;
+    w[0] = r;
+    --count;
+    int i = 1, j = 0;
+    for (; j < count && j < len; ++j, i = (i + 1) % n) {
+        r = f1(w[i] ^ w[(i + mid) % n] ^ w[(i + n - 1) % n]);
+        w[(i + mid) % n] += r;
+        r += key[j] + (uint32_t)i;
+        w[(i + mid + lag) % n] += r;
+        w[i] = r;
+    }
+    for (; j < count; ++j, i = (i + 1) % n) {
+        r = f1(w[i] ^ w[(i + mid) % n] ^ w[(i + n - 1) % n]);
+        w[(i + mid) % n] += r;
+        r += (uint32_t)i;
+        w[(i + mid + lag) % n] += r;
+        w[i] = r;
+    }
+    for (j = 0; j < n; ++j, i = (i + 1) % n) {
+        r = f2(w[i] + w[(i + mid) % n] + w[(i + n - 1) % n]);
+        w[(i + mid) % n] ^= r;
+        r -= (uint32_t)i;
+        w[(i + mid + lag) % n] ^= r;
+        w[i] = r;
+    }
+    w[MTSG_SFMT_N32] = MTSG_SFMT_N32;
+    sfmt_period_certification(w);
+}
+
+namespace {
+// HilbertCurve2D<uint8_t>::generate (core/sfcurve.h): ENorth 0, EEast 1, ESouth 2, EWest 3
+void hilbert(int order, int front, int right, int back, int left, uint8_t pos[2], uint8_t w, uint8_t h, uint32_t bx,
+             uint32_t by, std::vector<uint32_t> &out) {
+    if (order == 0) {
+        if (pos[0] < w && pos[1] < h) out.push_back((bx + pos[0]) | ((by + pos[1]) << 16));
+        return;
+    }
+    auto move = [&](int d) {
+        if (d == 0) pos[1]--; else if (d == 1) pos[0]++; else if (d == 2) pos[1]++; else pos[0]--;
+    };
+    hilbert(order - 1, left, back, right, front, pos, w, h, bx, by, out); move(right);
+    hilbert(order - 1, front, right, back, left, pos, w, h, bx, by, out); move(back);
+    hilbert(order - 1, front, right, back, left, pos, w, h, bx, by, out); move(left);
+    hilbert(order - 1, right, front, left, back, pos, w, h, bx, by, out);
+}
+}  // namespace
+
+// the crop's pixels (x | y << 16, crop-relative) in the reference's order:
+// BlockedImageProcess's spiral (imageproc.cpp:28-80), HilbertCurve2D per block
+// (renderproc.cpp:79-81); blockStart: first pixel of each block, then the count
+static void mtsg_render_order(uint32_t width, uint32_t height, uint32_t bs, std::vector<uint32_t> &order,
+                       std::vector<uint32_t> &blockStart) {
+    const int nbx = (int)std::ceil((float)width / (float)bs), nby = (int)std::ceil((float)height / (float)bs);
+    const int total = nbx * nby;
+    int cx = nbx / 2, cy = nby / 2, dir = 0 /* ERight */, stepsLeft = 1, numSteps = 1;
+    const float invLog2 = 1.0f / (float)std::log((double)2.0f);   // math::fastlog (math.h:193-195)
+    order.clear();
+    blockStart.clear();
+    for (int b = 0; b < total; ++b) {
+        const int bw = std::min<int>((int)width - cx * (int)bs, (int)bs), bh = std::min<int>((int)height - cy * (int)bs, (int)bs);
+        blockStart.push_back((uint32_t)order.size());
+        const int order2 = (int)std::ceil(invLog2 * (float)std::log((double)(float)std::max(bw, bh)));
+        uint8_t pos[2] = {0, 0};
+        hilbert(order2, 0, 1, 2, 3, pos, (uint8_t)bw, (uint8_t)bh, (uint32_t)(cx * (int)bs), (uint32_t)(cy * (int)bs),
+                order);
+        if (b + 1 == total) break;
+        do {
+            if (dir == 0) ++cx; else if (dir == 1) ++cy; else if (dir == 2) --cx; else --cy;
+            if (--stepsLeft == 0) {
+                dir = (dir + 1) % 4;
+                if (dir == 2 || dir == 0) ++numSteps;   // ELeft, ERight
+                stepsLeft = numSteps;
+            }
+        } while (cx < 0 || cy < 0 || cx >= nbx || cy >= nby);
+    }
+    blockStart.push_back((uint32_t)order.size());
+}
+
 static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *film_host, float *film_dev,
                        float *samples_host, hipStream_t stream, mtsgpu_stats *stats) {
     if (!ctx || !P) return MTSGPU_EINVAL;
@@ -382,8 +508,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (!pathLike && !direct) return fail(ctx, MTSGPU_EINVAL, "unknown integrator");
     if (direct && P->emitter_samples + P->bsdf_samples == 0)
         return fail(ctx, MTSGPU_EINVAL, "direct: emitterSamples + bsdfSamples must be positive");
-    if (P->sampler != MTSGPU_SAMPLER_SOBOL && P->sampler != MTSGPU_SAMPLER_INDEPENDENT)
+    if (P->sampler < MTSGPU_SAMPLER_SOBOL || P->sampler > MTSGPU_SAMPLER_SFMT_BLOCKS)
         return fail(ctx, MTSGPU_EINVAL, "unknown sampler");
+    const bool replay = P->sampler == MTSGPU_SAMPLER_SFMT_REPLAY || P->sampler == MTSGPU_SAMPLER_SFMT_BLOCKS;
+    if (replay && (!pathLike || L.row_stride > 1 || P->width > 65535 || P->height > 65535))
+        return fail(ctx, MTSGPU_EINVAL, "SFMT replay: path/volpath over a whole crop window (no row shards)");
     L.sampler = (uint32_t)P->sampler;
     const uint64_t perSampleIdx = direct ? std::max<uint64_t>(1, std::max(P->emitter_samples, P->bsdf_samples)) : 1;
     uint32_t sppBits = 0;
@@ -471,11 +600,35 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
+    if (replay) {
+        // IndependentSampler's Random() = seed(5489); RenderJob clones it per worker in
+        // order (renderjob.cpp:58-66).  Units: one worker over all blocks, or one per block
+        if (chunk < P->spp) return fail(ctx, MTSGPU_EINVAL, "SFMT replay: sampleCount exceeds one chunk");
+        std::vector<uint32_t> order, blockStart;
+        mtsg_render_order(P->width, P->height, MTSG_BLOCK_SIZE, order, blockStart);
+        std::vector<uint32_t> unitStart;
+        if (P->sampler == MTSGPU_SAMPLER_SFMT_BLOCKS) unitStart = blockStart;
+        else unitStart = {0u, (uint32_t)order.size()};
+        const uint32_t units = (uint32_t)unitStart.size() - 1;
+        std::vector<uint32_t> streams((size_t)units * MTSG_SFMT_WORDS, 0u), master(MTSG_SFMT_WORDS, 0u);
+        mtsg_sfmt_seed(master.data(), 5489ull);
+        for (uint32_t u = 0; u < units; ++u) mtsg_sfmt_clone(streams.data() + (size_t)u * MTSG_SFMT_WORDS, master.data());
+        if ((e = upload(ctx->rp_order, order, stream)) != hipSuccess || (e = upload(ctx->rp_start, unitStart, stream)) != hipSuccess ||
+            (e = upload(ctx->rp_sfmt, streams, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)   // the host vectors go out of scope
+            return hip_fail(ctx, e, "replay upload");
+        L.replay = 1;
+        L.units = units;
+        L.order = (const uint32_t *)ctx->rp_order.p;
+        L.unit_start = (const uint32_t *)ctx->rp_start.p;
+        L.sfmt = (uint32_t *)ctx->rp_sfmt.p;
+    }
     // execution engine (same per-sample results): the wavefront pipeline or the megakernel
     bool wave = false;   // default: the megakernel (DESIGN.md 4 has the engine A/B)
     if (const char *env = std::getenv("MTSGPU_ENGINE")) wave = pathLike && std::strcmp(env, "wavefront") == 0;
     if (P->flags & MTSGPU_FLAG_WAVEFRONT) wave = pathLike;
     if (P->flags & MTSGPU_FLAG_MEGAKERNEL) wave = false;
+    if (replay) wave = false;   // one lane per replay unit
     int shadeGrid = 0, traceGrid = 0;
     uint32_t slots = 0;
     if (wave) {
@@ -520,7 +673,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
                                            slots, P->cancel);
             if (rc != MTSGPU_OK) return rc;
         } else {
-            const uint64_t blocksNeeded = (L.num_items + 255) / 256;
+            const uint64_t blocksNeeded = replay ? (L.units + 255) / 256 : (L.num_items + 255) / 256;
             const int grid = (int)std::min<uint64_t>((uint64_t)ctx->num_cus * bpc, std::max<uint64_t>(1, blocksNeeded));
             if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
         }
@@ -627,7 +780,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_qray, &ctx->wf_sray, &ctx->wf_hit,
-                      &ctx->wf_occl, &ctx->wf_rcnt, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->env_grows, &ctx->env_gcols};
+                      &ctx->wf_occl, &ctx->wf_rcnt, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
     for (hipEvent_t &e : ctx->wf_ev)
         if (e) (void)hipEventDestroy(e);
@@ -679,6 +832,29 @@ int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *o
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 32, hipMemcpyDeviceToHost);
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
     return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "arith probe");
+}
+
+// diagnostics: n nextULong draws of the device's SFMT19937 from Random(seed), or
+// from its clone-th Random(&master) clone (host seeding, device generation)
+int mtsgpu_debug_sfmt(mtsgpu_ctx *ctx, uint64_t seed, int clone, uint64_t *out, int n) {
+    if (!ctx || !out || n <= 0 || clone < 0) return MTSGPU_EINVAL;
+    std::vector<uint32_t> master(MTSG_SFMT_WORDS, 0u), child(MTSG_SFMT_WORDS, 0u);
+    mtsg_sfmt_seed(master.data(), seed);
+    for (int k = 0; k < clone; ++k) mtsg_sfmt_clone(child.data(), master.data());
+    const std::vector<uint32_t> &st = clone > 0 ? child : master;
+    uint32_t *dw = nullptr;
+    unsigned long long *dout = nullptr;
+    hipError_t e;
+    (void)hipSetDevice(ctx->device);
+    if ((e = hipMalloc(&dw, MTSG_SFMT_WORDS * 4)) != hipSuccess || (e = hipMalloc(&dout, (size_t)n * 8)) != hipSuccess)
+        return hip_fail(ctx, e, "malloc");
+    e = hipMemcpy(dw, st.data(), MTSG_SFMT_WORDS * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mtsg_launch_sfmt_probe(dw, dout, n, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(dw);
+    (void)hipFree(dout);
+    return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "sfmt probe");
 }
 
 int mtsgpu_debug_counters(mtsgpu_ctx *ctx, uint64_t *out16) {

@@ -81,7 +81,8 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1, MTSG_EMITTER_CONSTANT = 2 };
 enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4 };
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
-enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1 };    // = MTSGPU_SAMPLER_*
+enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
+       MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*
 
 struct MtsgShape {
     int32_t bsdf, emitter, has_normals, has_uv;
@@ -256,6 +257,12 @@ struct MtsgLaunch {
     uint32_t lum_samples, bsdf_samples;
     float weight_lum, weight_bsdf, frac_lum, frac_bsdf;
     uint32_t lum_dim, bsdf_dim, array_end;
+    // the SFMT replay samplers (MTSGPU_SAMPLER_SFMT_*): lane u renders unit u's pixels
+    // order[unit_start[u] .. unit_start[u + 1]) (x | y << 16, crop-relative), all
+    // samples of a pixel in turn, drawing from stream sfmt[u * MTSG_SFMT_WORDS ..]
+    uint32_t replay, units;
+    const uint32_t *order, *unit_start;
+    uint32_t *sfmt;
     float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics)

@@ -27,6 +27,7 @@
 #include "dbsdf.h"
 #include "denv.h"
 #include "layout.h"
+#include "sfmt.h"
 
 #define BLOCK 256
 
@@ -62,7 +63,15 @@ struct SobolCtx {
     glb_u32 *glob;            // [1024][MTSG_NIBBLES][16]
     uint32_t lds_dims, nibbles, scramble;
     bool indep;               // the `independent` sampler: `index` is a stream key
+    bool replay;              // SFMT replay: draws come from the lane's SFMT stream
+    uint32_t *sfmt;           // the streams (lane u: sfmt + u * MTSG_SFMT_WORDS)
 };
+
+// the SFMT replay stream of this lane (MtsgLaunch::sfmt; unit = global lane index)
+typedef __attribute__((address_space(1))) uint32_t glb_w32;
+__device__ __forceinline__ glb_w32 *lane_sfmt(const SobolCtx &C) {
+    return (glb_w32 *)C.sfmt + ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * MTSG_SFMT_WORDS;
+}
 
 // The independent sampler (independent.cpp:82-104): a counter-based stream per
 // (pixel, sample) -- splitmix64-finalised key, one finalised draw per dimension
@@ -657,11 +666,18 @@ struct PathVars {
 };
 
 __device__ __forceinline__ float next1d(const SobolCtx &C, SamplerState &s) {   // sobol.cpp:219-229
+    if (C.replay) { s.dim++; return sfmt_next_float(lane_sfmt(C)); }   // independent.cpp:97-99
     if (s.dim >= MTSG_SOBOL_DIMS && !C.indep) { s.err = true; return 0.0f; }
     return sobol_sample(C, s.sobolIndex, s.dim++);
 }
 __device__ __forceinline__ void next2d(const SobolCtx &C, float resolution, SamplerState &s, int px, int py,
                                        float &u, float &v) {                       // sobol.cpp:231-250
+    if (C.replay) {   // independent.cpp:101-105: value1, then value2
+        u = sfmt_next_float(lane_sfmt(C));
+        v = sfmt_next_float(lane_sfmt(C));
+        s.dim += 2;
+        return;
+    }
     if (s.dim + 1 >= 5 && s.dim < 5) s.dim = 5;   // skip the (empty) array dimensions [5,5)
     if (s.dim + 1 >= MTSG_SOBOL_DIMS && !C.indep) { s.err = true; u = v = 0.0f; return; }
     if (!C.indep && s.dim == 0 && s.sobolIndex != (uint64_t)s.sampleIndex) {
@@ -870,7 +886,9 @@ __device__ __forceinline__ LdsView<SCENE_LDS> stage_lds(const MtsgLaunch &L, uin
     v.SC.lds_dims = L.lds_dims;
     v.SC.nibbles = L.nibbles;
     v.SC.scramble = L.scramble;
-    v.SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
+    v.SC.indep = L.sampler != MTSG_SAMPLER_SOBOL;
+    v.SC.replay = L.replay != 0;
+    v.SC.sfmt = L.sfmt;
     v.stackBase = base2 + sceneWords;
     return v;
 }
@@ -893,12 +911,26 @@ struct PathShader {
     // the renderBlock loop body for item `it` up to Li()'s prologue
     // (integrator.cpp:165-186, path.cpp:119-133); false for a padding pixel
     __device__ __forceinline__ bool start(PathState &st, uint64_t it) const {
-        const MtsgDeviceScene &S = L.scene;
-        SamplerState &smp = st.smp;
-        PathVars &P = st.P;
         const uint32_t jj = (uint32_t)(it / L.num_pixels);
         st.pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
         if (!pixel_of(L, st.pix, st.px, st.py)) return false;
+        begin(st, jj);
+        return true;
+    }
+
+    // the SFMT replay's next sample: crop pixel xy (x | y << 16), sample jj of the chunk
+    __device__ __forceinline__ void start_xy(PathState &st, uint32_t xy, uint32_t jj) const {
+        const uint32_t lx = xy & 0xffffu, ly = xy >> 16;   // row_stride 1: compact row = ly
+        st.px = (int)(L.x0 + lx);
+        st.py = (int)(L.y0 + ly);
+        st.pix = ((ly >> 3) * L.tiles_x + (lx >> 3)) * 64u + (ly & 7u) * 8u + (lx & 7u);   // pixel_of's inverse
+        begin(st, jj);
+    }
+
+    __device__ __forceinline__ void begin(PathState &st, uint32_t jj) const {
+        const MtsgDeviceScene &S = L.scene;
+        SamplerState &smp = st.smp;
+        PathVars &P = st.P;
         const int px = st.px, py = st.py;
         uint32_t &j = st.j;
         float &sx = st.sx, &sy = st.sy;
@@ -942,7 +974,6 @@ struct PathShader {
         primary = true;
         haveShadow = false;
         st.active = true;
-        return true;
     }
 
     // the rest of one bounce, given the step's trace results: returns true
@@ -1285,7 +1316,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    uint64_t item = (uint64_t)xcd_block() * BLOCK + threadIdx.x;
+    uint64_t item = L.replay ? 0 : (uint64_t)xcd_block() * BLOCK + threadIdx.x;
     bool done = false;
     PathState st;
     st.active = false;
@@ -1300,6 +1331,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     while (true) {
         // ---- A: start the next sample
         while (!st.active && !done) {
+            if (L.replay) {   // SFMT replay: this lane's unit, pixel after pixel, in order
+                const uint32_t unit = blockIdx.x * BLOCK + threadIdx.x;
+                if (unit >= L.units) { done = true; break; }
+                const uint32_t k0 = L.unit_start[unit], n = L.unit_start[unit + 1] - k0;
+                if (item >= (uint64_t)n * L.chunk_spp) { done = true; break; }
+                const uint32_t k = k0 + (uint32_t)(item / L.chunk_spp), jj = (uint32_t)(item % L.chunk_spp);
+                ++item;
+                sh.start_xy(st, L.order[k], jj);
+                break;
+            }
             if (item >= L.num_items) { done = true; break; }
             const uint64_t it = item;
             item += lanes;
@@ -1940,6 +1981,8 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
     SC.nibbles = L.nibbles;
     SC.scramble = L.scramble;
     SC.indep = L.sampler == MTSG_SAMPLER_INDEPENDENT;
+    SC.replay = false;   // the SFMT replay renders path / volpath only (capi.cpp)
+    SC.sfmt = nullptr;
     lds_stk_n *stkN = (lds_stk_n *)(lds + base2 + sceneWords) + threadIdx.x;
     lds_stk_d *stkD = (lds_stk_d *)(lds + base2 + sceneWords + L.stack_depth * BLOCK) + threadIdx.x;
     unsigned long long cRays = 0, cShadow = 0, cSamples = 0, cErr = 0, cN = 0, cT = 0;
@@ -2157,6 +2200,17 @@ __global__ void film_reduce(MtsgLaunch L) {
 __global__ void film_finalize(float *__restrict__ own, const float *__restrict__ spill, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) own[i] += spill[i];
+}
+
+// the device's SFMT19937 stream: n nextULong draws from the stream at w (one lane)
+__global__ void sfmt_probe(uint32_t *w, unsigned long long *out, int n) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int i = 0; i < n; ++i) out[i] = sfmt_next_ulong((glb_w32 *)w);
+}
+
+hipError_t mtsg_launch_sfmt_probe(uint32_t *w, unsigned long long *out, int n, hipStream_t s) {
+    hipLaunchKernelGGL(sfmt_probe, dim3(1), dim3(64), 0, s, w, out, n);
+    return hipGetLastError();
 }
 
 // element-wise IEEE checks of the device arithmetic the path relies on

@@ -27,7 +27,7 @@ class MtsgpuError(RuntimeError):
 
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
-           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
+           'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_debug_sfmt', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
            'mtsgpu_trace_rays']
 
 _lib = None
@@ -61,6 +61,7 @@ def load_library(path=None):
     L.mtsgpu_debug_arith.argtypes = [C.c_void_p, P(C.c_float), P(C.c_float), P(C.c_float), C.c_int]
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
     L.mtsgpu_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
+    L.mtsgpu_debug_sfmt.argtypes = [C.c_void_p, C.c_uint64, C.c_int, P(C.c_uint64), C.c_int]
     L.mtsgpu_trace_rays.argtypes = [C.c_void_p, P(C.c_float), C.c_uint32, C.c_int, P(C.c_float), P(C.c_double)]
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
@@ -109,6 +110,12 @@ class Context:
         out = (C.c_uint64 * 16)()
         self._check(self.L.mtsgpu_debug_counters(self.h, out))
         return list(out)
+
+    def debug_sfmt(self, seed, n, clone=0):
+        """n nextULong draws of the device's SFMT19937 from Random(seed) (or its clone-th clone)."""
+        out = np.zeros(n, np.uint64)
+        self._check(self.L.mtsgpu_debug_sfmt(self.h, C.c_uint64(seed), clone, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
+        return out
 
     def scene_info(self):
         info = (C.c_uint32 * 4)()

@@ -28,6 +28,10 @@ def lookup_ior(v):
     return float(v)
 
 
+# sampler plugin names -> MTSGPU_SAMPLER_* (include/mtsgpu.h)
+SAMPLERS = {'sobol': abi.SAMPLER_SOBOL, 'independent': abi.SAMPLER_INDEPENDENT,
+            'independent-sfmt': abi.SAMPLER_SFMT_REPLAY, 'independent-sfmt-blocks': abi.SAMPLER_SFMT_BLOCKS}
+
 @dataclass
 class Checkerboard:
     """`checkerboard` texture (src/textures/checkerboard.cpp) with Texture2D's
@@ -350,11 +354,14 @@ class PathIntegrator:
     hasAlpha: bool = False         # hdrfilm pixelFormat default "rgb" (hdrfilm.cpp:216)
     crop: Optional[tuple] = None   # hdrfilm crop window (x0, y0, w, h) (film.cpp:35-43); None = whole film
     film: Optional['HDRFilm'] = None   # hdrfilm output format (film.py); None = the hdrfilm defaults
-    sampler: str = 'sobol'         # 'sobol' or 'independent' (include/mtsgpu.h: MTSGPU_SAMPLER_*)
+    # 'sobol', 'independent' (counter-based streams), 'independent-sfmt' (the reference's
+    # SFMT19937 stream of a one-worker render, replayed) or 'independent-sfmt-blocks' (one
+    # SFMT clone per 32x32 block): include/mtsgpu.h MTSGPU_SAMPLER_*
+    sampler: str = 'sobol'
 
     def __post_init__(self):
-        if self.sampler not in ('sobol', 'independent'):
-            raise ValueError('sampler "%s" (sobol, independent)' % self.sampler)
+        if self.sampler not in SAMPLERS:
+            raise ValueError('sampler "%s" (%s)' % (self.sampler, ', '.join(SAMPLERS)))
         if self.rrDepth <= 0:
             raise ValueError("'rrDepth' must be set to a value greater than zero!")
         if self.maxDepth <= 0 and self.maxDepth != -1:
@@ -377,7 +384,7 @@ class PathIntegrator:
         p.height = height - y0 if h is None else h
         p.row_block, p.row_stride, p.row_phase = row_block, row_stride, row_phase
         p.integrator = abi.INTEGRATOR_PATH
-        p.sampler = abi.SAMPLER_INDEPENDENT if self.sampler == 'independent' else abi.SAMPLER_SOBOL
+        p.sampler = SAMPLERS[self.sampler]
         return p
 
 

@@ -67,6 +67,9 @@ def lib(variant='strict'):
                                         C.POINTER(C.c_float)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]
+        L.oracle_sfmt_u64.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.c_int, C.c_int]
+        L.oracle_render_order.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                          C.POINTER(C.c_int)]
         rc = L.oracle_sobol_init(m.SOBOL_PARAMS.encode())
         if rc != 0:
             raise RuntimeError('oracle_sobol_init failed: %d' % rc)
@@ -120,3 +123,24 @@ def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row
     if rc != 0:
         raise RuntimeError('oracle_render failed: %d' % rc)
     return film, smp, st.as_dict()
+
+
+def sfmt_u64(seed, n, clone=0):
+    """The first n outputs of the reference's Random(seed)::nextULong (SFMT19937), or
+    of the clone-th Random(&master) made from it (clone >= 1)."""
+    out = np.zeros(n, np.uint64)
+    lib().oracle_sfmt_u64(C.c_uint64(seed), out.ctypes.data_as(C.POINTER(C.c_uint64)), n, clone)
+    return out
+
+
+def render_order(width, height, block=32):
+    """The reference's pixel order over a crop: (pixels (n, 2) int32 relative to the
+    crop, block_start (num_blocks + 1,)) -- spiral blocks, Hilbert pixels."""
+    nb = -(-width // block) * -(-height // block)
+    pts = np.zeros((width * height, 2), np.int32)
+    bs = np.zeros(nb + 1, np.int32)
+    cnt = C.c_int(0)
+    ip = C.POINTER(C.c_int)
+    n = lib().oracle_render_order(width, height, block, pts.ctypes.data_as(ip), bs.ctypes.data_as(ip), C.byref(cnt))
+    assert n == width * height and cnt.value == nb
+    return pts, bs

@@ -447,6 +447,7 @@ typedef struct {
     uint32_t arrayEnd; /* m_arrayEndDim: dims [5, arrayEnd) hold the requested 2D arrays */
     int err;
     int indep;         /* the `independent` sampler (independent.cpp) instead of `sobol` */
+    struct SfmtState *rng;   /* SFMT replay: Random::nextFloat draws of the worker's stream */
 } Sampler;
 
 /* The independent sampler's stream (independent.cpp:82-104).  The reference
@@ -498,12 +499,20 @@ static void sampler_set_index(Sampler *s, uint64_t idx) { /* sobol.cpp:204-217 *
 }
 static void sampler_generate(Sampler *s, int px, int py) { s->px = px; s->py = py; sampler_set_index(s, 0); }
 
+static float sfmt_next_float(struct SfmtState *s);
 static float next1d(Sampler *s) { /* sobol.cpp:219-229; dims [5, arrayEnd) are the arrays' */
+    if (s->rng) { s->dim++; return sfmt_next_float(s->rng); }   /* independent.cpp:97-99 */
     if (s->dim >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
     if (s->dim >= SOBOL_DIMS && !s->indep) { s->err = 1; return 0.0f; }
     return smp_value(s, s->sobolIndex, s->dim++);
 }
 static void next2d(Sampler *s, float *u, float *v) { /* sobol.cpp:231-250 */
+    if (s->rng) {   /* independent.cpp:101-105: value1 then value2 */
+        *u = sfmt_next_float(s->rng);
+        *v = sfmt_next_float(s->rng);
+        s->dim += 2;
+        return;
+    }
     if (s->dim + 1 >= 5 && s->dim < s->arrayEnd) s->dim = s->arrayEnd;
     if (s->dim + 1 >= SOBOL_DIMS && !s->indep) { s->err = 1; *u = *v = 0.0f; return; }
     if (s->indep) {
@@ -527,6 +536,207 @@ static void sampler_array2d(const Sampler *s, uint32_t dim, uint32_t size, uint3
                             : oracle_sobol_lookup(s->logRes, j, (uint32_t)s->px, (uint32_t)s->py, s->scramble);
     *u = smp_value(s, idx, dim);
     *v = smp_value(s, idx, dim + 1);
+}
+
+/* ------------------------------------------------------------------------ */
+/* SFMT19937 (libcore/random.cpp:68-471, the generic (non-SSE) recursion,     */
+/* which the SSE path reproduces) and Random::nextULong / nextFloat /         */
+/* seed(Random *) (random.cpp:524-553, 630-639).  Pinned by the reference's   */
+/* own output vectors (src/tests/test_random.cpp:433-508).                    */
+/* ------------------------------------------------------------------------ */
+#define SFMT_N 156
+#define SFMT_N32 624
+#define SFMT_N64 312
+#define SFMT_POS1 122
+#define SFMT_SL1 18
+#define SFMT_SL2 1
+#define SFMT_SR1 11
+#define SFMT_SR2 1
+static const uint32_t SFMT_MSK[4] = {0xdfffffefu, 0xddfecb7fu, 0xbffaffffu, 0xbffffff6u};
+static const uint32_t SFMT_PARITY[4] = {0x00000001u, 0x00000000u, 0x00000000u, 0x13c9e684u};
+
+typedef struct SfmtState { uint32_t w[SFMT_N32]; int idx; } Sfmt;
+
+/* 128-bit little-endian shifts by `bytes` (random.cpp:139-171) */
+static void sfmt_shift_left(uint32_t out[4], const uint32_t in[4], int bytes) {
+    const uint64_t lo = (uint64_t)in[0] | ((uint64_t)in[1] << 32), hi = (uint64_t)in[2] | ((uint64_t)in[3] << 32);
+    const uint64_t ohi = (hi << (bytes * 8)) | (lo >> (64 - bytes * 8)), olo = lo << (bytes * 8);
+    out[0] = (uint32_t)olo; out[1] = (uint32_t)(olo >> 32); out[2] = (uint32_t)ohi; out[3] = (uint32_t)(ohi >> 32);
+}
+static void sfmt_shift_right(uint32_t out[4], const uint32_t in[4], int bytes) {
+    const uint64_t lo = (uint64_t)in[0] | ((uint64_t)in[1] << 32), hi = (uint64_t)in[2] | ((uint64_t)in[3] << 32);
+    const uint64_t olo = (lo >> (bytes * 8)) | (hi << (64 - bytes * 8)), ohi = hi >> (bytes * 8);
+    out[0] = (uint32_t)olo; out[1] = (uint32_t)(olo >> 32); out[2] = (uint32_t)ohi; out[3] = (uint32_t)(ohi >> 32);
+}
+/* do_recursion (random.cpp:204-219): r = a ^ (a << 8) ^ ((b >> 11) & MSK) ^ (c >> 8) ^ (d << 18) */
+static void sfmt_recursion(uint32_t *r, const uint32_t *a, const uint32_t *b, const uint32_t *c, const uint32_t *d) {
+    uint32_t x[4], y[4];
+    sfmt_shift_left(x, a, SFMT_SL2);
+    sfmt_shift_right(y, c, SFMT_SR2);
+    for (int k = 0; k < 4; ++k) r[k] = a[k] ^ x[k] ^ ((b[k] >> SFMT_SR1) & SFMT_MSK[k]) ^ y[k] ^ (d[k] << SFMT_SL1);
+}
+static void sfmt_gen_all(Sfmt *s) {   /* gen_rand_all (random.cpp:353-390) */
+    uint32_t *r1 = &s->w[4 * (SFMT_N - 2)], *r2 = &s->w[4 * (SFMT_N - 1)];
+    int i;
+    for (i = 0; i < SFMT_N - SFMT_POS1; ++i) {
+        uint32_t r[4];
+        sfmt_recursion(r, &s->w[4 * i], &s->w[4 * (i + SFMT_POS1)], r1, r2);
+        memcpy(&s->w[4 * i], r, sizeof r);
+        r1 = r2; r2 = &s->w[4 * i];
+    }
+    for (; i < SFMT_N; ++i) {
+        uint32_t r[4];
+        sfmt_recursion(r, &s->w[4 * i], &s->w[4 * (i + SFMT_POS1 - SFMT_N)], r1, r2);
+        memcpy(&s->w[4 * i], r, sizeof r);
+        r1 = r2; r2 = &s->w[4 * i];
+    }
+}
+static void sfmt_period_certification(Sfmt *s) {   /* random.cpp:322-347 */
+    uint32_t inner = 0;
+    for (int i = 0; i < 4; ++i) inner ^= s->w[i] & SFMT_PARITY[i];
+    for (int i = 16; i > 0; i >>= 1) inner ^= inner >> i;
+    if (inner & 1) return;
+    for (int i = 0; i < 4; ++i) {
+        uint32_t work = 1;
+        for (int j = 0; j < 32; ++j) {
+            if (work & SFMT_PARITY[i]) { s->w[i] ^= work; return; }
+            work <<= 1;
+        }
+    }
+}
+static void sfmt_init_gen_rand(Sfmt *s, uint64_t seed) {   /* random.cpp:397-406 */
+    uint64_t v = seed;
+    s->w[0] = (uint32_t)v; s->w[1] = (uint32_t)(v >> 32);
+    for (int i = 1; i < SFMT_N64; ++i) {
+        v = 6364136223846793005ull * (v ^ (v >> 62)) + (uint64_t)i;
+        s->w[2 * i] = (uint32_t)v; s->w[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    s->idx = SFMT_N32;
+    sfmt_period_certification(s);
+}
+static uint32_t sfmt_func1(uint32_t x) { return (x ^ (x >> 27)) * 1664525u; }
+static uint32_t sfmt_func2(uint32_t x) { return (x ^ (x >> 27)) * 1566083941u; }
+static void sfmt_init_by_array(Sfmt *s, const uint32_t *key, int len) {   /* random.cpp:408-471 */
+    const int size = SFMT_N32, lag = 11, mid = (size - lag) / 2;
+    uint32_t *p = s->w;
+    memset(p, 0x8b, sizeof s->w);
+    int count = len + 1 > SFMT_N32 ? len + 1 : SFMT_N32;
+    uint32_t r = sfmt_func1(p[0] ^ p[mid] ^ p[SFMT_N32 - 1]);
+    p[mid] += r;
+    r += (uint32_t)len;
+    p[mid + lag] += r;
+    p[0] = r;
+    count--;
+    int i = 1, j = 0;
+    for (; j < count && j < len; j++) {
+        r = sfmt_func1(p[i] ^ p[(i + mid) % SFMT_N32] ^ p[(i + SFMT_N32 - 1) % SFMT_N32]);
+        p[(i + mid) % SFMT_N32] += r;
+        r += key[j] + (uint32_t)i;
+        p[(i + mid + lag) % SFMT_N32] += r;
+        p[i] = r;
+        i = (i + 1) % SFMT_N32;
+    }
+    for (; j < count; j++) {
+        r = sfmt_func1(p[i] ^ p[(i + mid) % SFMT_N32] ^ p[(i + SFMT_N32 - 1) % SFMT_N32]);
+        p[(i + mid) % SFMT_N32] += r;
+        r += (uint32_t)i;
+        p[(i + mid + lag) % SFMT_N32] += r;
+        p[i] = r;
+        i = (i + 1) % SFMT_N32;
+    }
+    for (j = 0; j < SFMT_N32; j++) {
+        r = sfmt_func2(p[i] + p[(i + mid) % SFMT_N32] + p[(i + SFMT_N32 - 1) % SFMT_N32]);
+        p[(i + mid) % SFMT_N32] ^= r;
+        r -= (uint32_t)i;
+        p[(i + mid + lag) % SFMT_N32] ^= r;
+        p[i] = r;
+        i = (i + 1) % SFMT_N32;
+    }
+    s->idx = SFMT_N32;
+    sfmt_period_certification(s);
+}
+static uint64_t sfmt_next64(Sfmt *s) {   /* gen_rand64 (random.cpp:288-297) */
+    if (s->idx >= SFMT_N32) { sfmt_gen_all(s); s->idx = 0; }
+    const uint64_t r = (uint64_t)s->w[s->idx] | ((uint64_t)s->w[s->idx + 1] << 32);
+    s->idx += 2;
+    return r;
+}
+static float sfmt_next_float(struct SfmtState *s) {   /* Random::nextFloat, SINGLE_PRECISION (random.cpp:630-639) */
+    union { uint32_t u; float f; } x;
+    x.u = ((uint32_t)(sfmt_next64(s) & 0xFFFFFFFFull) >> 9) | 0x3f800000u;
+    return x.f - 1.0f;
+}
+/* Random(Random *parent) = seed(parent): 312 of the parent's outputs as the
+ * init_by_array key, little-endian 32-bit words (random.cpp:528-548) */
+static void sfmt_clone(Sfmt *child, Sfmt *parent) {
+    uint32_t key[SFMT_N32];
+    for (int i = 0; i < SFMT_N64; ++i) {
+        const uint64_t v = sfmt_next64(parent);
+        key[2 * i] = (uint32_t)v; key[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    sfmt_init_by_array(child, key, SFMT_N32);
+}
+
+/* test access: the first n outputs of Random(seed), or (clone >= 1) of the
+   clone-th Random(&master) clone of it */
+int oracle_sfmt_u64(uint64_t seed, uint64_t *out, int n, int clone) {
+    Sfmt s, c;
+    sfmt_init_gen_rand(&s, seed);
+    for (int k = 0; k < clone; ++k) sfmt_clone(&c, &s);
+    Sfmt *g = clone > 0 ? &c : &s;
+    for (int i = 0; i < n; ++i) out[i] = sfmt_next64(g);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* The reference's render order, for the SFMT replay samplers:               */
+/* BlockedImageProcess's spiral over blocks (librender/imageproc.cpp:28-80)   */
+/* and each block's pixels along HilbertCurve2D<uint8_t> (core/sfcurve.h,     */
+/* renderproc.cpp:79-81).  out: (x, y) pairs relative to the crop window;     */
+/* block_start[b] = index of block b's first pixel, block_start[total] = n.  */
+/* ------------------------------------------------------------------------ */
+static void hilbert_gen(int order, int front, int right, int back, int left, uint8_t *pos, uint8_t w, uint8_t h,
+                        int bx, int by, int *out, int *n) {
+    if (order == 0) {
+        if (pos[0] < w && pos[1] < h) { out[2 * *n] = bx + pos[0]; out[2 * *n + 1] = by + pos[1]; ++*n; }
+        return;
+    }
+    /* move(dir) in uint8_t arithmetic: ENorth y--, EEast x++, ESouth y++, EWest x-- */
+#define HMOVE(d) do { if ((d) == 0) pos[1]--; else if ((d) == 1) pos[0]++; else if ((d) == 2) pos[1]++; else pos[0]--; } while (0)
+    hilbert_gen(order - 1, left, back, right, front, pos, w, h, bx, by, out, n); HMOVE(right);
+    hilbert_gen(order - 1, front, right, back, left, pos, w, h, bx, by, out, n); HMOVE(back);
+    hilbert_gen(order - 1, front, right, back, left, pos, w, h, bx, by, out, n); HMOVE(left);
+    hilbert_gen(order - 1, right, front, left, back, pos, w, h, bx, by, out, n);
+#undef HMOVE
+}
+int oracle_render_order(int width, int height, int blockSize, int *out, int *block_start, int *num_blocks) {
+    const int nbx = (int)ceilf((float)width / (float)blockSize), nby = (int)ceilf((float)height / (float)blockSize);
+    const int total = nbx * nby;
+    /* EDirection {ERight = 0, EDown, ELeft, EUp} (render/imageproc.h:65-70) */
+    int cx = nbx / 2, cy = nby / 2, dir = 0, stepsLeft = 1, numSteps = 1, n = 0;
+    const float invLog2 = 1.0f / (float)log((double)2.0f);   /* math::fastlog in double (math.h:193-195) */
+    for (int b = 0; b < total; ++b) {
+        const int bw = width - cx * blockSize < blockSize ? width - cx * blockSize : blockSize;
+        const int bh = height - cy * blockSize < blockSize ? height - cy * blockSize : blockSize;
+        block_start[b] = n;
+        const int mx = bw > bh ? bw : bh;
+        const int order = (int)ceilf(invLog2 * (float)log((double)(float)mx));
+        uint8_t pos[2] = {0, 0};
+        /* generate(order, ENorth, EEast, ESouth, EWest): N = 0, E = 1, S = 2, W = 3 */
+        hilbert_gen(order, 0, 1, 2, 3, pos, (uint8_t)bw, (uint8_t)bh, cx * blockSize, cy * blockSize, out, &n);
+        if (b + 1 == total) break;
+        do {
+            if (dir == 0) ++cx; else if (dir == 1) ++cy; else if (dir == 2) --cx; else --cy;
+            if (--stepsLeft == 0) {
+                dir = (dir + 1) % 4;
+                if (dir == 2 || dir == 0) ++numSteps;
+                stepsLeft = numSteps;
+            }
+        } while (cx < 0 || cy < 0 || cx >= nbx || cy >= nby);
+    }
+    block_start[total] = n;
+    *num_blocks = total;
+    return n;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -3366,6 +3576,74 @@ static int film_put(const Filter *f, int W, int H, int px, int py, float sx, flo
 /* ------------------------------------------------------------------------ */
 /* SamplingIntegrator::renderBlock (librender/integrator.cpp:140-188)        */
 /* ------------------------------------------------------------------------ */
+typedef struct {
+    Scene *S;
+    const PathParams *PP;
+    const mtsgpu_render_params *P;
+    int direct;
+    float diffScale;
+    const Filter *F;
+    int W, H, fw, fh;
+    float *film, *spill, *samples;
+} RenderCtx;
+
+/* one pixel's sampleCount samples: sampler->generate(offset), then per sample
+ * next2D + sampleRayDifferential + Li + block->put + advance (integrator.cpp:
+ * 165-186); rng: the SFMT replay stream (NULL: sobol / counter-based streams) */
+static void render_pixel(const RenderCtx *R, long pi, int px, int py, Sfmt *rng, Counters *tot, uint64_t *pathLen,
+                         uint64_t *nsamples, int *err) {
+    const mtsgpu_render_params *P = R->P;
+    Sampler smp;
+    sampler_init(&smp, P->scramble, P->width, P->height);   /* crop size (integrator.cpp:37-41) */
+    smp.indep = P->sampler != MTSGPU_SAMPLER_SOBOL;
+    smp.rng = rng;
+    DirectParams DP;
+    memset(&DP, 0, sizeof DP);
+    if (R->direct) direct_configure(P->emitter_samples, P->bsdf_samples, &DP, &smp); /* configureSampler */
+    sampler_generate(&smp, px, py);
+    Counters C = {0, 0, 0, 0};
+    for (uint32_t j = 0; j < P->spp; ++j) {
+        float ux, uy;
+        next2d(&smp, &ux, &uy);
+        const float sx = (float)px + ux, sy = (float)py + uy;
+        Ray ray;
+        camera_sample_ray(&R->S->cam, sx, sy, &ray);
+        /* sensorRay.scaleDifferential(diffScaleFactor) (integrator.cpp:181, ray.h:163-168) */
+        ray.rxO = vadd(ray.o, vmul(vsub(ray.rxO, ray.o), R->diffScale));
+        ray.ryO = vadd(ray.o, vmul(vsub(ray.ryO, ray.o), R->diffScale));
+        ray.rxD = vadd(ray.d, vmul(vsub(ray.rxD, ray.d), R->diffScale));
+        ray.ryD = vadd(ray.d, vmul(vsub(ray.ryD, ray.d), R->diffScale));
+        float alpha; int depth = 1;
+        V3 L = R->direct ? Li_direct(R->S, R->PP, &DP, ray, &smp, &alpha, &C) : Li(R->S, R->PP, ray, &smp, &alpha, &depth, &C);
+        if (smp.err) *err = 1;
+        *pathLen += (uint64_t)depth; ++*nsamples;
+        float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};
+        film_put(R->F, R->W, R->H, px, py, sx, sy, val5, R->film, R->spill, R->fw, R->fh);
+        if (R->samples) {
+            float *rec = R->samples + ((size_t)pi * P->spp + j) * MTSGPU_SAMPLE_RECORD_FLOATS;
+            rec[0] = L.x; rec[1] = L.y; rec[2] = L.z; rec[3] = alpha;
+            rec[4] = sx; rec[5] = sy; rec[6] = (float)depth; rec[7] = smp.err ? 1.0f : 0.0f;
+        }
+        sampler_set_index(&smp, smp.sampleIndex + 1);
+    }
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    tot->rays += C.rays;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    tot->shadow += C.shadow;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    tot->tests += C.tests;
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+    tot->nodes += C.nodes;
+}
+
 int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
                   float *film, float *samples, mtsgpu_stats *stats, int libm_mode, int threads) {
     if (!g_sobol_ready) return MTSGPU_ESTATE;
@@ -3374,6 +3652,12 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     if (P->integrator != MTSGPU_INTEGRATOR_PATH && P->integrator != MTSGPU_INTEGRATOR_VOLPATH && !direct) return MTSGPU_EINVAL;
     if (P->spp == 0 || (!direct && (P->rr_depth <= 0 || (P->max_depth <= 0 && P->max_depth != -1)))) return MTSGPU_EINVAL;
     if (direct && P->emitter_samples + P->bsdf_samples == 0) return MTSGPU_EINVAL;
+    const int replay = P->sampler == MTSGPU_SAMPLER_SFMT_REPLAY || P->sampler == MTSGPU_SAMPLER_SFMT_BLOCKS;
+    if (P->sampler < MTSGPU_SAMPLER_SOBOL || P->sampler > MTSGPU_SAMPLER_SFMT_BLOCKS) return MTSGPU_EINVAL;
+    /* replay: the whole crop in the reference's block order; no sample arrays
+       (IndependentSampler::generate would draw them per pixel first) */
+    if (replay && (P->row_stride > 1 || direct))   /* path / volpath, as the GPU */
+        return MTSGPU_EINVAL;
     g_cr = libm_mode;
     Scene S;
     int rc = scene_configure(scene, &S);
@@ -3392,63 +3676,51 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     Counters tot = {0, 0, 0, 0};
     uint64_t pathLen = 0, nsamples = 0;
     int err = 0;
-    const float diffScale = 1.0f / sqrtf((float)P->spp);
+    RenderCtx R = {&S, &PP, P, direct, 1.0f / sqrtf((float)P->spp), &F, W, H, fw, fh, film, spill, samples};
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
+#endif
+    if (replay) {
+        /* the scene's IndependentSampler holds Random() = seed(5489) (random.cpp:473-489,
+           random.h:113); RenderJob clones it once per worker in core order (renderjob.cpp:
+           58-66), each clone seeded from the master's next 312 outputs.  SFMT_REPLAY: one
+           worker (`mitsuba -p 1`) renders every block in order; SFMT_BLOCKS: block k of
+           the spiral is rendered by clone k */
+        const int bs = BLOCK_SIZE;
+        const int nb = ((int)P->width + bs - 1) / bs * (((int)P->height + bs - 1) / bs);
+        int *ord = (int *)malloc(sizeof(int) * 2 * (size_t)P->width * P->height);
+        int *bstart = (int *)malloc(sizeof(int) * ((size_t)nb + 1));
+        int nblocks = 0;
+        oracle_render_order((int)P->width, (int)P->height, bs, ord, bstart, &nblocks);
+        const int units = P->sampler == MTSGPU_SAMPLER_SFMT_BLOCKS ? nblocks : 1;
+        Sfmt master;
+        sfmt_init_gen_rand(&master, 5489ull);
+        Sfmt *rngs = (Sfmt *)malloc(sizeof(Sfmt) * (size_t)units);
+        for (int u = 0; u < units; ++u) sfmt_clone(&rngs[u], &master);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : pathLen, nsamples) reduction(| : err)
+#endif
+        for (int u = 0; u < units; ++u) {
+            const int k0 = units == 1 ? 0 : bstart[u], k1 = units == 1 ? bstart[nblocks] : bstart[u + 1];
+            for (int k = k0; k < k1; ++k) {
+                const int lx = ord[2 * k], ly = ord[2 * k + 1];
+                render_pixel(&R, (long)ly * P->width + lx, (int)P->x0 + lx, (int)P->y0 + ly, &rngs[u], &tot, &pathLen,
+                             &nsamples, &err);
+            }
+        }
+        free(rngs);
+        free(bstart);
+        free(ord);
+    } else {
+#ifdef _OPENMP
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : pathLen, nsamples) reduction(| : err)
 #endif
-    for (long pi = 0; pi < (long)P->width * P->height; ++pi) {
-        const int lx = (int)(pi % P->width), ly = (int)(pi / P->width);
-        const int px = (int)P->x0 + lx, py = (int)P->y0 + ly;
-        if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
-        Sampler smp;
-        sampler_init(&smp, P->scramble, P->width, P->height);   /* crop size (integrator.cpp:37-41) */
-        smp.indep = P->sampler == MTSGPU_SAMPLER_INDEPENDENT;
-        DirectParams DP;
-        memset(&DP, 0, sizeof DP);
-        if (direct) direct_configure(P->emitter_samples, P->bsdf_samples, &DP, &smp); /* configureSampler */
-        sampler_generate(&smp, px, py);
-        Counters C = {0, 0, 0, 0};
-        for (uint32_t j = 0; j < P->spp; ++j) {
-            float ux, uy;
-            next2d(&smp, &ux, &uy);
-            const float sx = (float)px + ux, sy = (float)py + uy;
-            Ray ray;
-            camera_sample_ray(&S.cam, sx, sy, &ray);
-            /* sensorRay.scaleDifferential(diffScaleFactor) (integrator.cpp:181, ray.h:163-168) */
-            ray.rxO = vadd(ray.o, vmul(vsub(ray.rxO, ray.o), diffScale));
-            ray.ryO = vadd(ray.o, vmul(vsub(ray.ryO, ray.o), diffScale));
-            ray.rxD = vadd(ray.d, vmul(vsub(ray.rxD, ray.d), diffScale));
-            ray.ryD = vadd(ray.d, vmul(vsub(ray.ryD, ray.d), diffScale));
-            float alpha; int depth = 1;
-            V3 L = direct ? Li_direct(&S, &PP, &DP, ray, &smp, &alpha, &C) : Li(&S, &PP, ray, &smp, &alpha, &depth, &C);
-            if (smp.err) err = 1;
-            pathLen += (uint64_t)depth; nsamples++;
-            float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};
-            film_put(&F, W, H, px, py, sx, sy, val5, film, spill, fw, fh);
-            if (samples) {
-                float *rec = samples + ((size_t)pi * P->spp + j) * MTSGPU_SAMPLE_RECORD_FLOATS;
-                rec[0] = L.x; rec[1] = L.y; rec[2] = L.z; rec[3] = alpha;
-                rec[4] = sx; rec[5] = sy; rec[6] = (float)depth; rec[7] = smp.err ? 1.0f : 0.0f;
-            }
-            sampler_set_index(&smp, smp.sampleIndex + 1);
+        for (long pi = 0; pi < (long)P->width * P->height; ++pi) {
+            const int lx = (int)(pi % P->width), ly = (int)(pi / P->width);
+            const int px = (int)P->x0 + lx, py = (int)P->y0 + ly;
+            if (((uint32_t)(py - (int)P->y0) / rb) % rs != P->row_phase) continue;
+            render_pixel(&R, pi, px, py, NULL, &tot, &pathLen, &nsamples, &err);
         }
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-        tot.rays += C.rays;
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-        tot.shadow += C.shadow;
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-        tot.tests += C.tests;
-#ifdef _OPENMP
-#pragma omp atomic
-#endif
-        tot.nodes += C.nodes;
     }
     for (size_t i = 0; i < filmFloats; ++i) film[i] += spill[i];
     free(spill);

@@ -25,6 +25,12 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *pa
 
 /* Unit-level entry points (tests/) */
 int oracle_sobol_init(const char *joe_kuo_path);
+/* SFMT19937 (random.cpp): the first n outputs of Random(seed), or of its clone-th clone */
+int oracle_sfmt_u64(uint64_t seed, uint64_t *out, int n, int clone);
+/* the reference's render order over a width x height crop: blocks in
+   BlockedImageProcess's spiral, pixels on each block's Hilbert curve;
+   out: 2 ints per pixel, block_start: num_blocks + 1 entries */
+int oracle_render_order(int width, int height, int blockSize, int *out, int *block_start, int *num_blocks);
 float oracle_sobol_sample(uint64_t index, uint32_t dim, uint32_t scramble);
 uint64_t oracle_sobol_lookup(uint32_t m, uint32_t frame, uint32_t px, uint32_t py, uint64_t scramble);
 uint32_t oracle_sobol_matrix(uint32_t dim, uint32_t col);
