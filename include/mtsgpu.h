@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 5
+#define MTSGPU_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -328,6 +328,36 @@ int mtsgpu_debug_sfmt(mtsgpu_ctx *ctx, uint64_t seed, int clone, uint64_t *out, 
  * halves); rows h0+1, cols h0*(w0+1), weights h0 floats (any may be NULL). */
 int mtsgpu_debug_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *texels, size_t texel_cap,
                             float *rows, float *cols, float *weights);
+/* ---- device groups: one render over several GPUs ------------------------
+ * SURVEY.md 8(b)'s `mtsgpu_create(const int *devices, int n, ...)`: a group
+ * holds one context per listed device (a device may be listed twice: two
+ * contexts on one GPU).  mtsgpu_group_render shards the crop window's rows
+ * over the members -- member k renders rows y with ((y - y0) / row_block) % n
+ * == k (row_block = params->row_block, 8 if 0), the interleaved tiles of
+ * BlockedImageProcess (src/librender/imageproc.cpp:28-80) -- one host thread
+ * per member, each into its own HBM film, and merges the films on the first
+ * member's device (peer copies over xGMI, then dst += src in member order:
+ * renderproc.cpp:142-149's Film::put sum; disjoint rows make it exact for the
+ * box filter).  params->row_stride must be 0 or 1 (the group owns the
+ * sharding).  The SFMT replay samplers render on the first member alone (their
+ * streams follow one block order).  Stats are summed, kernel_ms is the
+ * slowest member's. */
+typedef struct mtsgpu_group mtsgpu_group;
+int mtsgpu_group_create(const int *devices, int n, mtsgpu_group **out);
+int mtsgpu_group_size(const mtsgpu_group *group);
+/* Upload the scene to every member (configured once per member, in parallel). */
+int mtsgpu_group_upload_scene(mtsgpu_group *group, const mtsgpu_scene_desc *scene);
+/* Render into `film` (host memory, the mtsgpu_render layout).  Blocking. */
+int mtsgpu_group_render(mtsgpu_group *group, const mtsgpu_render_params *params, float *film, mtsgpu_stats *stats);
+/* The same with the merged film left in HBM on the first member's device
+ * (`film_device`, (W+2b)(H+2b)x5 floats). */
+int mtsgpu_group_render_device(mtsgpu_group *group, const mtsgpu_render_params *params, float *film_device,
+                               mtsgpu_stats *stats);
+/* Member k's context (borrowed; for develop / trace_rays on one device). */
+mtsgpu_ctx *mtsgpu_group_member(mtsgpu_group *group, int k);
+const char *mtsgpu_group_last_error(mtsgpu_group *group);
+void mtsgpu_group_destroy(mtsgpu_group *group);
+
 /* Last error message of this context (or of the last failed create). */
 const char *mtsgpu_last_error(mtsgpu_ctx *ctx);
 void mtsgpu_destroy(mtsgpu_ctx *ctx);

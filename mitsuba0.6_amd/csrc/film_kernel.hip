@@ -133,3 +133,29 @@ hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film
     }
     return hipErrorInvalidValue;
 }
+
+// Film merge of a device group (mtsgpu_group_render): dst += src over the
+// (W+2b)(H+2b)x5 ImageBlock, the Film::put sum of the per-device blocks
+// (renderproc.cpp:142-149).  Streaming float4 pass, HBM-bound: 3 x 4 B per float.
+__global__ __launch_bounds__(256) void film_accumulate(float4 *__restrict__ dst, const float4 *__restrict__ src,
+                                                        size_t n4, float *__restrict__ dtail,
+                                                        const float *__restrict__ stail, uint32_t ntail) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        float4 a = dst[i];
+        const float4 b = src[i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        dst[i] = a;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < ntail) dtail[threadIdx.x] += stail[threadIdx.x];
+}
+
+hipError_t mtsg_launch_film_accumulate(float *dst, const float *src, size_t n, int num_cus, hipStream_t s) {
+    const size_t n4 = n / 4;
+    const uint32_t tail = (uint32_t)(n - 4 * n4);
+    const size_t want = (n4 + 255) / 256, cap = (size_t)std::max(num_cus, 1) * 8;
+    const int grid = (int)std::max<size_t>(1, std::min(want, cap));
+    hipLaunchKernelGGL(film_accumulate, dim3(grid), dim3(256), 0, s, (float4 *)dst, (const float4 *)src, n4,
+                       dst + 4 * n4, src + 4 * n4, tail);
+    return hipGetLastError();
+}

@@ -28,7 +28,9 @@ class MtsgpuError(RuntimeError):
 EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu_render',
            'mtsgpu_render_device', 'mtsgpu_last_error', 'mtsgpu_destroy', 'mtsgpu_abi_version',
            'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_debug_sfmt', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
-           'mtsgpu_trace_rays']
+           'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
+           'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
+           'mtsgpu_group_destroy']
 
 _lib = None
 
@@ -66,6 +68,16 @@ def load_library(path=None):
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
     L.mtsgpu_develop_device.argtypes = [C.c_void_p, P(abi.DevelopParams), C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mtsgpu_group_create.argtypes = [P(C.c_int), C.c_int, P(C.c_void_p)]
+    L.mtsgpu_group_size.argtypes = [C.c_void_p]
+    L.mtsgpu_group_upload_scene.argtypes = [C.c_void_p, P(abi.SceneDesc)]
+    L.mtsgpu_group_render.argtypes = [C.c_void_p, P(abi.RenderParams), P(C.c_float), P(abi.Stats)]
+    L.mtsgpu_group_render_device.argtypes = [C.c_void_p, P(abi.RenderParams), C.c_void_p, P(abi.Stats)]
+    L.mtsgpu_group_member.argtypes = [C.c_void_p, C.c_int]
+    L.mtsgpu_group_member.restype = C.c_void_p
+    L.mtsgpu_group_last_error.argtypes = [C.c_void_p]
+    L.mtsgpu_group_last_error.restype = C.c_char_p
+    L.mtsgpu_group_destroy.argtypes = [C.c_void_p]
     if L.mtsgpu_abi_version() != abi.ABI_VERSION:
         raise NativeUnavailable('ABI version mismatch')
     if path is None:
@@ -204,6 +216,61 @@ class Context:
     def close(self):
         if self.h:
             self.L.mtsgpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceGroup:
+    """One render over several GPUs of this node (mtsgpu_group_*): the library
+    shards the rows over the devices, one host thread each, and merges the films
+    on the first device over xGMI (include/mtsgpu.h).  A device may be listed
+    twice (two contexts on one GPU)."""
+
+    def __init__(self, devices, lib_path=None):
+        self.L = load_library(lib_path)
+        devs = (C.c_int * len(devices))(*devices)
+        h = C.c_void_p()
+        rc = self.L.mtsgpu_group_create(devs, len(devices), C.byref(h))
+        if rc != 0:
+            raise NativeUnavailable('mtsgpu_group_create failed: %s' % self.L.mtsgpu_group_last_error(None).decode())
+        self.h = h
+        self.devices = list(devices)
+        self.scene = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise MtsgpuError(rc, self.L.mtsgpu_group_last_error(self.h).decode())
+
+    def __len__(self):
+        return self.L.mtsgpu_group_size(self.h)
+
+    def upload(self, scene):
+        d = scene.desc()
+        self._check(self.L.mtsgpu_group_upload_scene(self.h, C.byref(d)))
+        self.scene = scene
+
+    def render(self, integ, window=None, engine=None, row_block=8):
+        """Returns (film (H+2b, W+2b, 5) float32, stats dict) of the whole window."""
+        sc = self.scene
+        W, H = sc.sensor.width, sc.sensor.height
+        x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
+        p = integ.params(W, H, x0, y0, w, h, row_block, 1, 0)
+        p.flags |= Context._engine_flags(engine)
+        b = film_border(integ.rfilter, integ.rfilterParam)
+        film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
+        st = abi.Stats()
+        self._check(self.L.mtsgpu_group_render(self.h, C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)),
+                                                C.byref(st)))
+        return film, st.as_dict()
+
+    def close(self):
+        if self.h:
+            self.L.mtsgpu_group_destroy(self.h)
             self.h = None
 
     def __del__(self):

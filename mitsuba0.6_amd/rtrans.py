@@ -6,11 +6,12 @@ BSDF is configured.  This module resolves the same file name, in order:
 
 1. an explicit directory (`BSDF.rtransDir`, or the XML scene's directory),
 2. `$MTSGPU_MICROFACET_DIR`, then `$MITSUBA_DIR/data/microfacet`,
-3. the tables generated in-tree by `tools/rtrans_gen.c` (build() writes them
-   to `mitsuba0.6_amd/_build/microfacet/`).  These follow the reference's
-   generator (src/utils/rdielprec.cpp) with a different quadrature, so they
-   agree with the shipped files only to the tolerance DESIGN.md states; a
-   warning says when they are used.
+3. the tables generated in-tree by `tools/rtrans_nd.c` (build() writes them
+   to `mitsuba0.6_amd/_build/microfacet/`): the reference's generator
+   (src/utils/rdielprec.cpp) with its own adaptive cubature (NDIntegrator,
+   src/libcore/quad.cpp) restated.  They match the shipped files bit for bit
+   in 54-66% of the entries and to 1e-5 in 99% (tests/test_roughplastic_host.py,
+   DESIGN.md 2); a warning says when they are used.
 
 The bytes are handed to the library unchanged (mtsgpu_bsdf_desc.rtrans_data);
 the library parses, checks and reduces them as RoughPlastic::configure does.
@@ -47,7 +48,7 @@ def table_path(distribution, extra_dirs=None):
     if os.path.isfile(gen):
         if name not in _warned:
             _warned.add(name)
-            warnings.warn('roughplastic: using the generated table %s (tools/rtrans_gen.c); point '
+            warnings.warn('roughplastic: using the generated table %s (tools/rtrans_nd.c); point '
                           'MTSGPU_MICROFACET_DIR at Mitsuba\'s data/microfacet for the reference\'s own' % gen)
         return gen
     raise FileNotFoundError('roughplastic: no rough transmittance table data/microfacet/%s (set '

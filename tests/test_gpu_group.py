@@ -1,0 +1,63 @@
+"""Device groups (mtsgpu_group_*): one render call sharded over several GPUs,
+films merged on the first device (include/mtsgpu.h).
+
+A one-GPU box lists device 0 more than once: the members are separate
+contexts with their own films, so the row sharding, the per-member renders on
+parallel host threads and the in-order merge all run as on a node.  Bar: with
+the box filter the merged film equals the single-context film bit for bit
+(disjoint rows, Film::put sums of zeros elsewhere); with the gaussian filter the
+overlapping borders of neighbouring row blocks are summed in another order
+(rtol 2e-6, as the row-shard test of test_gpu_parity.py)."""
+import numpy as np
+import pytest
+
+from mitsuba_amd import scenes
+from mitsuba_amd.integrator import DeviceGroup, MtsgpuError
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('n', [1, 2, 3])
+def test_group_film_equals_single_context(gpu_ctx, n):
+    sc, it = scenes.build('C1', width=96, height=72, spp=8)
+    gpu_ctx.upload(sc)
+    film_1, _, st_1 = gpu_ctx.render(it)
+    g = DeviceGroup([0] * n)
+    assert len(g) == n
+    g.upload(sc)
+    film_g, st_g = g.render(it)
+    assert np.array_equal(film_g.view(np.uint32), film_1.view(np.uint32))
+    for k in ('samples', 'rays', 'shadow_rays', 'path_length_sum'):
+        assert st_g[k] == st_1[k], k
+    g.close()
+
+
+def test_group_gaussian_window_and_row_block(gpu_ctx):
+    sc, it = scenes.build('C1', width=80, height=64, spp=4)
+    it.rfilter = 'gaussian'
+    gpu_ctx.upload(sc)
+    win = (5, 3, 61, 49)
+    film_1, _, _ = gpu_ctx.render(it, window=win)
+    g = DeviceGroup([0, 0])
+    g.upload(sc)
+    for rb in (1, 8, 32):
+        film_g, st = g.render(it, window=win, row_block=rb)
+        np.testing.assert_allclose(film_g, film_1, rtol=2e-6, atol=1e-6)
+        assert st['samples'] == 61 * 49 * 4
+    g.close()
+
+
+def test_group_rejects_row_stride_and_render_before_upload():
+    g = DeviceGroup([0, 0])
+    sc, it = scenes.build('C1', width=16, height=16, spp=1)
+    with pytest.raises(MtsgpuError, match='before upload'):
+        g.render(it)
+    g.upload(sc)
+    import ctypes as C
+    from mitsuba_amd import abi
+    p = it.params(16, 16, 0, 0, 16, 16, 8, 2, 0)
+    film = np.zeros((16, 16, 5), np.float32)
+    rc = g.L.mtsgpu_group_render(g.h, C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)), C.byref(abi.Stats()))
+    assert rc == abi.EINVAL
+    assert b'row_stride' in g.L.mtsgpu_group_last_error(g.h)
+    g.close()

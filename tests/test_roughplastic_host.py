@@ -3,11 +3,12 @@
 stand-in tables against the reference's shipped ones, and the library's
 configure() errors (mtsgpu_check_scene) next to the oracle's.
 
-Pinning: the generator (tools/rtrans_gen.c) is checked against the
-reference's own data/microfacet/*.dat when this container has them (the
-files stay in /root/reference; nothing is copied).  Where the shipped ggx
-table holds exact zeros near total internal reflection, a Monte Carlo
-estimate agrees with the generator, not with the file."""
+Pinning: the generator (tools/rtrans_nd.c, the reference's rdielprec.cpp +
+NDIntegrator restated) is checked against the reference's own
+data/microfacet/*.dat when this container has them (the files stay in
+/root/reference; nothing is copied), and a reduced C5 is rendered by the
+oracle on both tables: that image difference is C5's stated tolerance
+(DESIGN.md 2)."""
 import os
 import struct
 
@@ -43,14 +44,38 @@ def test_generated_tables_layout(name, alphas, amax):
     np.testing.assert_allclose(t[:50, 0, 99], 1 - ((eta - 1) / (eta + 1)) ** 2, rtol=1e-6)
 
 
+# measured: bit-identical entries, |diff| <= 1e-6, p99, max
 @pytest.mark.skipif(not os.path.isdir(REF), reason='reference data not in this container')
-@pytest.mark.parametrize('name,p90,p99', [('beckmann', 2e-4, 2e-3), ('ggx', 1e-3, 2e-2), ('phong', 1e-4, 2e-3)])
-def test_generated_tables_match_reference(name, p90, p99):
+@pytest.mark.parametrize('name,exact,close,p99,dmax', [('beckmann', 0.65, 0.987, 3e-5, 3e-3),
+                                                       ('ggx', 0.60, 0.986, 5e-5, 2e-2),
+                                                       ('phong', 0.54, 0.957, 2e-5, 1e-2)])
+def test_generated_tables_match_reference(name, exact, close, p99, dmax):
     na, ra, a = _load(os.path.join(rtrans.GENERATED_DIR, name + '.dat'))
     nb, rb, b = _load(os.path.join(REF, name + '.dat'))
     assert (na, ra) == (nb, rb)
     d = np.abs(a - b)
-    assert np.percentile(d, 90) < p90 and np.percentile(d, 99) < p99, np.percentile(d, [90, 99])
+    stats = ((d == 0).mean(), (d <= 1e-6).mean(), np.percentile(d, 99), d.max())
+    assert stats[0] > exact and stats[1] > close and stats[2] < p99 and stats[3] < dmax, stats
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason='reference data not in this container')
+def test_c5_image_on_reference_vs_generated_tables(oracle):
+    """C5's tolerance: the same reduced C5 frame, rendered by the oracle on the
+    reference's ggx.dat and on the generated one."""
+    films = []
+    for d in (REF, rtrans.GENERATED_DIR):
+        sc, it = scenes.build('C5', width=64, height=40, spp=16, blob=(24, 16), env_size=(64, 32))
+        for b in sc.bsdfs:
+            if b.type == 'roughplastic':
+                b.rtransDir = d
+        assert any(b.type == 'roughplastic' for b in sc.bsdfs)
+        rtrans._cache.clear()
+        film, _, _ = oracle.render(sc, it, libm_mode=1)
+        films.append(film[..., :3].astype(np.float64))
+    rtrans._cache.clear()
+    ref, gen = films
+    rel_rmse = np.sqrt(np.mean((gen - ref) ** 2)) / np.sqrt(np.mean(ref ** 2))
+    assert rel_rmse < 2e-5, rel_rmse          # measured 9.8e-6 (DESIGN.md 2)
 
 
 def test_table_resolution_order(tmp_path, monkeypatch):
