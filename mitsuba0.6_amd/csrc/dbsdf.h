@@ -815,3 +815,44 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
     r.weight = weight;
     return r;
 }
+
+// Call-site dispatch.  DIFF_ONLY (MTSG_FEAT_DIFF: every BSDF of the scene is
+// diffuse, diffuse.cpp:110-150) evaluates the diffuse lobe inline, so the
+// bounce loop makes no out-of-line calls and writes no callee-saved VGPRs to
+// scratch around them; otherwise the out-of-line functions above are called.
+// (Inlining the diffuse case in front of the calls for every scene cost C3-C5
+// 2-4%: profiles/r02_ab_diffuse_fast.log.)
+template <bool EXT, bool DIFF_ONLY>
+__device__ __forceinline__ f3 bsdf_eval_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if constexpr (DIFF_ONLY) {
+        if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
+        return mul(bsdf_refl<EXT>(b, u, v), D_INV_PI * wo.z);
+    } else {
+        return bsdf_eval<EXT>(b, rt, wi, wo, u, v);
+    }
+}
+template <bool EXT, bool DIFF_ONLY>
+__device__ __forceinline__ float bsdf_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if constexpr (DIFF_ONLY) {
+        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+        return D_INV_PI * wo.z;
+    } else {
+        return bsdf_pdf<EXT>(b, rt, wi, wo, u, v);
+    }
+}
+template <bool EXT, bool DIFF_ONLY>
+__device__ __forceinline__ BSample bsdf_sample_fast(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d,
+                                                    float u, float v) {
+    if constexpr (DIFF_ONLY) {
+        BSample r;
+        r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
+        if (wi.z <= 0) return r;
+        r.wo = square_to_cosine_hemisphere(sx, sy);
+        r.sampledType = MTSG_F_DIFF_REFL;
+        r.pdf = D_INV_PI * r.wo.z;
+        r.weight = bsdf_refl<EXT>(b, u, v);
+        return r;
+    } else {
+        return bsdf_sample<EXT>(b, rt, wi, sx, sy, u1d, u, v);
+    }
+}

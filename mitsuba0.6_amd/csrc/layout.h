@@ -79,7 +79,8 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
 };
 
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1, MTSG_EMITTER_CONSTANT = 2 };
-enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4 };
+enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4,
+       MTSG_FEAT_DIFF = 8 };   // DIFF: every BSDF is diffuse (path megakernel, FEAT 0 scenes only)
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
 enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
        MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*
@@ -248,6 +249,7 @@ struct MtsgLaunch {
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
+    uint32_t all_diffuse;             // kernel variant: every BSDF is diffuse (MTSG_FEAT_DIFF)
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     int32_t integrator;               // MTSGPU_INTEGRATOR_*

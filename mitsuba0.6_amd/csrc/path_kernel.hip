@@ -901,7 +901,7 @@ template <bool INSTR, bool SCENE_LDS, int FEAT>
 struct PathShader {
     static constexpr bool STATS = INSTR;
     static constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
-                          ANA = (FEAT & MTSG_FEAT_ANA) != 0;
+                          ANA = (FEAT & MTSG_FEAT_ANA) != 0, DIFF = (FEAT & MTSG_FEAT_DIFF) != 0;
     const MtsgLaunch &L;
     const HitSrc<SCENE_LDS> &hs;
     const SobolCtx &SC;
@@ -1184,9 +1184,9 @@ struct PathShader {
                                         if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
                                     }
                                 }
-                                const f3 bsdfVal = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                const f3 bsdfVal = bsdf_eval_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
                                 if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                    const float bsdfPdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                    const float bsdfPdf = bsdf_pdf_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
                                     const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
                                     const float weight = pa / (pa + pb);
                                     c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
@@ -1219,11 +1219,11 @@ struct PathShader {
                         const bool flip = P.its.wi.z < 0;
                         f3 qwi = P.its.wi;
                         if (flip) qwi.z = -qwi.z;
-                        bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
+                        bs = bsdf_sample_fast<EXT, DIFF>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
                                               bx2, by2, u1d, P.its.u, P.its.v);
                         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
                     } else {
-                        bs = bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                        bs = bsdf_sample_fast<EXT, DIFF>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
                     }
                     if (!is_zero(bs.weight) && !smp.err) {
                         P.scattered |= bs.sampledType != MTSG_F_NULL;
@@ -1883,8 +1883,8 @@ __device__ __forceinline__ void bsdf_eval_pdf_2s(const MtsgDeviceScene &S, GBsdf
             if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
         }
     }
-    val = bsdf_eval<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
-    if (pdf) *pdf = bsdf_pdf<EXT>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+    val = bsdf_eval_fast<EXT, false>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+    if (pdf) *pdf = bsdf_pdf_fast<EXT, false>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
 }
 template <bool EXT>
 __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsdf &bsdf, const Hit &h, float bx,
@@ -1893,12 +1893,12 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
         const bool flip = h.wi.z < 0;
         f3 qwi = h.wi;
         if (flip) qwi.z = -qwi.z;
-        BSample bs = bsdf_sample<EXT>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
+        BSample bs = bsdf_sample_fast<EXT, false>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
                                       u1d, h.u, h.v);
         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
         return bs;
     }
-    return bsdf_sample<EXT>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
+    return bsdf_sample_fast<EXT, false>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
 }
 
 // direct_kernel's shadow rays: the any-hit traversal as a separate (not
@@ -2282,7 +2282,10 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
         return hipGetLastError();
     }
     switch (mtsg_path_features(L)) {
-        case 0: launch_path<0>(L, grid, instr, stream); break;
+        case 0:
+            if (L.all_diffuse) launch_path<MTSG_FEAT_DIFF>(L, grid, instr, stream);
+            else launch_path<0>(L, grid, instr, stream);
+            break;
         case MTSG_FEAT_ENV: launch_path<MTSG_FEAT_ENV>(L, grid, instr, stream); break;
         case MTSG_FEAT_EXT: launch_path<MTSG_FEAT_EXT>(L, grid, instr, stream); break;
         case MTSG_FEAT_ENV | MTSG_FEAT_EXT: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, instr, stream); break;

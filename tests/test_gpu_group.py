@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from mitsuba_amd import scenes
-from mitsuba_amd.integrator import DeviceGroup, MtsgpuError
+from mitsuba_amd.integrator import DeviceGroup
 
 pytestmark = pytest.mark.gpu
 
@@ -48,16 +48,20 @@ def test_group_gaussian_window_and_row_block(gpu_ctx):
 
 
 def test_group_rejects_row_stride_and_render_before_upload():
-    g = DeviceGroup([0, 0])
-    sc, it = scenes.build('C1', width=16, height=16, spp=1)
-    with pytest.raises(MtsgpuError, match='before upload'):
-        g.render(it)
-    g.upload(sc)
     import ctypes as C
     from mitsuba_amd import abi
-    p = it.params(16, 16, 0, 0, 16, 16, 8, 2, 0)
-    film = np.zeros((16, 16, 5), np.float32)
-    rc = g.L.mtsgpu_group_render(g.h, C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)), C.byref(abi.Stats()))
-    assert rc == abi.EINVAL
+    g = DeviceGroup([0, 0])
+    sc, it = scenes.build('C1', width=16, height=16, spp=1)
+    from mitsuba_amd.scene import film_border
+    b = film_border(it.rfilter, it.rfilterParam)
+    film = np.zeros((16 + 2 * b, 16 + 2 * b, 5), np.float32)    # the (W+2b)(H+2b)x5 layout the library writes
+
+    def call(p):
+        return g.L.mtsgpu_group_render(g.h, C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)), C.byref(abi.Stats()))
+    assert call(it.params(16, 16, 0, 0, 16, 16, 8, 1, 0)) == abi.ESTATE
+    assert b'before upload' in g.L.mtsgpu_group_last_error(g.h)
+    g.upload(sc)
+    assert call(it.params(16, 16, 0, 0, 16, 16, 8, 2, 0)) == abi.EINVAL
     assert b'row_stride' in g.L.mtsgpu_group_last_error(g.h)
+    assert call(it.params(16, 16, 0, 0, 16, 16, 8, 1, 0)) == abi.OK
     g.close()
