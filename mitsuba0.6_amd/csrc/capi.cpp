@@ -543,6 +543,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     // LDS as the rest allows (the others are read through L1/L2)
     L.ext = H.ext ? 1u : 0u;
     L.ana = H.analytic.empty() ? 0u : 1u;
+    // gfx950 has 32 CUs per XCD; the hardware deals workgroups round-robin over
+    // the XCDs of the device (a CPX partition is one XCD: no remap)
+    L.xcds = (uint32_t)std::max(1, ctx->num_cus / 32);
     L.all_diffuse = std::getenv("MTSGPU_NO_DIFF_VARIANT") ? 0u : 1u;
     for (const MtsgBsdf &b : H.bsdfs) L.all_diffuse &= b.type == MTSGPU_BSDF_DIFFUSE ? 1u : 0u;
     // MIDirectIntegrator::configure / configureSampler (direct.cpp:128-143)

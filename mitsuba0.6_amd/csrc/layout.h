@@ -250,6 +250,7 @@ struct MtsgLaunch {
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     uint32_t all_diffuse;             // kernel variant: every BSDF is diffuse (MTSG_FEAT_DIFF)
+    uint32_t xcds;                    // XCDs the device's CUs span (workgroup -> XCD remap; 1: none)
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     int32_t integrator;               // MTSGPU_INTEGRATOR_*

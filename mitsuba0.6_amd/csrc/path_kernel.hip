@@ -131,14 +131,16 @@ __device__ __forceinline__ uint64_t sobol_lookup(const MtsgLookup &L, uint32_t f
 // Renumber them so that XCD x runs the x-th contiguous eighth of the grid: the
 // items (pixels in 8x8 tiles) the lanes of one XCD hold at a time are then
 // neighbours, and their rays share BVH nodes and triangles in that XCD's L2.
-__device__ __forceinline__ uint32_t xcd_block() {
+// `xcds` comes from the host (MtsgLaunch::xcds: CUs / 32 on gfx950, 1 on a
+// CPX partition); no remap when it is 1 or does not divide the grid.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb, uint32_t xcds) {
 #ifdef MTSG_NO_XCD_REMAP
-    return blockIdx.x;
+    return b;
 #else
-    const uint32_t nb = gridDim.x;
-    return (nb % 8u == 0) ? (blockIdx.x % 8u) * (nb / 8u) + blockIdx.x / 8u : blockIdx.x;
+    return (xcds > 1u && nb % xcds == 0) ? (b % xcds) * (nb / xcds) + b / xcds : b;
 #endif
 }
+__device__ __forceinline__ uint32_t xcd_block(uint32_t xcds) { return xcd_remap(blockIdx.x, gridDim.x, xcds); }
 
 struct SamplerState {
     uint64_t sobolIndex;
@@ -1316,7 +1318,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    uint64_t item = L.replay ? 0 : (uint64_t)xcd_block() * BLOCK + threadIdx.x;
+    uint64_t item = L.replay ? 0 : (uint64_t)xcd_block(L.xcds) * BLOCK + threadIdx.x;
     bool done = false;
     PathState st;
     st.active = false;
@@ -1535,9 +1537,9 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
 // megakernel's xcd_block), regenerating as soon as a path ends; flag WF_DONE
 // marks a slot whose items are used up.
 enum { WF_DONE = 128 };
-__device__ __forceinline__ uint64_t wf_lane_index(uint32_t s) {
+__device__ __forceinline__ uint64_t wf_lane_index(uint32_t s, uint32_t xcds) {
     const uint32_t G = gridDim.x, t = s % BLOCK, b = (s / BLOCK) % G, r = s / (BLOCK * G);
-    const uint32_t pb = (G % 8u == 0) ? (b % 8u) * (G / 8u) + b / 8u : b;
+    const uint32_t pb = xcd_remap(b, G, xcds);
     return ((uint64_t)r * G + pb) * BLOCK + t;
 }
 
@@ -1587,7 +1589,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_SHADE_WAVES) void wf_shade(MtsgLaunc
         // regeneration: the slot's next item (static stride, no atomics)
         bool done = (flags & WF_DONE) != 0;
         if (!st.active && !done) {
-            uint64_t it = (ended || was) ? (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots : wf_lane_index(s);
+            uint64_t it = (ended || was) ? (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots : wf_lane_index(s, L.xcds);
             while (true) {
                 if (it >= L.num_items) { done = true; break; }
                 if (sh.start(st, it)) break;
@@ -2026,7 +2028,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
     };
 
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    for (uint64_t it = (uint64_t)xcd_block() * BLOCK + threadIdx.x; it < L.num_items; it += lanes) {
+    for (uint64_t it = (uint64_t)xcd_block(L.xcds) * BLOCK + threadIdx.x; it < L.num_items; it += lanes) {
         const uint32_t jj = (uint32_t)(it / L.num_pixels);
         const uint32_t pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
         int px, py;

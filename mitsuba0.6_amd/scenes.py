@@ -251,12 +251,14 @@ def blob_mesh(nu=236, nv=148, radius=1.0, center=(0.0, 1.0, 0.0), uv=False):
 
 
 def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env_size=(1024, 512),
-               blob=(236, 148), area_light=False, env_weight=1.0, plastic=False):
+               blob=(236, 148), area_light=False, env_weight=1.0, plastic=False, object_mesh=None):
     """Config C3: a ~69k-triangle object in roughconductor GGX alpha=0.1 (copper) on a
     diffuse checker ground, lit only by a 1024x512 environment map.
     plastic=True is config C5: the object in roughplastic GGX whose roughness is a
     checkerboard texture over spherical UVs (alpha 0.05 / 0.3), so every shading
-    point interpolates the 2D (alpha x theta) rough-transmittance slice."""
+    point interpolates the 2D (alpha x theta) rough-transmittance slice.
+    object_mesh: a Mesh (e.g. Mitsuba's data/tests/bunny.ply through ply.load_ply,
+    already in world space) in place of the procedural object."""
     if plastic:
         obj = BSDF('roughplastic', distribution='ggx', diffuseReflectance=(0.2, 0.35, 0.6),
                    alpha=Checkerboard(color0=0.05, color1=0.3, uscale=8.0, vscale=4.0))
@@ -266,7 +268,10 @@ def matpreview(width=1280, height=720, spp=512, rfilter='box', max_depth=-1, env
     g1 = BSDF('diffuse', reflectance=(0.15, 0.15, 0.15))
     bsdfs = [obj, g0, g1]
     meshes = []
-    if plastic:
+    if object_mesh is not None:
+        object_mesh.bsdf = 0
+        meshes.append(object_mesh)
+    elif plastic:
         p, i, tc = blob_mesh(*blob, uv=True)
         meshes.append(Mesh(p, i, texcoords=tc, bsdf=0, name='object'))
     else:

@@ -3,6 +3,7 @@
 #  1. rocprofv3 --kernel-trace --stats of the bench command itself (C2, C3)
 #  2. separate PMC passes FETCH_SIZE / WRITE_SIZE (MI355X_MICROARCH.md "HBM")
 #     over one full frame of each config, for bench.py's roofline.traffic
+#  3. one SQ pass (wave cycles, VALU issue, waits) for bench.py's roofline.valu
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -eu
 OUT=${1:-gpurun_out/prof}
@@ -16,5 +17,9 @@ for cfg in ${CONFIGS:-C2 C3 C4}; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/pmc_${cfg}_$ctr -o pmc --output-format csv \
         -- python3 $ROOT/tools/prof_run.py $cfg 1 1 > $OUT/pmc_${cfg}_$ctr.log 2>&1
   done
+  # wave-cycle budget (VALU issue, waits) over 1/4 of the rows: 8 SQ counters + 1 GRBM
+  timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY \
+      SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d $OUT/pmc_${cfg}_SQ -o pmc \
+      --output-format csv -- python3 $ROOT/tools/prof_run.py $cfg 1 4 > $OUT/pmc_${cfg}_SQ.log 2>&1
 done
 echo done > $OUT/ok

@@ -5,7 +5,12 @@ For each config: the path kernel's per-launch FETCH_SIZE / WRITE_SIZE (KiB, as
 rocprofv3 reports them) and HBM bytes corrected per MI355X_MICROARCH.md: on
 gfx950 FETCH_SIZE counts half the bytes of wide reads (x2), WRITE_SIZE is
 exact.  Writes profiles/<round>_traffic_<cfg>.json and copies the kernel
-stats CSVs of the bench runs."""
+stats CSVs of the bench runs.  From the SQ pass, profiles/<round>_valu_<cfg>.json:
+the wave-cycle budget (SQ_WAVE_CYCLES = ACTIVE_INST_ANY + WAIT_ANY +
+WAIT_INST_ANY, MI355X_MICROARCH.md "rocprofv3 PMC slots"), the VALU issue
+fraction per wave, and VALU-busy per SIMD = 4 x ACTIVE_INST_VALU (quad-cycles)
+/ (SIMDs x GRBM_GUI_ACTIVE / 8): rocprofv3 sums GRBM_GUI_ACTIVE over the 8
+XCDs (it reads 8x the dispatch's duration in shader cycles)."""
 import csv
 import glob
 import json
@@ -54,3 +59,24 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
     log = os.path.join(src, 'bench_%s.log' % cfg)
     if os.path.exists(log):
         shutil.copy(log, os.path.join(prof, '%s_bench_%s.log' % (rnd, cfg)))
+
+SIMDS, XCDS = 256 * 4, 8
+for cfg in ('C2', 'C3', 'C4', 'C5'):
+    base = os.path.join(src, 'pmc_%s_SQ' % cfg, '**', '*counter_collection.csv')
+    names = ['SQ_WAVES', 'SQ_WAVE_CYCLES', 'SQ_ACTIVE_INST_VALU', 'SQ_ACTIVE_INST_ANY', 'SQ_WAIT_ANY',
+             'SQ_WAIT_INST_ANY', 'SQ_INSTS_VALU', 'SQ_BUSY_CYCLES', 'GRBM_GUI_ACTIVE']
+    v = {n: counter(base, n) for n in names}
+    if not all(v.values()):
+        continue
+    c = {n: sum(x) / len(x) for n, x in v.items()}
+    wc = c['SQ_WAVE_CYCLES']
+    out = {'config': cfg, 'kernel': 'path_kernel', 'counters': c,
+           'valu_busy_per_simd': 4 * c['SQ_ACTIVE_INST_VALU'] / (SIMDS * c['GRBM_GUI_ACTIVE'] / XCDS),
+           'valu_issue_frac_per_wave': c['SQ_ACTIVE_INST_VALU'] / wc,
+           'any_issue_frac_per_wave': c['SQ_ACTIVE_INST_ANY'] / wc,
+           'wait_frac_per_wave': c['SQ_WAIT_ANY'] / wc,
+           'issue_stall_frac_per_wave': c['SQ_WAIT_INST_ANY'] / wc,
+           'valu_insts_per_wave': c['SQ_INSTS_VALU'] / max(1.0, c['SQ_WAVES']),
+           'note': '1/4 of the rows (tools/prof_run.py %s 1 4); SQ cycle counters in quad-cycles' % cfg}
+    json.dump(out, open(os.path.join(prof, '%s_valu_%s.json' % (rnd, cfg)), 'w'), indent=1)
+    print(cfg, {k: out[k] for k in out if k.endswith('frac_per_wave') or k.startswith('valu_busy')})
