@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 6
+#define MTSGPU_ABI_VERSION 7
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -309,6 +309,26 @@ int mtsgpu_develop(mtsgpu_ctx *ctx, const mtsgpu_develop_params *params, const f
  * shadow queries write t = 1 (occluded) or 0.  Host buffers; the kernel's
  * device time goes to *kernel_ms if non-NULL. */
 int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow, float *hits, double *kernel_ms);
+/* The same with flags: MTSGPU_TRACE_SHADOW (the occlusion test) and
+ * MTSGPU_TRACE_KDTREE: traverse the reference's own SAH kd-tree, built on the
+ * host as GenericKDTree::buildInternal builds it (gkdtree.h:959-1264; min-max
+ * binning above 65536 primitives, O(n log n) SAH sweep with perfect splits,
+ * retraction) on first use, with SAHKDTree3D::rayIntersectHavran and its
+ * mailbox (sahkdtree3.h:178-308): among exactly tied triangles the one the
+ * reference tests last wins, where the BVH path takes the larger primitive
+ * number.  Triangle scenes only. */
+enum { MTSGPU_TRACE_SHADOW = 1u, MTSGPU_TRACE_KDTREE = 2u };
+int mtsgpu_trace_rays_ex(mtsgpu_ctx *ctx, const float *rays, uint32_t n, uint32_t flags, float *hits,
+                         double *kernel_ms);
+/* The kd-tree of the uploaded scene (built if needed): info8 = {nodes, indices,
+ * inner nodes, leaves, non-empty leaves, retracted splits, pruned primitives,
+ * depth limit}; nodes (2 words each, KDNode layout gkdtree.h:453-601) and
+ * indices are copied when their capacities (in words) suffice. */
+int mtsgpu_debug_kdtree(mtsgpu_ctx *ctx, uint32_t *nodes, size_t node_cap, uint32_t *indices, size_t index_cap,
+                        uint32_t *info8);
+/* Host-only (no device needed): configure `scene` and build its kd-tree, as above. */
+int mtsgpu_kdtree_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *indices,
+                       size_t index_cap, uint32_t *info8, char *msg, size_t cap);
 /* Diagnostics (tests): device arithmetic probe -- for each i, out[8i..8i+7] =
  * {a/b, sqrt|a|, sin a, cos a, acos(clamp a), atan2(a,b), exp(-|a|), a*b+a}
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */

@@ -14,7 +14,8 @@ STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTA
 BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC, BSDF_ROUGHPLASTIC = 0, 1, 2, 3
 BSDF_CONDUCTOR, BSDF_DIELECTRIC, BSDF_PLASTIC, BSDF_TWOSIDED = 4, 5, 6, 7
 TEX_NONE, TEX_CHECKERBOARD = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
+TRACE_SHADOW, TRACE_KDTREE = 1, 2           # mtsgpu_trace_rays_ex flags
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP, EMITTER_CONSTANT = 0, 1, 2
 SHAPE_TRIMESH, SHAPE_RECTANGLE, SHAPE_DISK, SHAPE_SPHERE = 0, 1, 2, 3

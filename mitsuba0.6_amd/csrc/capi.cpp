@@ -20,6 +20,7 @@
 #include "layout.h"
 #include "scene_build.h"
 #include "sfmt.h"
+#include "kdtree.h"
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
@@ -27,6 +28,9 @@ hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStr
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
 hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32_t n, float *out, bool shadow,
                              uint32_t stackDepth, int numCUs, hipStream_t stream);
+hipError_t mtsg_launch_trace_kd(const MtsgDeviceScene &S, const uint32_t *kdNodes, const uint32_t *kdIndices,
+                                const MtsgTri *kdTris, const float *rays, uint32_t n, float *out, bool shadow,
+                                int numCUs, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
 hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
                                 bool instr, hipStream_t s);
@@ -82,6 +86,10 @@ struct mtsgpu_ctx {
     // wavefront pipeline: path slots, ray queues and results, counters
     DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_rcnt, wf_live, wf_ovf, wf_part;
     DevBuf rp_order, rp_start, rp_sfmt;   // SFMT replay: render order, unit starts, streams
+    // the reference's SAH kd-tree (kdtree_build.cpp), built on first use
+    bool kd_built = false;
+    KdTree kd;
+    DevBuf kd_nodes, kd_indices, kd_tris;
     uint32_t *wf_live_host = nullptr;   // pinned: live-slot counts read back while the pipeline runs
     hipEvent_t wf_ev[8] = {};
     unsigned long long last_counters[16] = {};
@@ -170,6 +178,7 @@ int mtsgpu_create(int device, mtsgpu_ctx **out) {
 int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     if (!ctx || !scene) return MTSGPU_EINVAL;
     ctx->have_scene = false;
+    ctx->kd_built = false;
     std::string err;
     int rc = mtsg_configure_scene(scene, ctx->host, err);
     if (rc) return fail(ctx, rc, err);
@@ -779,7 +788,7 @@ const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() :
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    DevBuf *bufs[] = {&ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+    DevBuf *bufs[] = {&ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
@@ -796,11 +805,94 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     delete ctx;
 }
 
+namespace {
+// the kd-tree over the uploaded scene's triangles (global primitive order: the
+// TriAccel slots carry their primitive number), uploaded with TriAccel records
+// in that order; scenes with analytic shapes are not supported here
+// host part: the tree over the configured scene's triangles in global order
+int build_kd_host(const HostScene &H, KdTree &kd, std::vector<MtsgTri> *tg, std::string &err) {
+    if (!H.analytic.empty()) { err = "kd-tree: scenes with analytic shapes are not supported"; return MTSGPU_EINVAL; }
+    const size_t prims = H.tris.size();
+    std::vector<float> P(prims * 9);
+    if (tg) tg->assign(prims, MtsgTri());
+    for (size_t s = 0; s < prims; ++s) {
+        const uint32_t prim = H.tris[s].prim;
+        if (prim >= prims) { err = "kd-tree: primitive numbering"; return MTSGPU_EINVAL; }
+        if (tg) (*tg)[prim] = H.tris[s];
+        for (int v = 0; v < 3; ++v)
+            for (int k = 0; k < 3; ++k)   // prim_vtx is in global primitive order (only the TriAccel slots are in leaf order)
+                P[9 * (size_t)prim + 3 * v + k] = H.positions[3 * (size_t)H.prim_vtx[4 * (size_t)prim + v] + k];
+    }
+    mtsg_build_kdtree(P.data(), (uint32_t)prims, kd, true);
+    return MTSGPU_OK;
+}
+
+void kd_export(const KdTree &K, uint32_t *nodes, size_t node_cap, uint32_t *indices, size_t index_cap, uint32_t *info8) {
+    const uint32_t v[8] = {(uint32_t)(K.nodes.size() / 2), (uint32_t)K.indices.size(), K.stats.inner, K.stats.leaves,
+                           K.stats.nonempty_leaves, K.stats.retracted, K.stats.pruned, K.stats.max_depth};
+    std::memcpy(info8, v, sizeof v);
+    if (nodes && node_cap >= K.nodes.size()) std::memcpy(nodes, K.nodes.data(), K.nodes.size() * 4);
+    if (indices && index_cap >= K.indices.size()) std::memcpy(indices, K.indices.data(), K.indices.size() * 4);
+}
+
+int ensure_kdtree(mtsgpu_ctx *ctx) {
+    if (ctx->kd_built) return MTSGPU_OK;
+    std::vector<MtsgTri> tg;
+    std::string err;
+    int rc = build_kd_host(ctx->host, ctx->kd, &tg, err);
+    if (rc) return fail(ctx, rc, err);
+    (void)hipSetDevice(ctx->device);
+    hipError_t e;
+    if ((e = upload(ctx->kd_nodes, ctx->kd.nodes, ctx->stream)) != hipSuccess ||
+        (e = upload(ctx->kd_indices, ctx->kd.indices, ctx->stream)) != hipSuccess ||
+        (e = upload(ctx->kd_tris, tg, ctx->stream)) != hipSuccess || (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+        return hip_fail(ctx, e, "kd-tree upload");
+    ctx->kd_built = true;
+    return MTSGPU_OK;
+}
+}  // namespace
+
 int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow, float *hits, double *kernel_ms) {
+    return mtsgpu_trace_rays_ex(ctx, rays, n, shadow ? MTSGPU_TRACE_SHADOW : 0u, hits, kernel_ms);
+}
+
+int mtsgpu_debug_kdtree(mtsgpu_ctx *ctx, uint32_t *nodes, size_t node_cap, uint32_t *indices, size_t index_cap,
+                        uint32_t *info8) {
+    if (!ctx || !info8) return MTSGPU_EINVAL;
+    if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "debug_kdtree before upload_scene");
+    int rc = ensure_kdtree(ctx);
+    if (rc) return rc;
+    kd_export(ctx->kd, nodes, node_cap, indices, index_cap, info8);
+    return MTSGPU_OK;
+}
+
+int mtsgpu_kdtree_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *indices,
+                       size_t index_cap, uint32_t *info8, char *msg, size_t cap) {
+    if (!scene || !info8) return MTSGPU_EINVAL;
+    HostScene H;
+    KdTree K;
+    std::string err;
+    int rc = mtsg_configure_scene(scene, H, err);
+    if (!rc) rc = build_kd_host(H, K, nullptr, err);
+    if (msg && cap) {
+        std::strncpy(msg, err.c_str(), cap - 1);
+        msg[cap - 1] = 0;
+    }
+    if (!rc) kd_export(K, nodes, node_cap, indices, index_cap, info8);
+    return rc;
+}
+
+int mtsgpu_trace_rays_ex(mtsgpu_ctx *ctx, const float *rays, uint32_t n, uint32_t flags, float *hits,
+                         double *kernel_ms) {
+    const int shadow = (flags & MTSGPU_TRACE_SHADOW) ? 1 : 0;
     if (!ctx) return MTSGPU_EINVAL;
     if (!ctx->have_scene) return fail(ctx, MTSGPU_ESTATE, "trace_rays before upload_scene");
     if (!rays || !hits) return fail(ctx, MTSGPU_EINVAL, "trace_rays: NULL buffer");
     if (n == 0) return MTSGPU_OK;
+    if (flags & MTSGPU_TRACE_KDTREE) {
+        int rc = ensure_kdtree(ctx);
+        if (rc) return rc;
+    }
     (void)hipSetDevice(ctx->device);
     hipError_t e;
     if ((e = ctx->qrays.ensure((size_t)n * 32)) != hipSuccess || (e = ctx->qhits.ensure((size_t)n * 16)) != hipSuccess)
@@ -808,8 +900,12 @@ int mtsgpu_trace_rays(mtsgpu_ctx *ctx, const float *rays, uint32_t n, int shadow
     hipStream_t s = ctx->stream;
     if ((e = hipMemcpyAsync(ctx->qrays.p, rays, (size_t)n * 32, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipEventRecord(ctx->ev0, s)) != hipSuccess ||
-        (e = mtsg_launch_trace(ctx->dscene, (const float *)ctx->qrays.p, n, (float *)ctx->qhits.p, shadow != 0,
-                               ctx->host.bvh_depth + 2, ctx->num_cus, s)) != hipSuccess ||
+        (e = (flags & MTSGPU_TRACE_KDTREE)
+                 ? mtsg_launch_trace_kd(ctx->dscene, (const uint32_t *)ctx->kd_nodes.p, (const uint32_t *)ctx->kd_indices.p,
+                                        (const MtsgTri *)ctx->kd_tris.p, (const float *)ctx->qrays.p, n,
+                                        (float *)ctx->qhits.p, shadow != 0, ctx->num_cus, s)
+                 : mtsg_launch_trace(ctx->dscene, (const float *)ctx->qrays.p, n, (float *)ctx->qhits.p, shadow != 0,
+                                     ctx->host.bvh_depth + 2, ctx->num_cus, s)) != hipSuccess ||
         (e = hipEventRecord(ctx->ev1, s)) != hipSuccess ||
         (e = hipMemcpyAsync(hits, ctx->qhits.p, (size_t)n * 16, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)

@@ -2173,6 +2173,120 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(MtsgDeviceScene S, 
     }
 }
 
+// The reference's own kd-tree (kdtree_build.cpp) traversed as
+// SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308): entry/exit points on
+// a stack of MTS_KD_MAXDEPTH entries, leaves tested over the global [mint,
+// maxt] with the 8-entry hashed mailbox (:138-152, MTS_KD_MAILBOX_ENABLED),
+// and ShapeKDTree::intersect's TriAccel test (skdtree.h:248-338), which keeps
+// a hit at t == maxt: among exactly tied triangles the last one tested wins,
+// as in the reference.  TriAccel records are in global primitive order.
+// Correctness path (mtsgpu_trace_rays with MTSGPU_TRACE_KDTREE): the stack
+// lives in scratch.
+template <bool ANY>
+__device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
+                            const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
+                            float &bu, float &bv, uint32_t &bprim) {
+    struct Ent { uint32_t node; float t; uint32_t prev; float p[3]; };
+    constexpr uint32_t NONE = 0xffffffffu;
+    Ent stack[48];
+    uint32_t mbox[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mbox[i] = 0xffffffffu;
+    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+    const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
+    uint32_t enPt = 0, exPt = 1;
+    stack[0].t = mint;
+    for (int k = 0; k < 3; ++k) stack[0].p[k] = oa[k] + da[k] * mint;   // ray(mint)
+    stack[1].t = maxt;
+    for (int k = 0; k < 3; ++k) stack[1].p[k] = oa[k] + da[k] * maxt;
+    stack[1].node = NONE;
+    bool found = false;
+    uint32_t node = 0;
+    while (node != NONE) {
+        uint2 n = nodes[node];
+        while (!(n.x & 0x80000000u)) {
+            const float split = __uint_as_float(n.y);
+            const int axis = (int)(n.x & 3u);
+            const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+            uint32_t farChild;
+            if (stack[enPt].p[axis] <= split) {
+                if (stack[exPt].p[axis] <= split) { node = left; n = nodes[node]; continue; }
+                if (stack[enPt].p[axis] == split) { node = left + 1; n = nodes[node]; continue; }
+                node = left;
+                farChild = left + 1;
+            } else {
+                if (split < stack[exPt].p[axis]) { node = left + 1; n = nodes[node]; continue; }
+                farChild = left;
+                node = left + 1;
+            }
+            const float distToSplit = (split - oa[axis]) * rcp[axis];
+            const uint32_t tmp = exPt++;
+            if (exPt == enPt) ++exPt;
+            if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
+            stack[exPt].prev = tmp;
+            stack[exPt].t = distToSplit;
+            stack[exPt].node = farChild;
+            for (int k = 0; k < 3; ++k) stack[exPt].p[k] = oa[k] + da[k] * distToSplit;
+            stack[exPt].p[axis] = split;
+            n = nodes[node];
+        }
+        for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
+            const uint32_t prim = indices[e];
+            if (mbox[prim & 7u] == prim) continue;
+            const MtsgTri &tr = tris[prim];
+            const uint32_t k = tr.k;
+            float o_u, o_v, o_k, d_u, d_v, d_k;
+            if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+            else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+            else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+            // TriAccel::rayIntersect (triaccel.h:92-160) on [mint, maxt]
+            const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
+            if (!(t < mint || t > maxt)) {
+                const float hu = o_u + t * d_u - tr.a_u;
+                const float hv = o_v + t * d_v - tr.a_v;
+                const float u = hv * tr.b_nu + hu * tr.b_nv;
+                const float v = hu * tr.c_nu + hv * tr.c_nv;
+                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                    if (ANY) return true;
+                    maxt = t;
+                    found = true;
+                    bt = t; bu = u; bv = v; bprim = prim;
+                }
+            }
+            mbox[prim & 7u] = prim;
+        }
+        if (stack[exPt].t > maxt) break;
+        enPt = exPt;
+        node = stack[exPt].node;
+        exPt = stack[enPt].prev;
+    }
+    return found;
+}
+
+template <bool ANY>
+__global__ __launch_bounds__(BLOCK) void trace_kd_kernel(MtsgDeviceScene S, const uint2 *__restrict__ kdNodes,
+                                                         const uint32_t *__restrict__ kdIndices,
+                                                         const MtsgTri *__restrict__ kdTris,
+                                                         const float4 *__restrict__ rays, uint32_t n,
+                                                         float4 *__restrict__ out) {
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+        const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];
+        const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
+        float4 r = make_float4(INFINITY, 0.0f, 0.0f, __uint_as_float(0xffffffffu));
+        float mint, maxt;
+        if (ray_interval(S, o, d, a.w, b.w, ANY, mint, maxt)) {
+            float t = 0, u = 0, v = 0;
+            uint32_t prim = 0;
+            const bool hit = kd_traverse<ANY>(kdNodes, kdIndices, kdTris, o, d, mint, maxt, t, u, v, prim);
+            if (ANY) r.x = hit ? 1.0f : 0.0f;
+            else if (hit) r = make_float4(t, u, v, __uint_as_float(prim));
+        } else if (ANY) {
+            r.x = 0.0f;
+        }
+        out[i] = r;
+    }
+}
+
 // per-pixel ordered sum of the own-pixel splats: film_own[p] (+)= c[0] + c[1] + ...
 // in sample order -- the reference's `*dest++ += weight * value[k]` sequence
 __global__ void film_reduce(MtsgLaunch L) {
@@ -2325,6 +2439,20 @@ hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32
     if (shadow) { if (ana) MTSG_TRACE(true, true); else MTSG_TRACE(true, false); }
     else { if (ana) MTSG_TRACE(false, true); else MTSG_TRACE(false, false); }
 #undef MTSG_TRACE
+    return hipGetLastError();
+}
+
+hipError_t mtsg_launch_trace_kd(const MtsgDeviceScene &S, const uint32_t *kdNodes, const uint32_t *kdIndices,
+                                const MtsgTri *kdTris, const float *rays, uint32_t n, float *out, bool shadow,
+                                int numCUs, hipStream_t stream) {
+    const uint32_t want = (n + BLOCK - 1) / BLOCK;
+    const int grid = (int)std::max<uint32_t>(1, std::min<uint32_t>(want, (uint32_t)(4 * numCUs)));
+    if (shadow)
+        hipLaunchKernelGGL(trace_kd_kernel<true>, dim3(grid), dim3(BLOCK), 0, stream, S, (const uint2 *)kdNodes,
+                           kdIndices, kdTris, (const float4 *)rays, n, (float4 *)out);
+    else
+        hipLaunchKernelGGL(trace_kd_kernel<false>, dim3(grid), dim3(BLOCK), 0, stream, S, (const uint2 *)kdNodes,
+                           kdIndices, kdTris, (const float4 *)rays, n, (float4 *)out);
     return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_debug_sfmt', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
            'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
-           'mtsgpu_group_destroy']
+           'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host']
 
 _lib = None
 
@@ -68,6 +68,10 @@ def load_library(path=None):
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
     L.mtsgpu_develop_device.argtypes = [C.c_void_p, P(abi.DevelopParams), C.c_void_p, C.c_void_p, C.c_void_p]
+    L.mtsgpu_trace_rays_ex.argtypes = [C.c_void_p, P(C.c_float), C.c_uint32, C.c_uint32, P(C.c_float), P(C.c_double)]
+    L.mtsgpu_debug_kdtree.argtypes = [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_size_t, P(C.c_uint32)]
+    L.mtsgpu_kdtree_host.argtypes = [P(abi.SceneDesc), P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_size_t,
+                                     P(C.c_uint32), C.c_char_p, C.c_size_t]
     L.mtsgpu_group_create.argtypes = [P(C.c_int), C.c_int, P(C.c_void_p)]
     L.mtsgpu_group_size.argtypes = [C.c_void_p]
     L.mtsgpu_group_upload_scene.argtypes = [C.c_void_p, P(abi.SceneDesc)]
@@ -94,6 +98,29 @@ def check_scene(scene):
     rc = L.mtsgpu_check_scene(C.byref(d), buf, 1024)
     if rc != 0:
         raise MtsgpuError(rc, buf.value.decode())
+
+
+KD_KEYS = ('nodes', 'indices', 'inner', 'leaves', 'nonempty_leaves', 'retracted', 'pruned', 'max_depth')
+
+
+def kdtree_host(scene):
+    """The reference's SAH kd-tree of `scene`, built on the host without a device
+    (mtsgpu_kdtree_host): (nodes (N, 2) uint32 KDNode words, indices, info dict)."""
+    L = load_library()
+    d = scene.desc()
+    info = (C.c_uint32 * 8)()
+    buf = C.create_string_buffer(512)
+    rc = L.mtsgpu_kdtree_host(C.byref(d), None, 0, None, 0, info, buf, 512)
+    if rc != 0:
+        raise MtsgpuError(rc, buf.value.decode())
+    nodes = np.zeros((info[0], 2), np.uint32)
+    idx = np.zeros(max(1, info[1]), np.uint32)
+    up = C.POINTER(C.c_uint32)
+    rc = L.mtsgpu_kdtree_host(C.byref(d), nodes.ctypes.data_as(up), nodes.size, idx.ctypes.data_as(up), idx.size,
+                              info, buf, 512)
+    if rc != 0:
+        raise MtsgpuError(rc, buf.value.decode())
+    return nodes, idx[:info[1]], dict(zip(KD_KEYS, list(info)))
 
 
 class Context:
@@ -192,9 +219,22 @@ class Context:
         self._check(self.L.mtsgpu_develop_device(self.h, C.byref(p), C.c_void_p(film_ptr), C.c_void_p(out_ptr),
                                                   C.c_void_p(stream_ptr) if stream_ptr else None))
 
-    def trace_rays(self, o, d, mint=1e-4, maxt=np.inf, shadow=False):
+    def kdtree(self):
+        """The reference's SAH kd-tree of the uploaded scene (mtsgpu_debug_kdtree):
+        (nodes (N, 2) uint32 KDNode words, indices uint32, info dict)."""
+        info = (C.c_uint32 * 8)()
+        self._check(self.L.mtsgpu_debug_kdtree(self.h, None, 0, None, 0, info))
+        nodes = np.zeros((info[0], 2), np.uint32)
+        idx = np.zeros(max(1, info[1]), np.uint32)
+        up = C.POINTER(C.c_uint32)
+        self._check(self.L.mtsgpu_debug_kdtree(self.h, nodes.ctypes.data_as(up), nodes.size, idx.ctypes.data_as(up),
+                                               idx.size, info))
+        return nodes, idx[:info[1]], dict(zip(KD_KEYS, list(info)))
+
+    def trace_rays(self, o, d, mint=1e-4, maxt=np.inf, shadow=False, kdtree=False):
         """Scene::rayIntersect (shadow=False) / occlusion (shadow=True) for a batch of
-        rays: o, d (n, 3); mint, maxt scalars or (n,).  Returns (hits (n, 4) float32
+        rays: o, d (n, 3); mint, maxt scalars or (n,).  kdtree=True traverses the
+        reference's own kd-tree (MTSGPU_TRACE_KDTREE).  Returns (hits (n, 4) float32
         {t, u, v, prim bits}, kernel ms)."""
         o = np.asarray(o, np.float32).reshape(-1, 3)
         d = np.asarray(d, np.float32).reshape(-1, 3)
@@ -203,7 +243,8 @@ class Context:
         rays[:, 0:3], rays[:, 3], rays[:, 4:7], rays[:, 7] = o, mint, d, maxt
         hits = np.empty((n, 4), np.float32)
         ms = C.c_double()
-        self._check(self.L.mtsgpu_trace_rays(self.h, abi.fptr(rays), n, int(shadow), abi.fptr(hits), C.byref(ms)))
+        flags = (abi.TRACE_SHADOW if shadow else 0) | (abi.TRACE_KDTREE if kdtree else 0)
+        self._check(self.L.mtsgpu_trace_rays_ex(self.h, abi.fptr(rays), n, flags, abi.fptr(hits), C.byref(ms)))
         return hits, ms.value
 
     def debug_arith(self, a, b):

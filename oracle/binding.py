@@ -65,6 +65,8 @@ def lib(variant='strict'):
         L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
         L.oracle_trace_rays.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.c_uint32, C.c_int,
                                         C.POINTER(C.c_float)]
+        L.oracle_trace_rays_kd.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                           C.POINTER(C.c_float), C.c_uint32, C.c_int, C.POINTER(C.c_float)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]
         L.oracle_sfmt_u64.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.c_int, C.c_int]
@@ -92,6 +94,26 @@ def trace_rays(scene, o, d, mint=1e-4, maxt=np.inf, shadow=False):
     rc = lib().oracle_trace_rays(C.byref(desc), rays.ctypes.data_as(fp), n, int(shadow), hits.ctypes.data_as(fp))
     if rc != 0:
         raise RuntimeError('oracle_trace_rays failed: %d' % rc)
+    return hits
+
+
+def trace_rays_kd(scene, nodes, indices, o, d, mint=1e-4, maxt=np.inf, shadow=False):
+    """The same batch over a given kd-tree (KDNode words `nodes`, primitive lists
+    `indices`) with SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308)."""
+    o = np.asarray(o, np.float32).reshape(-1, 3)
+    d = np.asarray(d, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    rays = np.empty((n, 8), np.float32)
+    rays[:, 0:3], rays[:, 3], rays[:, 4:7], rays[:, 7] = o, mint, d, maxt
+    hits = np.empty((n, 4), np.float32)
+    nodes = np.ascontiguousarray(nodes, np.uint32)
+    indices = np.ascontiguousarray(indices, np.uint32)
+    desc = scene.desc()
+    fp, up = C.POINTER(C.c_float), C.POINTER(C.c_uint32)
+    rc = lib().oracle_trace_rays_kd(C.byref(desc), nodes.ctypes.data_as(up), indices.ctypes.data_as(up),
+                                    rays.ctypes.data_as(fp), n, int(shadow), hits.ctypes.data_as(fp))
+    if rc != 0:
+        raise RuntimeError('oracle_trace_rays_kd failed: %d' % rc)
     return hits
 
 

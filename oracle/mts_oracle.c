@@ -3900,6 +3900,118 @@ int oracle_trace_rays(const mtsgpu_scene_desc *scene, const float *rays, uint32_
     return MTSGPU_OK;
 }
 
+/* SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308) over a given kd-tree
+ * (KDNode words, gkdtree.h:453-601; the product's builder exports it through
+ * mtsgpu_debug_kdtree), with the 8-entry hashed mailbox (:138-152) and
+ * ShapeKDTree::intersect's TriAccel test on the global [mint, maxt] (a hit at
+ * t == maxt is kept: the last of exactly tied triangles wins). */
+static int kd_havran(const Scene *S, const uint32_t *nodes, const uint32_t *indices, const Ray *ray, float mint,
+                     float maxt, int shadow, uint32_t *prim, float *tu, float *tv, float *tt) {
+    typedef struct { uint32_t node; float t; uint32_t prev; float p[3]; } Ent;
+    Ent stack[48];
+    uint32_t mbox[8];
+    memset(mbox, 0xFF, sizeof mbox);
+    const float oa[3] = {ray->o.x, ray->o.y, ray->o.z}, da[3] = {ray->d.x, ray->d.y, ray->d.z};
+    const float rcp[3] = {ray->dRcp.x, ray->dRcp.y, ray->dRcp.z};
+    uint32_t enPt = 0, exPt = 1;
+    stack[0].t = mint;
+    for (int k = 0; k < 3; ++k) stack[0].p[k] = oa[k] + da[k] * mint;
+    stack[1].t = maxt;
+    for (int k = 0; k < 3; ++k) stack[1].p[k] = oa[k] + da[k] * maxt;
+    stack[1].node = 0xffffffffu;
+    int found = 0;
+    uint32_t node = 0;
+    while (node != 0xffffffffu) {
+        while (!(nodes[2 * node] & 0x80000000u)) {
+            const uint32_t comb = nodes[2 * node];
+            float split;
+            memcpy(&split, &nodes[2 * node + 1], 4);
+            const int axis = (int)(comb & 3u);
+            const uint32_t left = node + ((comb & ~(3u | 0x40000000u)) >> 2);
+            uint32_t farChild;
+            if (stack[enPt].p[axis] <= split) {
+                if (stack[exPt].p[axis] <= split) { node = left; continue; }
+                if (stack[enPt].p[axis] == split) { node = left + 1; continue; }
+                node = left;
+                farChild = left + 1;
+            } else {
+                if (split < stack[exPt].p[axis]) { node = left + 1; continue; }
+                farChild = left;
+                node = left + 1;
+            }
+            const float distToSplit = (split - oa[axis]) * rcp[axis];
+            const uint32_t tmp = exPt++;
+            if (exPt == enPt) ++exPt;
+            if (exPt >= 48) return found;
+            stack[exPt].prev = tmp;
+            stack[exPt].t = distToSplit;
+            stack[exPt].node = farChild;
+            for (int k = 0; k < 3; ++k) stack[exPt].p[k] = oa[k] + da[k] * distToSplit;
+            stack[exPt].p[axis] = split;
+        }
+        for (uint32_t e = nodes[2 * node] & 0x7fffffffu; e != nodes[2 * node + 1]; ++e) {
+            const uint32_t p = indices[e];
+            if (mbox[p & 7u] == p) continue;
+            float u, v, t;
+            if (triaccel_intersect(&S->ta[p], ray, mint, maxt, &u, &v, &t)) {
+                if (shadow) return 1;
+                maxt = t;
+                found = 1;
+                *prim = p; *tu = u; *tv = v; *tt = t;
+            }
+            mbox[p & 7u] = p;
+        }
+        if (stack[exPt].t > maxt) break;
+        enPt = exPt;
+        node = stack[exPt].node;
+        exPt = stack[enPt].prev;
+    }
+    return found;
+}
+
+/* oracle_trace_rays over a given kd-tree (ShapeKDTree::rayIntersect: scene
+ * clip + adaptive epsilon as scene_intersect / scene_occluded, then Havran) */
+int oracle_trace_rays_kd(const mtsgpu_scene_desc *scene, const uint32_t *nodes, const uint32_t *indices,
+                         const float *rays, uint32_t n, int shadow, float *hits) {
+    Scene S;
+    int rc = scene_configure(scene, &S);
+    if (rc) { scene_free(&S); return rc; }
+    #pragma omp parallel for schedule(dynamic, 256)
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        const float *r = rays + 8 * i;
+        Ray ray;
+        memset(&ray, 0, sizeof ray);
+        ray.o = v3(r[0], r[1], r[2]);
+        ray_set_dir(&ray, v3(r[4], r[5], r[6]));
+        ray.mint = r[3]; ray.maxt = r[7];
+        float *h = hits + 4 * i;
+        uint32_t prim = 0xffffffffu;
+        float mint, maxt, u = 0, v = 0, t = INFINITY;
+        int hit = 0;
+        if (aabb_ray(S.aabbMin, S.aabbMax, &ray, &mint, &maxt)) {
+            float rayMinT = ray.mint;
+            if (rayMinT == EPSILON)
+                rayMinT *= shadow ? smax(smax(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z))
+                                  : smax(smax(smax(fabsf(ray.o.x), fabsf(ray.o.y)), fabsf(ray.o.z)), EPSILON);
+            if (rayMinT > mint) mint = rayMinT;
+            if (ray.maxt < maxt) maxt = ray.maxt;
+            if (maxt > mint) hit = kd_havran(&S, nodes, indices, &ray, mint, maxt, shadow, &prim, &u, &v, &t);
+        }
+        if (shadow) {
+            h[0] = hit ? 1.0f : 0.0f; h[1] = h[2] = 0.0f;
+            prim = 0xffffffffu;
+        } else if (hit) {
+            h[0] = t; h[1] = u; h[2] = v;
+        } else {
+            h[0] = INFINITY; h[1] = h[2] = 0.0f;
+            prim = 0xffffffffu;
+        }
+        memcpy(&h[3], &prim, 4);
+    }
+    scene_free(&S);
+    return MTSGPU_OK;
+}
+
 int oracle_intersect(const mtsgpu_scene_desc *scene, const float *o, const float *d, float *out16) {
     Scene S;
     int rc = scene_configure(scene, &S);
