@@ -229,6 +229,11 @@ enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1,
    neither flag: the library's per-scene default */
 #define MTSGPU_FLAG_WAVEFRONT 2u
 #define MTSGPU_FLAG_MEGAKERNEL 4u
+/* trace every ray through the reference's own SAH kd-tree (see
+   mtsgpu_trace_rays_ex) instead of the BVH: exact-t ties then resolve as in
+   the reference (the triangle tested last wins); runs in the wavefront engine,
+   path / volpath, triangle scenes only */
+#define MTSGPU_FLAG_KDTREE 8u
 
 /* Film layout produced by mtsgpu_render: an ImageBlock of the full crop
  * (film_width+2b) x (film_height+2b) pixels, 5 floats each {R,G,B,alpha,w},

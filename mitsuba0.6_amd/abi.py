@@ -92,6 +92,7 @@ class RenderParams(C.Structure):
 FLAG_TRAVERSAL_STATS = 1
 FLAG_WAVEFRONT = 2
 FLAG_MEGAKERNEL = 4
+FLAG_KDTREE = 8                          # trace through the reference's kd-tree (wavefront engine)
 
 
 class DevelopParams(C.Structure):

@@ -97,6 +97,8 @@ struct mtsgpu_ctx {
 
 namespace {
 
+int ensure_kdtree(mtsgpu_ctx *ctx);   // the reference's SAH kd-tree, built on first use (below)
+
 int fail(mtsgpu_ctx *ctx, int code, const std::string &msg) {
     if (ctx) ctx->err = msg;
     return code;
@@ -643,6 +645,18 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     if (P->flags & MTSGPU_FLAG_WAVEFRONT) wave = pathLike;
     if (P->flags & MTSGPU_FLAG_MEGAKERNEL) wave = false;
     if (replay) wave = false;   // one lane per replay unit
+    if (P->flags & MTSGPU_FLAG_KDTREE) {
+        // the reference's own kd-tree: the wavefront engine with wf_trace_kd
+        if (!pathLike || replay)
+            return fail(ctx, MTSGPU_EINVAL, "kd-tree traversal: path / volpath with the sobol or independent sampler");
+        if (P->flags & MTSGPU_FLAG_MEGAKERNEL) return fail(ctx, MTSGPU_EINVAL, "kd-tree traversal runs in the wavefront engine");
+        const int rc = ensure_kdtree(ctx);
+        if (rc) return rc;
+        wave = true;
+        L.kd_nodes = (const uint32_t *)ctx->kd_nodes.p;
+        L.kd_indices = (const uint32_t *)ctx->kd_indices.p;
+        L.kd_tris = (const MtsgTri *)ctx->kd_tris.p;
+    }
     int shadeGrid = 0, traceGrid = 0;
     uint32_t slots = 0;
     if (wave) {

@@ -251,6 +251,10 @@ struct MtsgLaunch {
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     uint32_t all_diffuse;             // kernel variant: every BSDF is diffuse (MTSG_FEAT_DIFF)
     uint32_t xcds;                    // XCDs the device's CUs span (workgroup -> XCD remap; 1: none)
+    // MTSGPU_FLAG_KDTREE (wavefront engine): wf_trace traverses the reference's kd-tree
+    const uint32_t *kd_nodes;         // KDNode words (2 per node), null: the BVH
+    const uint32_t *kd_indices;
+    const MtsgTri *kd_tris;           // TriAccel records in global primitive order
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     int32_t integrator;               // MTSGPU_INTEGRATOR_*

@@ -497,6 +497,96 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
     return true;
 }
 
+// The reference's own kd-tree (kdtree_build.cpp) traversed as
+// SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308): entry/exit points on
+// a stack of MTS_KD_MAXDEPTH entries, leaves tested over the global [mint,
+// maxt] with the 8-entry hashed mailbox (:138-152, MTS_KD_MAILBOX_ENABLED),
+// and ShapeKDTree::intersect's TriAccel test (skdtree.h:248-338), which keeps
+// a hit at t == maxt: among exactly tied triangles the last one tested wins,
+// as in the reference.  TriAccel records are in global primitive order.
+// Correctness path (mtsgpu_trace_rays with MTSGPU_TRACE_KDTREE): the stack
+// lives in scratch.
+template <bool ANY>
+__device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
+                            const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
+                            float &bu, float &bv, uint32_t &bprim) {
+    struct Ent { uint32_t node; float t; uint32_t prev; float p[3]; };
+    constexpr uint32_t NONE = 0xffffffffu;
+    Ent stack[48];
+    uint32_t mbox[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) mbox[i] = 0xffffffffu;
+    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+    const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
+    uint32_t enPt = 0, exPt = 1;
+    stack[0].t = mint;
+    for (int k = 0; k < 3; ++k) stack[0].p[k] = oa[k] + da[k] * mint;   // ray(mint)
+    stack[1].t = maxt;
+    for (int k = 0; k < 3; ++k) stack[1].p[k] = oa[k] + da[k] * maxt;
+    stack[1].node = NONE;
+    bool found = false;
+    uint32_t node = 0;
+    while (node != NONE) {
+        uint2 n = nodes[node];
+        while (!(n.x & 0x80000000u)) {
+            const float split = __uint_as_float(n.y);
+            const int axis = (int)(n.x & 3u);
+            const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+            uint32_t farChild;
+            if (stack[enPt].p[axis] <= split) {
+                if (stack[exPt].p[axis] <= split) { node = left; n = nodes[node]; continue; }
+                if (stack[enPt].p[axis] == split) { node = left + 1; n = nodes[node]; continue; }
+                node = left;
+                farChild = left + 1;
+            } else {
+                if (split < stack[exPt].p[axis]) { node = left + 1; n = nodes[node]; continue; }
+                farChild = left;
+                node = left + 1;
+            }
+            const float distToSplit = (split - oa[axis]) * rcp[axis];
+            const uint32_t tmp = exPt++;
+            if (exPt == enPt) ++exPt;
+            if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
+            stack[exPt].prev = tmp;
+            stack[exPt].t = distToSplit;
+            stack[exPt].node = farChild;
+            for (int k = 0; k < 3; ++k) stack[exPt].p[k] = oa[k] + da[k] * distToSplit;
+            stack[exPt].p[axis] = split;
+            n = nodes[node];
+        }
+        for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
+            const uint32_t prim = indices[e];
+            if (mbox[prim & 7u] == prim) continue;
+            const MtsgTri &tr = tris[prim];
+            const uint32_t k = tr.k;
+            float o_u, o_v, o_k, d_u, d_v, d_k;
+            if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+            else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+            else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+            // TriAccel::rayIntersect (triaccel.h:92-160) on [mint, maxt]
+            const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
+            if (!(t < mint || t > maxt)) {
+                const float hu = o_u + t * d_u - tr.a_u;
+                const float hv = o_v + t * d_v - tr.a_v;
+                const float u = hv * tr.b_nu + hu * tr.b_nv;
+                const float v = hu * tr.c_nu + hv * tr.c_nv;
+                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                    if (ANY) return true;
+                    maxt = t;
+                    found = true;
+                    bt = t; bu = u; bv = v; bprim = prim;
+                }
+            }
+            mbox[prim & 7u] = prim;
+        }
+        if (stack[exPt].t > maxt) break;
+        enPt = exPt;
+        node = stack[exPt].node;
+        exPt = stack[enPt].prev;
+    }
+    return found;
+}
+
 // ShapeKDTree::rayIntersect (skdtree.cpp:112-142 closest, :207-226 shadow):
 // scene-AABB clip + adaptive ray epsilon -> [mint, maxt] for the traversal
 __device__ __forceinline__ bool ray_interval(const MtsgDeviceScene &S, f3 o, f3 d, float rmint, float rmaxt,
@@ -1724,6 +1814,41 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
     }
 }
 
+// wf_trace over the reference's kd-tree (MTSGPU_FLAG_KDTREE): the same queues,
+// kd_traverse (SAHKDTree3D::rayIntersectHavran) per ray; hits carry the global
+// primitive number, as wf_trace's do for triangle scenes
+template <bool STATS>
+__global__ __launch_bounds__(BLOCK) void wf_trace_kd(MtsgLaunch L, MtsgWave W, unsigned long long *part) {
+    __shared__ uint32_t red[BLOCK / 64 * 16];
+    if (blockIdx.x == 0 && threadIdx.x == 0) W.live[W.parity ^ 1u] = 0;
+    const uint32_t region = blockIdx.x / W.split, part0 = blockIdx.x % W.split;
+    if (region >= W.regions) return;
+    const uint32_t nc = W.rcnt[(W.parity * 2 + 0) * W.regions + region];
+    const uint32_t ns = W.rcnt[(W.parity * 2 + 1) * W.regions + region];
+    if (part0 * BLOCK >= nc + ns) return;   // block-uniform
+    const uint2 *kn = (const uint2 *)L.kd_nodes;
+    const uint32_t n = nc + ns, base = region * W.rounds * BLOCK;
+    for (uint32_t i = part0 * BLOCK + threadIdx.x; i < n; i += W.split * BLOCK) {
+        const bool shadow = i >= nc;
+        const uint32_t k = base + (shadow ? i - nc : i);
+        const float4 *q = shadow ? W.sray : W.qray;
+        const float4 a = q[2 * (size_t)k], b = q[2 * (size_t)k + 1];
+        const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
+        float ht = 0, hu = 0, hv = 0;
+        uint32_t prim = 0;
+        if (shadow) {
+            W.occl[k] = kd_traverse<true>(kn, L.kd_indices, L.kd_tris, o, d, a.w, b.w, ht, hu, hv, prim) ? 1u : 0u;
+        } else {
+            const bool hit = kd_traverse<false>(kn, L.kd_indices, L.kd_tris, o, d, a.w, b.w, ht, hu, hv, prim);
+            W.hit[k] = make_float4(ht, hu, hv, __uint_as_float(hit ? prim : MTSG_WF_NONE));
+        }
+    }
+    if (STATS) {
+        uint32_t v[16] = {};
+        block_counters(part, v, red);
+    }
+}
+
 // the per-block partial counters of a chunk -> MtsgLaunch::counters
 __global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters) {
     const uint32_t k = threadIdx.x & 15u;   // 256 threads: counter k, blocks b = threadIdx / 16 (mod 16)
@@ -2173,96 +2298,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void trace_kernel(MtsgDeviceScene S, 
     }
 }
 
-// The reference's own kd-tree (kdtree_build.cpp) traversed as
-// SAHKDTree3D::rayIntersectHavran (sahkdtree3.h:178-308): entry/exit points on
-// a stack of MTS_KD_MAXDEPTH entries, leaves tested over the global [mint,
-// maxt] with the 8-entry hashed mailbox (:138-152, MTS_KD_MAILBOX_ENABLED),
-// and ShapeKDTree::intersect's TriAccel test (skdtree.h:248-338), which keeps
-// a hit at t == maxt: among exactly tied triangles the last one tested wins,
-// as in the reference.  TriAccel records are in global primitive order.
-// Correctness path (mtsgpu_trace_rays with MTSGPU_TRACE_KDTREE): the stack
-// lives in scratch.
-template <bool ANY>
-__device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
-                            const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
-                            float &bu, float &bv, uint32_t &bprim) {
-    struct Ent { uint32_t node; float t; uint32_t prev; float p[3]; };
-    constexpr uint32_t NONE = 0xffffffffu;
-    Ent stack[48];
-    uint32_t mbox[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) mbox[i] = 0xffffffffu;
-    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
-    const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
-    uint32_t enPt = 0, exPt = 1;
-    stack[0].t = mint;
-    for (int k = 0; k < 3; ++k) stack[0].p[k] = oa[k] + da[k] * mint;   // ray(mint)
-    stack[1].t = maxt;
-    for (int k = 0; k < 3; ++k) stack[1].p[k] = oa[k] + da[k] * maxt;
-    stack[1].node = NONE;
-    bool found = false;
-    uint32_t node = 0;
-    while (node != NONE) {
-        uint2 n = nodes[node];
-        while (!(n.x & 0x80000000u)) {
-            const float split = __uint_as_float(n.y);
-            const int axis = (int)(n.x & 3u);
-            const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
-            uint32_t farChild;
-            if (stack[enPt].p[axis] <= split) {
-                if (stack[exPt].p[axis] <= split) { node = left; n = nodes[node]; continue; }
-                if (stack[enPt].p[axis] == split) { node = left + 1; n = nodes[node]; continue; }
-                node = left;
-                farChild = left + 1;
-            } else {
-                if (split < stack[exPt].p[axis]) { node = left + 1; n = nodes[node]; continue; }
-                farChild = left;
-                node = left + 1;
-            }
-            const float distToSplit = (split - oa[axis]) * rcp[axis];
-            const uint32_t tmp = exPt++;
-            if (exPt == enPt) ++exPt;
-            if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-            stack[exPt].prev = tmp;
-            stack[exPt].t = distToSplit;
-            stack[exPt].node = farChild;
-            for (int k = 0; k < 3; ++k) stack[exPt].p[k] = oa[k] + da[k] * distToSplit;
-            stack[exPt].p[axis] = split;
-            n = nodes[node];
-        }
-        for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
-            const uint32_t prim = indices[e];
-            if (mbox[prim & 7u] == prim) continue;
-            const MtsgTri &tr = tris[prim];
-            const uint32_t k = tr.k;
-            float o_u, o_v, o_k, d_u, d_v, d_k;
-            if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
-            else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
-            else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-            // TriAccel::rayIntersect (triaccel.h:92-160) on [mint, maxt]
-            const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
-            if (!(t < mint || t > maxt)) {
-                const float hu = o_u + t * d_u - tr.a_u;
-                const float hv = o_v + t * d_v - tr.a_v;
-                const float u = hv * tr.b_nu + hu * tr.b_nv;
-                const float v = hu * tr.c_nu + hv * tr.c_nv;
-                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
-                    if (ANY) return true;
-                    maxt = t;
-                    found = true;
-                    bt = t; bu = u; bv = v; bprim = prim;
-                }
-            }
-            mbox[prim & 7u] = prim;
-        }
-        if (stack[exPt].t > maxt) break;
-        enPt = exPt;
-        node = stack[exPt].node;
-        exPt = stack[enPt].prev;
-    }
-    return found;
-}
-
 template <bool ANY>
 __global__ __launch_bounds__(BLOCK) void trace_kd_kernel(MtsgDeviceScene S, const uint2 *__restrict__ kdNodes,
                                                          const uint32_t *__restrict__ kdIndices,
@@ -2502,6 +2537,11 @@ hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned
 
 hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
                                 bool stats, hipStream_t s) {
+    if (L.kd_nodes) {
+        if (stats) hipLaunchKernelGGL(wf_trace_kd<true>, dim3(grid), dim3(BLOCK), 0, s, L, W, part);
+        else hipLaunchKernelGGL(wf_trace_kd<false>, dim3(grid), dim3(BLOCK), 0, s, L, W, part);
+        return hipGetLastError();
+    }
     const size_t lds = mtsg_wf_trace_lds_bytes(L);
 #define MTSG_WFT(ST, SL, A) hipLaunchKernelGGL((wf_trace<ST, SL, A>), dim3(grid), dim3(BLOCK), lds, s, L, W, part)
     const bool ana = L.ana != 0;

@@ -169,11 +169,14 @@ class Context:
             return abi.FLAG_WAVEFRONT
         if engine == 'megakernel':
             return abi.FLAG_MEGAKERNEL
-        raise ValueError('engine must be None, "wavefront" or "megakernel"')
+        if engine == 'kdtree':       # the wavefront engine over the reference's kd-tree
+            return abi.FLAG_KDTREE
+        raise ValueError('engine must be None, "wavefront", "megakernel" or "kdtree"')
 
     def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False, engine=None):
         """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict).
-        engine: None (the library's default), 'wavefront' or 'megakernel'."""
+        engine: None (the library's default), 'wavefront', 'megakernel' or 'kdtree'
+        (the wavefront engine tracing through the reference's kd-tree)."""
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
         x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))

@@ -65,6 +65,7 @@ def lib(variant='strict'):
         L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
         L.oracle_trace_rays.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.c_uint32, C.c_int,
                                         C.POINTER(C.c_float)]
+        L.oracle_set_kdtree.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_trace_rays_kd.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                            C.POINTER(C.c_float), C.c_uint32, C.c_int, C.POINTER(C.c_float)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -123,9 +124,11 @@ def configure_rc(scene):
     return lib().oracle_configure(C.byref(d))
 
 
-def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0), variant='strict'):
+def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0), variant='strict',
+           kdtree=None):
     """Render with the oracle; returns (film (H+2b, W+2b, 5), samples or None, stats dict).
-    variant='refflags' renders with the reference-flags build (lib())."""
+    variant='refflags' renders with the reference-flags build (lib()).
+    kdtree=(nodes, indices): every ray query traverses that kd-tree (Havran)."""
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     from pkgimport import mitsuba_amd
@@ -139,9 +142,18 @@ def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row
     smp = np.zeros((w * h * integ.sampleCount, m.abi.SAMPLE_RECORD_FLOATS), np.float32) if samples else None
     st = m.abi.Stats()
     d = scene.desc()
-    rc = L.oracle_render(C.byref(d), C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)),
-                         smp.ctypes.data_as(C.POINTER(C.c_float)) if samples else None,
-                         C.byref(st), libm_mode, threads)
+    up = C.POINTER(C.c_uint32)
+    if kdtree is not None:
+        kn = np.ascontiguousarray(kdtree[0], np.uint32)
+        ki = np.ascontiguousarray(kdtree[1], np.uint32)
+        L.oracle_set_kdtree(kn.ctypes.data_as(up), ki.ctypes.data_as(up))
+    try:
+        rc = L.oracle_render(C.byref(d), C.byref(p), film.ctypes.data_as(C.POINTER(C.c_float)),
+                             smp.ctypes.data_as(C.POINTER(C.c_float)) if samples else None,
+                             C.byref(st), libm_mode, threads)
+    finally:
+        if kdtree is not None:
+            L.oracle_set_kdtree(None, None)
     if rc != 0:
         raise RuntimeError('oracle_render failed: %d' % rc)
     return film, smp, st.as_dict()

@@ -52,6 +52,9 @@
 #define BLOCK_SIZE 32 /* scene.cpp:24 */
 
 static int g_cr = 0; /* libm mode */
+/* oracle_set_kdtree: traverse this kd-tree (KDNode words, primitive lists) in
+   Scene::rayIntersect / isOccluded instead of the BVH (NULL: the BVH) */
+static const uint32_t *g_kd_nodes = NULL, *g_kd_indices = NULL;
 
 /* std::max / std::min semantics (NaN handling matters) */
 static inline float smax(float a, float b) { return (a < b) ? b : a; }
@@ -2993,6 +2996,8 @@ typedef struct {
 
 /* ShapeKDTree::rayIntersect(ray, its) (skdtree.cpp:112-142) + fillIntersectionRecord<true>
  * (skdtree.h:343-429) */
+static int kd_havran(const Scene *S, const uint32_t *nodes, const uint32_t *indices, const Ray *ray, float mint,
+                     float maxt, int shadow, uint32_t *prim, float *tu, float *tv, float *tt);
 static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *C) {
     float mint, maxt;
     its->valid = 0;
@@ -3006,7 +3011,8 @@ static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *
     if (ray->maxt < maxt) maxt = ray->maxt;
     if (!(maxt > mint)) return;
     uint32_t prim; float u, v, t;
-    if (!trace_closest(S, ray, mint, maxt, &prim, &u, &v, &t, C)) return;
+    if (g_kd_nodes ? !kd_havran(S, g_kd_nodes, g_kd_indices, ray, mint, maxt, 0, &prim, &u, &v, &t)
+                   : !trace_closest(S, ray, mint, maxt, &prim, &u, &v, &t, C)) return;
     const Mesh *m = &S->meshes[S->taMesh[prim]];
     uint32_t tri = S->taTri[prim];
     its->valid = 1; its->t = t; its->mesh = (int)S->taMesh[prim]; its->tri = tri;
@@ -3056,6 +3062,10 @@ static int scene_occluded(const Scene *S, const Ray *ray, Counters *C) {
     if (rayMinT > mint) mint = rayMinT;
     if (ray->maxt < maxt) maxt = ray->maxt;
     if (!(maxt > mint)) return 0;
+    if (g_kd_nodes) {
+        uint32_t prim; float u, v, t;
+        return kd_havran(S, g_kd_nodes, g_kd_indices, ray, mint, maxt, 1, &prim, &u, &v, &t);
+    }
     return trace_any(S, ray, mint, maxt, C);
 }
 
@@ -3967,6 +3977,11 @@ static int kd_havran(const Scene *S, const uint32_t *nodes, const uint32_t *indi
         exPt = stack[enPt].prev;
     }
     return found;
+}
+
+void oracle_set_kdtree(const uint32_t *nodes, const uint32_t *indices) {
+    g_kd_nodes = nodes;
+    g_kd_indices = indices;
 }
 
 /* oracle_trace_rays over a given kd-tree (ShapeKDTree::rayIntersect: scene
