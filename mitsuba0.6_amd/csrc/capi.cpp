@@ -583,7 +583,13 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             L.lds_dims = (uint32_t)std::min<size_t>(32, (perBlock - fixed) / ((size_t)L.nibbles * 16 * 4));
         }
     }
-    if (const char *env = std::getenv("MTSGPU_WAVES")) L.waves = std::atoi(env) == 4 ? 4u : 3u;
+    // the all-diffuse variant makes no calls: 4 waves/SIMD (128 VGPRs) beat 3 (C2 +8.3%)
+    // and 5 (-15%) (profiles/r02_ab_c2_waves4.log, r02_ab_c2_waves45.log)
+    if (L.scene_lds && L.all_diffuse) L.waves = 4;
+    if (const char *env = std::getenv("MTSGPU_WAVES")) {
+        const int w = std::atoi(env);
+        L.waves = w == 4 ? 4u : 3u;
+    }
     if (const char *env = std::getenv("MTSGPU_SOBOL_LDS_DIMS"))
         L.lds_dims = (uint32_t)std::min(1024l, std::max(0l, std::strtol(env, nullptr, 10)));
     // own-pixel splat buffer [5][chunk][pixels]; spp processed in chunks that fit the budget

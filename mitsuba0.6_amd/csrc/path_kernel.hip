@@ -2402,7 +2402,12 @@ static void launch_path_w(const MtsgLaunch &L, int grid, bool instr, hipStream_t
 
 template <int FEAT>
 static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
-    if (L.scene_lds) launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+    if (L.scene_lds) {
+        if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {   // no calls: room for 4 waves (capi.cpp)
+            if (L.waves == 4) { launch_path_w<true, FEAT, 4>(L, grid, instr, stream); return; }
+        }
+        launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+    }
     else if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
     else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
 }
@@ -2596,13 +2601,18 @@ static int occupancy_w(const MtsgLaunch &L, int *bpc) {
 }
 template <int FEAT>
 static int occupancy_e(const MtsgLaunch &L, int *bpc) {
-    if (L.scene_lds) return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
+    if (L.scene_lds) {
+        if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {
+            if (L.waves == 4) return occupancy_w<true, FEAT, 4>(L, bpc);
+        }
+        return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
+    }
     if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
     return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
 }
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
     switch (mtsg_path_features(L)) {
-        case 0: return occupancy_e<0>(L, blocksPerCU);
+        case 0: return L.all_diffuse ? occupancy_e<MTSG_FEAT_DIFF>(L, blocksPerCU) : occupancy_e<0>(L, blocksPerCU);
         case MTSG_FEAT_ENV: return occupancy_e<MTSG_FEAT_ENV>(L, blocksPerCU);
         case MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_EXT>(L, blocksPerCU);
         case MTSG_FEAT_ENV | MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, blocksPerCU);

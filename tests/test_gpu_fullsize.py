@@ -4,8 +4,9 @@ small cases of test_gpu_parity.py.
 - C1 (Cornell box, 512x512, 64 spp: 16.8 M samples) whole frame: every
   per-sample record (Li, alpha, sample position, path depth) bit-identical to
   the oracle, and the ray / shadow-ray / path-length counters equal.
-- C2 (Cornell box 1280x720, 512 spp), C3 (matpreview + envmap, 512 spp) and
-  C4 (atrium, 256 spp): a full-resolution row band at the configured spp,
+- C2 (Cornell box 1280x720, 512 spp), C3 (matpreview + envmap, 512 spp),
+  C4 (atrium, 256 spp) and C5 (textured roughplastic, 1024 spp): a
+  full-resolution row band at the configured spp,
   rendered by the full-frame launch geometry (window = whole rows).
 
 Same bar as test_gpu_parity.py.  The oracle runs on the
@@ -48,7 +49,7 @@ def test_c1_full_frame_bitexact(gpu_ctx, oracle):
     np.testing.assert_allclose(film_g, film_o, rtol=1e-6, atol=1e-7)
 
 
-@pytest.mark.parametrize('cfg,rows', [('C2', (352, 8)), ('C3', (356, 4)), ('C4', (300, 2))])
+@pytest.mark.parametrize('cfg,rows', [('C2', (352, 8)), ('C3', (356, 4)), ('C4', (300, 2)), ('C5', (360, 1))])
 def test_full_resolution_row_band_bitexact(gpu_ctx, oracle, cfg, rows):
     sc, it = scenes.build(cfg)
     W = sc.sensor.width
