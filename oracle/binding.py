@@ -65,6 +65,9 @@ def lib(variant='strict'):
         L.oracle_configure.argtypes = [C.POINTER(abi.SceneDesc)]
         L.oracle_trace_rays.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.c_uint32, C.c_int,
                                         C.POINTER(C.c_float)]
+        L.oracle_rdiel_trans_weight.argtypes = [C.c_int, C.c_float, C.c_float, C.POINTER(C.c_float), C.c_float,
+                                                C.c_float, C.c_int]
+        L.oracle_rdiel_trans_weight.restype = C.c_float
         L.oracle_set_kdtree.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         L.oracle_trace_rays_kd.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                            C.POINTER(C.c_float), C.c_uint32, C.c_int, C.POINTER(C.c_float)]
@@ -178,3 +181,12 @@ def render_order(width, height, block=32):
     n = lib().oracle_render_order(width, height, block, pts.ctypes.data_as(ip), bs.ctypes.data_as(ip), C.byref(cnt))
     assert n == width * height and cnt.value == nb
     return pts, bs
+
+
+def rdiel_trans_weight(distr, alpha, eta, wi, sx, sy, walter=False):
+    """Rough-transmittance integrand (oracle_rdiel_trans_weight) at one point:
+    distr 0/1/2 = beckmann/ggx/phong."""
+    L = lib()
+    w = (C.c_float * 3)(*[float(x) for x in wi])
+    return L.oracle_rdiel_trans_weight(int(distr), alpha, eta, w, sx, sy, int(bool(walter)))
+

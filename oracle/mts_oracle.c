@@ -3821,6 +3821,36 @@ int oracle_bsdf_sample(const mtsgpu_bsdf_desc *bd, const float *wi3, const float
     *eta = r.eta;
     return (int)r.sampledType;
 }
+/* The rough-transmittance integrand the reference's generator integrates
+ * (rdielprec.cpp:40-56: roughdielectric's sample(bRec, sample) restricted to
+ * ETransmission in EImportance mode, roughdielectric.cpp:424-511), computed
+ * with this oracle's own microfacet, Fresnel and refraction functions, with
+ * D(m)cos(m) sampling (sampleVisible = false) and optionally without Walter's
+ * roughness scaling (the state the shipped tables were generated in).  Test
+ * hook: tests/test_rtrans_pinning.py compares it with tools/rtrans_nd.c, whose
+ * integrals reproduce the reference's data/microfacet/<distr>.dat. */
+float oracle_rdiel_trans_weight(int type, float alpha, float eta, const float *wi3, float sx, float sy, int walter) {
+    g_cr = 1;
+    if (sx == 1) sx = 1 - EPSILON;
+    if (sy == 1) sy = 1 - EPSILON;
+    const V3 wi = v3(wi3[0], wi3[1], wi3[2]);
+    const float a = smax(alpha, 1e-4f);
+    const float avg = ((a + a) + a) * (1.0f / 3);   /* Spectrum::average of the constant texture */
+    Distr d, sd;
+    distr_init(&d, type, avg, avg, 0);
+    sd = d;
+    if (walter) distr_scale_alpha(&sd, 1.2f - 0.2f * sqrtf(fabsf(wi.z)));
+    float pdf;
+    const V3 m = distr_sample(&sd, vmul(wi, signumf(wi.z)), sx, sy, &pdf);
+    if (pdf == 0) return 0.0f;
+    float cosThetaT;
+    const float F = fresnel_dielectric_ext(vdot(wi, m), &cosThetaT, eta);
+    if (cosThetaT == 0) return 0.0f;
+    const V3 wo = refract_v(wi, m, eta, cosThetaT);
+    if (wi.z * wo.z >= 0) return 0.0f;
+    return (1 - F) * fabsf(distr_eval(&d, m) * distr_G(&d, wi, wo, m) * vdot(wi, m) / (pdf * wi.z));
+}
+
 int oracle_bsdf_eval(const mtsgpu_bsdf_desc *bd, const float *wi3, const float *wo3,
                      float *value3, float *pdf, int libm_mode) {
     g_cr = libm_mode;

@@ -46,6 +46,7 @@ int oracle_env_tables(const mtsgpu_scene_desc *scene, float *params, uint16_t *t
 /* configure() only: the status the reference's plugin constructors/configure() raise */
 int oracle_configure(const mtsgpu_scene_desc *scene);
 int oracle_trace_rays(const mtsgpu_scene_desc *scene, const float *rays, uint32_t n, int shadow, float *hits);
+float oracle_rdiel_trans_weight(int type, float alpha, float eta, const float *wi3, float sx, float sy, int walter);
 void oracle_set_kdtree(const uint32_t *nodes, const uint32_t *indices);
 int oracle_trace_rays_kd(const mtsgpu_scene_desc *scene, const uint32_t *nodes, const uint32_t *indices,
                          const float *rays, uint32_t n, int shadow, float *hits);

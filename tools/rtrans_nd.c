@@ -37,6 +37,8 @@
  * usage: rtrans_nd <beckmann|ggx|phong> <out.dat> [threads]
  *        rtrans_nd <distr> --cell <inverted> <iorIdx> <alphaIdx>
  *              prints the cell's 100 transmittances and diffuse term (%a)
+ *        rtrans_nd <distr> --weights < "alpha eta wx wy wz sx sy walter" lines
+ *              prints the integrand (the transmission weight) per line (%a)
  */
 #include <math.h>
 #include <stdint.h>
@@ -686,6 +688,20 @@ int main(int argc, char **argv) {
     /* rdielprec.cpp:152-163: the grid in Float from the single-precision header values */
 #define IOR_AT(i) ((Float)iorStart + ((Float)iorEnd - (Float)iorStart) * FPOW((Float)(i) * iorStep, (Float)4.0f))
 #define ALPHA_AT(j) ((Float)alphaStart + ((Float)alphaEnd - (Float)alphaStart) * FPOW((Float)(j) * alphaStep, (Float)4.0f))
+    if (!strcmp(argv[2], "--weights")) {
+        /* the integrand itself, for the oracle pinning test: stdin lines
+           "alpha eta wx wy wz sx sy walter" -> the transmission weight (%a) */
+        double a, e, wx, wy, wz, sx, sy;
+        int walter;
+        while (scanf("%lf %lf %lf %lf %lf %lf %lf %d", &a, &e, &wx, &wy, &wz, &sx, &sy, &walter) == 8) {
+            Cell c;
+            c.type = type; c.visible = 0; c.alpha = (Float)a; c.eta = (Float)e;
+            c.wi = v3((Float)wx, (Float)wy, (Float)wz);
+            g_nowalter = !walter;
+            printf("%a\n", (double)trans_weight(&c, (Float)sx, (Float)sy));
+        }
+        return 0;
+    }
     if (!strcmp(argv[2], "--cell")) {
         if (argc < 6) return 2;
         int inv = atoi(argv[3]), i = atoi(argv[4]), j = atoi(argv[5]);
