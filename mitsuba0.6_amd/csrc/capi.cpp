@@ -77,6 +77,8 @@ struct mtsgpu_ctx {
     bool have_scene = false;
     HostScene host;
     MtsgDeviceScene dscene;
+    DevBuf scan_tris;   // k-grouped TriAccel records of scan-sized scenes
+    uint32_t scan_n[3] = {0, 0, 0};
     DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
@@ -195,6 +197,18 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         (e = upload(ctx->emitters, H.emitters, s)) != hipSuccess || (e = upload(ctx->area_cdf, H.area_cdf, s)) != hipSuccess ||
         (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, sobol_nibble_tables(), s)) != hipSuccess)
         return hip_fail(ctx, e, "scene upload");
+    // tiny scenes: the TriAccel records grouped by projection axis, so the scan
+    // runs three branch-free loops (the closest hit and its tie rule do not
+    // depend on the order the records are tested in)
+    ctx->scan_n[0] = ctx->scan_n[1] = ctx->scan_n[2] = 0;
+    if (H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty()) {
+        std::vector<MtsgTri> g;
+        for (uint32_t k = 0; k < 3; ++k)
+            for (const MtsgTri &t : H.tris)
+                if (t.k == k) { g.push_back(t); ctx->scan_n[k]++; }
+        if (g.empty()) g.push_back(MtsgTri{});
+        if ((e = upload(ctx->scan_tris, g, s)) != hipSuccess) return hip_fail(ctx, e, "scene upload");
+    }
     const MtsgEnv *denv = nullptr;
     if (H.env.emitter >= 0) {
         if ((e = upload(ctx->env_texels, H.env_texels, s)) != hipSuccess || (e = upload(ctx->env_rows, H.env_cdf_rows, s)) != hipSuccess ||
@@ -549,6 +563,8 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.scene_lds = (sceneBytes <= (32u << 10) && !std::getenv("MTSGPU_NO_SCENE_LDS")) ? 1u : 0u;
     L.scan = (L.scene_lds && H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty() && !std::getenv("MTSGPU_NO_SCAN"))
                  ? 1u : 0u;
+    L.scan_tris = (const MtsgTri *)ctx->scan_tris.p;
+    for (int k = 0; k < 3; ++k) L.scan_n[k] = ctx->scan_n[k];
     // large scenes are latency-bound: run 4 waves/SIMD when 4 blocks' traversal
     // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
     // LDS as the rest allows (the others are read through L1/L2)
@@ -808,7 +824,7 @@ const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() :
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    DevBuf *bufs[] = {&ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,

@@ -256,6 +256,8 @@ struct MtsgLaunch {
     const uint32_t *kd_indices;
     const MtsgTri *kd_tris;           // TriAccel records in global primitive order
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
+    const MtsgTri *scan_tris;         // the scan's TriAccel records grouped by projection axis k = 0, 1, 2
+    uint32_t scan_n[3];               // (degenerate k = 3 records dropped); counts per group
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     int32_t integrator;               // MTSGPU_INTEGRATOR_*
     uint32_t sampler;                 // MTSGPU_SAMPLER_*

@@ -435,43 +435,60 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
 
 #endif
 
-// Tiny scenes (<= MTSG_SCAN_MAX primitives, e.g. the Cornell box): every lane tests
-// every TriAccel record in one wave-uniform loop.  The records are read through
-// the constant address space with a uniform index, i.e. by scalar loads into
-// SGPRs: no traversal stack, no divergent node loop, no VGPRs for the records.
-// The closest hit and the tie rule are those of traverse().
 typedef __attribute__((address_space(4))) const MtsgTri cst_tri;
-template <bool ANY, bool STATS>
-__device__ __forceinline__ bool scan_tris(cst_tri *tris, uint32_t n, f3 o, f3 d, float mint, float maxt,
-                                          uint32_t &bestSlot, float &bu, float &bv, float &bt,
-                                          unsigned long long &tests) {
-    bool found = false;
-    uint32_t bestPrim = 0;
-    bt = maxt;
+// one projection axis' records: the coordinate permutation is a compile-time
+// constant, so the loop is straight-line code around the correctly rounded
+// division; each record is read whole (two scalar loads) at the loop head
+template <int K, bool ANY, bool STATS>
+__device__ __forceinline__ bool scan_k(cst_tri *tris, uint32_t n, f3 o, f3 d, float mint, bool &found,
+                                       uint32_t &bestPrim, float &bu, float &bv, float &bt,
+                                       unsigned long long &tests) {
+    const float o_u = K == 0 ? o.y : K == 1 ? o.z : o.x, o_v = K == 0 ? o.z : K == 1 ? o.x : o.y,
+                o_k = K == 0 ? o.x : K == 1 ? o.y : o.z;
+    const float d_u = K == 0 ? d.y : K == 1 ? d.z : d.x, d_v = K == 0 ? d.z : K == 1 ? d.x : d.y,
+                d_k = K == 0 ? d.x : K == 1 ? d.y : d.z;
     for (uint32_t i = 0; i < n; ++i) {
         if (STATS) tests++;
         cst_tri &tr = tris[i];
-        const uint32_t k = tr.k;
-        float o_u, o_v, o_k, d_u, d_v, d_k;
-        if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
-        else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
-        else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-        else continue;
+        const float n_u = tr.n_u, n_v = tr.n_v, n_d = tr.n_d, a_u = tr.a_u, a_v = tr.a_v, b_nu = tr.b_nu,
+                    b_nv = tr.b_nv, c_nu = tr.c_nu, c_nv = tr.c_nv;
+        const uint32_t prim = tr.prim;
         // TriAccel::rayIntersect (triaccel.h:92-160)
-        const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
+        const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
         if (t < mint || t > bt) continue;
-        const float hu = o_u + t * d_u - tr.a_u;
-        const float hv = o_v + t * d_v - tr.a_v;
-        const float u = hv * tr.b_nu + hu * tr.b_nv;
-        const float v = hu * tr.c_nu + hv * tr.c_nv;
+        const float hu = o_u + t * d_u - a_u;
+        const float hv = o_v + t * d_v - a_v;
+        const float u = hv * b_nu + hu * b_nv;
+        const float v = hu * c_nu + hv * c_nv;
         if (u >= 0 && v >= 0 && u + v <= 1.0f) {
             if (ANY) return true;
-            const uint32_t prim = tr.prim;
             if (!found || t < bt || prim > bestPrim) {
-                found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+                found = true; bestPrim = prim; bt = t; bu = u; bv = v;
             }
         }
     }
+    return false;
+}
+
+// Tiny scenes (<= MTSG_SCAN_MAX triangles, no analytic shapes): every lane
+// tests every TriAccel record, read from the constant address space with a
+// uniform index (scalar loads into SGPRs): no traversal stack, no divergent
+// node loop.  The records come grouped by projection axis (L.scan_tris); the
+// result -- the closest t, ties to the larger primitive index as in
+// traverse() -- does not depend on the test order.  Returns the
+// primitive index (not a slot) in bestPrim.
+template <bool ANY, bool STATS>
+__device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float mint, float maxt,
+                                          uint32_t &bestPrim, float &bu, float &bv, float &bt,
+                                          unsigned long long &tests) {
+    cst_tri *tris = (cst_tri *)L.scan_tris;
+    const uint32_t n0 = L.scan_n[0], n1 = L.scan_n[1], n2 = L.scan_n[2];
+    bool found = false;
+    bestPrim = 0;
+    bt = maxt;
+    if (scan_k<0, ANY, STATS>(tris, n0, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
+    if (scan_k<1, ANY, STATS>(tris + n0, n1, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
+    if (scan_k<2, ANY, STATS>(tris + n0 + n1, n2, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
     return found;
 }
 
@@ -899,8 +916,12 @@ struct PathState {
     float rmint, rmaxt, smaxt;
 };
 
+// per-lane counts: 32-bit for the always-on ones (fewer live VGPRs in the
+// persistent loop; finish() flushes them long before they could wrap),
+// 64-bit for the INSTR-only traversal statistics
 struct PathCounters {
-    unsigned long long rays, shadow, len, samples, nodes, tests, err, hits, nee, sobol;
+    uint32_t rays, shadow, len, samples, err;
+    unsigned long long nodes, tests, hits, nee, sobol;
 };
 
 // LDS of path_kernel / wf_shade: [Sobol nibble tables][look_up column tables]
@@ -1366,10 +1387,19 @@ struct PathShader {
             rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
             rec[4] = sx; rec[5] = sy; rec[6] = (float)P.depth; rec[7] = smp.err ? 1.0f : 0.0f;
         }
-        c.len += (unsigned long long)P.depth;
+        c.len += (uint32_t)P.depth;
         c.samples++;
         if (STATS) c.sobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
         if (smp.err) c.err++;
+        // a lane's rays and shadow rays never exceed its path lengths plus samples:
+        // flush the 32-bit counts well before any of them can wrap
+        if (__builtin_expect((c.len | c.samples) >= 0x40000000u, 0)) {
+            atomicAdd(L.counters + 0, (unsigned long long)c.samples);
+            atomicAdd(L.counters + 1, (unsigned long long)c.rays);
+            atomicAdd(L.counters + 2, (unsigned long long)c.shadow);
+            atomicAdd(L.counters + 3, (unsigned long long)c.len);
+            c.samples = c.rays = c.shadow = c.len = 0;
+        }
         st.active = false;
         haveRay = haveShadow = false;
     }
@@ -1377,10 +1407,10 @@ struct PathShader {
 
 template <bool STATS>
 __device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const PathCounters &c) {
-    atomicAdd(L.counters + 0, c.samples);
-    atomicAdd(L.counters + 1, c.rays);
-    atomicAdd(L.counters + 2, c.shadow);
-    atomicAdd(L.counters + 3, c.len);
+    atomicAdd(L.counters + 0, (unsigned long long)c.samples);
+    atomicAdd(L.counters + 1, (unsigned long long)c.rays);
+    atomicAdd(L.counters + 2, (unsigned long long)c.shadow);
+    atomicAdd(L.counters + 3, (unsigned long long)c.len);
     if (STATS) {
         atomicAdd(L.counters + 4, c.nodes);
         atomicAdd(L.counters + 5, c.tests);
@@ -1388,7 +1418,7 @@ __device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const P
         atomicAdd(L.counters + 9, c.nee);
         atomicAdd(L.counters + 10, c.sobol);
     }
-    if (c.err) atomicAdd(L.counters + 6, c.err);
+    if (c.err) atomicAdd(L.counters + 6, (unsigned long long)c.err);
 }
 
 // The persistent megakernel: grid = CUs x resident blocks; every lane runs
@@ -1453,7 +1483,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 #endif
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS && L.scan)
-                    occluded = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, st.P.its.p, st.sd, mint, maxt,
+                    occluded = scan_tris<true, STATS>(L, st.P.its.p, st.sd, mint, maxt,
                                                       sl, a0, a1, a2, c.tests);
                 else if (SCENE_LDS)
                     occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
@@ -1464,6 +1494,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                                           S.analytic);
             }
         }
+        // the NEE estimate is added now (as shade() would first thing), so it
+        // is not live across the closest-hit traversal
+        if (st.active && st.haveShadow) {
+            if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
+            st.haveShadow = false;
+        }
         bool hit = false;
         uint32_t slot = 0, prim = 0;
         float hu = 0, hv = 0, ht = 0;
@@ -1472,7 +1508,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             float mint, maxt;
             if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS && L.scan)
-                    hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, st.ro, st.rd, mint, maxt, slot, hu,
+                    hit = scan_tris<false, STATS>(L, st.ro, st.rd, mint, maxt, slot, hu,
                                                   hv, ht, c.tests);
                 else if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
@@ -1482,7 +1518,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
                                                       S.analytic);
             }
-            if (hit) prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+            if (hit) prim = (SCENE_LDS && L.scan) ? slot : SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
         }
 
         // ---- C: shade -------------------------------------------------------
@@ -1781,7 +1817,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
         if (shadow) {
             bool occ;
             if (SCENE_LDS && L.scan)
-                occ = scan_tris<true, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+                occ = scan_tris<true, STATS>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
                 occ = traverse<true, STATS, ANA, MTSG_WF_LDS_STACK>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD,
                                                                     slot, hu, hv, ht, cN, cT, S.analytic, ovf);
@@ -1793,7 +1829,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
         } else {
             bool hit;
             if (SCENE_LDS && L.scan)
-                hit = scan_tris<false, STATS>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+                hit = scan_tris<false, STATS>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
                 hit = traverse<false, STATS, ANA, MTSG_WF_LDS_STACK>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD,
                                                                      slot, hu, hv, ht, cN, cT, S.analytic, ovf);
@@ -1802,7 +1838,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
                                                                      mint, maxt, stkN, stkD, slot, hu, hv, ht, cN, cT,
                                                                      S.analytic, ovf);
             const uint32_t w = !hit ? MTSG_WF_NONE : ANA ? slot
-                             : (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+                             : (SCENE_LDS && L.scan) ? slot : SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
             W.hit[k] = make_float4(ht, hu, hv, __uint_as_float(w));
         }
     }
@@ -2123,7 +2159,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         bool hit = false;
         if (ray_interval(S, o, d, rmint, rmaxt, false, mint, maxt)) {
             if (SCENE_LDS && L.scan)
-                hit = scan_tris<false, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, slot, hu, hv, ht, cT);
+                hit = scan_tris<false, false>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
                 hit = traverse<false, false, ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, slot, hu, hv, ht, cN,
                                                   cT, S.analytic);
@@ -2132,7 +2168,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
                                                   slot, hu, hv, ht, cN, cT, S.analytic);
         }
         if (hit) {
-            const uint32_t prim = (SCENE_LDS && !L.scan) ? ldsTris[slot].prim : S.tris[slot].prim;
+            const uint32_t prim = (SCENE_LDS && L.scan) ? slot : SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
             fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, o, d, h);
         } else {
             h = Hit{};
@@ -2145,7 +2181,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         if (!ray_interval(S, o, d, D_EPSILON, dist * (1 - D_SHADOW_EPSILON), true, mint, maxt)) return false;
         if (SCENE_LDS && L.scan) {
             uint32_t sl; float a0, a1, a2;
-            return scan_tris<true, false>((cst_tri *)S.tris, S.num_prims, o, d, mint, maxt, sl, a0, a1, a2, cT);
+            return scan_tris<true, false>(L, o, d, mint, maxt, sl, a0, a1, a2, cT);
         }
         if (SCENE_LDS) return shadow_any<ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, cN, cT, S.analytic);
         return shadow_any<ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD, cN, cT,
