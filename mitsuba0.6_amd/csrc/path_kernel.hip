@@ -492,6 +492,68 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
     return found;
 }
 
+// The megakernel's two rays of one bounce leave the same vertex (the NEE
+// shadow ray and the next closest-hit ray, both from its.p), so a tiny scene
+// tests them in one pass over the records: the TriAccel numerator is shared,
+// the records are loaded once, and the pairs of products pack into
+// v_pk_mul/v_pk_add.  Each ray's result is exactly that of its own scan_tris
+// (an empty interval, mint = +inf and maxt = -inf, disables a ray).
+template <int K, bool STATS>
+__device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 ds, f3 dc, float minS, float maxS,
+                                            float minC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
+                                            float &bv, float &bt, unsigned long long &tests) {
+    const float o_u = K == 0 ? o.y : K == 1 ? o.z : o.x, o_v = K == 0 ? o.z : K == 1 ? o.x : o.y,
+                o_k = K == 0 ? o.x : K == 1 ? o.y : o.z;
+    const float s_u = K == 0 ? ds.y : K == 1 ? ds.z : ds.x, s_v = K == 0 ? ds.z : K == 1 ? ds.x : ds.y,
+                s_k = K == 0 ? ds.x : K == 1 ? ds.y : ds.z;
+    const float c_u = K == 0 ? dc.y : K == 1 ? dc.z : dc.x, c_v = K == 0 ? dc.z : K == 1 ? dc.x : dc.y,
+                c_k = K == 0 ? dc.x : K == 1 ? dc.y : dc.z;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (STATS) tests += 2;
+        cst_tri &tr = tris[i];
+        const float n_u = tr.n_u, n_v = tr.n_v, n_d = tr.n_d, a_u = tr.a_u, a_v = tr.a_v, b_nu = tr.b_nu,
+                    b_nv = tr.b_nv, c_nu = tr.c_nu, c_nv = tr.c_nv;
+        const uint32_t prim = tr.prim;
+        // TriAccel::rayIntersect (triaccel.h:92-160) for both rays
+        const float num = n_d - o_u * n_u - o_v * n_v - o_k;
+        const float tS = num / (s_u * n_u + s_v * n_v + s_k);
+        const float tC = num / (c_u * n_u + c_v * n_v + c_k);
+        if (!(tS < minS || tS > maxS)) {
+            const float hu = o_u + tS * s_u - a_u;
+            const float hv = o_v + tS * s_v - a_v;
+            const float u = hv * b_nu + hu * b_nv;
+            const float v = hu * c_nu + hv * c_nv;
+            if (u >= 0 && v >= 0 && u + v <= 1.0f) occ = true;
+        }
+        if (!(tC < minC || tC > bt)) {
+            const float hu = o_u + tC * c_u - a_u;
+            const float hv = o_v + tC * c_v - a_v;
+            const float u = hv * b_nu + hu * b_nv;
+            const float v = hu * c_nu + hv * c_nv;
+            if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+                if (!found || tC < bt || prim > bestPrim) {
+                    found = true; bestPrim = prim; bt = tC; bu = u; bv = v;
+                }
+            }
+        }
+    }
+}
+
+template <bool STATS>
+__device__ __forceinline__ void scan_pair(const MtsgLaunch &L, f3 o, f3 ds, f3 dc, float minS, float maxS, float minC,
+                                          float maxC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
+                                          float &bv, float &bt, unsigned long long &tests) {
+    cst_tri *tris = (cst_tri *)L.scan_tris;
+    const uint32_t n0 = L.scan_n[0], n1 = L.scan_n[1], n2 = L.scan_n[2];
+    occ = false;
+    found = false;
+    bestPrim = 0;
+    bt = maxC;
+    scan_pair_k<0, STATS>(tris, n0, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
+    scan_pair_k<1, STATS>(tris + n0, n1, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
+    scan_pair_k<2, STATS>(tris + n0 + n1, n2, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
+}
+
 // AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
 __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, float &nearT, float &farT) {
     nearT = -INFINITY; farT = INFINITY;
@@ -1472,6 +1534,32 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 
         // ---- B: trace the shadow ray, then the closest-hit ray ---------------
         bool occluded = false;
+        bool hit = false;
+        uint32_t slot = 0, prim = 0;
+        float hu = 0, hv = 0, ht = 0;
+        if (SCENE_LDS && L.scan) {
+            // tiny scene: both rays of the bounce in one pass (scan_pair); when
+            // both exist they leave the same point (ro was set to its.p)
+            float minS = INFINITY, maxS = -INFINITY, minC = INFINITY, maxC = -INFINITY;
+            bool okS = false, okC = false;
+            if (st.active && st.haveShadow) {
+                c.shadow++;
+#ifndef MTSG_ABL_NO_SHADOW
+                if (!is_zero(st.P.neeC)) okS = ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, minS, maxS);
+#endif
+                if (!okS) { minS = INFINITY; maxS = -INFINITY; }
+            }
+            if (st.active && st.haveRay) {
+                c.rays++;
+                okC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
+                if (!okC) { minC = INFINITY; maxC = -INFINITY; }
+            }
+            if (__any(okS || okC))
+                scan_pair<STATS>(L, okC ? st.ro : st.P.its.p, st.sd, st.rd, minS, maxS, minC, maxC, occluded, hit,
+                                 prim, hu, hv, ht, c.tests);
+            hit = hit && okC;
+            occluded = occluded && okS;
+        } else {
         if (st.active && st.haveShadow) {
             c.shadow++;
             float mint, maxt;
@@ -1482,10 +1570,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
 #endif
                 uint32_t sl; float a0, a1, a2;
-                if (SCENE_LDS && L.scan)
-                    occluded = scan_tris<true, STATS>(L, st.P.its.p, st.sd, mint, maxt,
-                                                      sl, a0, a1, a2, c.tests);
-                else if (SCENE_LDS)
+                if (SCENE_LDS)
                     occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
                                                           sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
                 else
@@ -1500,17 +1585,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
             st.haveShadow = false;
         }
-        bool hit = false;
-        uint32_t slot = 0, prim = 0;
-        float hu = 0, hv = 0, ht = 0;
         if (st.active && st.haveRay) {
             c.rays++;
             float mint, maxt;
             if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
-                if (SCENE_LDS && L.scan)
-                    hit = scan_tris<false, STATS>(L, st.ro, st.rd, mint, maxt, slot, hu,
-                                                  hv, ht, c.tests);
-                else if (SCENE_LDS)
+                if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
                                                       hu, hv, ht, c.nodes, c.tests, S.analytic);
                 else
@@ -1518,7 +1597,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
                                                       S.analytic);
             }
-            if (hit) prim = (SCENE_LDS && L.scan) ? slot : SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
+            if (hit) prim = SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
+        }
+        }
+        if (st.active && st.haveShadow) {   // scan_pair case
+            if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
+            st.haveShadow = false;
         }
 
         // ---- C: shade -------------------------------------------------------
