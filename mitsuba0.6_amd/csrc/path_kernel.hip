@@ -492,6 +492,9 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
     return found;
 }
 
+#ifndef MTSG_SCAN_UNROLL
+#define MTSG_SCAN_UNROLL 1
+#endif
 // The megakernel's two rays of one bounce leave the same vertex (the NEE
 // shadow ray and the next closest-hit ray, both from its.p), so a tiny scene
 // tests them in one pass over the records: the TriAccel numerator is shared,
@@ -508,6 +511,7 @@ __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 
                 s_k = K == 0 ? ds.x : K == 1 ? ds.y : ds.z;
     const float c_u = K == 0 ? dc.y : K == 1 ? dc.z : dc.x, c_v = K == 0 ? dc.z : K == 1 ? dc.x : dc.y,
                 c_k = K == 0 ? dc.x : K == 1 ? dc.y : dc.z;
+#pragma unroll MTSG_SCAN_UNROLL
     for (uint32_t i = 0; i < n; ++i) {
         if (STATS) tests += 2;
         cst_tri &tr = tris[i];
