@@ -619,7 +619,7 @@ __device__ __noinline__ BSample sm_sample(GBsdf &b, f3 wi, float sx, float sy, f
 
 // ---- BSDF::eval / pdf / sample --------------------------------------------
 template <bool EXT>
-BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     const f3 zero = mk(0, 0, 0);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
         if (wi.z <= 0 || wo.z <= 0) return zero;
@@ -668,7 +668,7 @@ BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
 }
 
 template <bool EXT>
-BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
@@ -704,6 +704,27 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) 
     float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
     prob *= reflect ? F : (1 - F);
     return fabsf(prob * dwh_dwo);
+}
+
+template <bool EXT>
+BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    return bsdf_eval_body<EXT>(b, rt, wi, wo, u, v);
+}
+template <bool EXT>
+BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    return bsdf_pdf_body<EXT>(b, rt, wi, wo, u, v);
+}
+
+// BSDF::eval, then BSDF::pdf of the same query where the value is nonzero
+// (the NEE estimate of path.cpp:176-199 needs both): one out-of-line call, so
+// the caller's live registers are saved around one call instead of two
+struct EvalPdf { f3 val; float pdf; };
+template <bool EXT>
+BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    EvalPdf r;
+    r.val = bsdf_eval_body<EXT>(b, rt, wi, wo, u, v);
+    r.pdf = is_zero(r.val) ? 0.0f : bsdf_pdf_body<EXT>(b, rt, wi, wo, u, v);
+    return r;
 }
 
 // BSDF::sample(bRec, pdf, sample): roughdielectric consumes one more 1D sample
@@ -838,6 +859,17 @@ __device__ __forceinline__ float bsdf_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 
         return D_INV_PI * wo.z;
     } else {
         return bsdf_pdf<EXT>(b, rt, wi, wo, u, v);
+    }
+}
+template <bool EXT, bool DIFF_ONLY>
+__device__ __forceinline__ EvalPdf bsdf_eval_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if constexpr (DIFF_ONLY) {
+        EvalPdf r;
+        r.val = bsdf_eval_fast<EXT, true>(b, rt, wi, wo, u, v);
+        r.pdf = bsdf_pdf_fast<EXT, true>(b, rt, wi, wo, u, v);
+        return r;
+    } else {
+        return bsdf_eval_pdf<EXT>(b, rt, wi, wo, u, v);
     }
 }
 template <bool EXT, bool DIFF_ONLY>

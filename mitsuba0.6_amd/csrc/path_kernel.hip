@@ -1363,9 +1363,11 @@ struct PathShader {
                                         if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
                                     }
                                 }
-                                const f3 bsdfVal = bsdf_eval_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                const EvalPdf ep = bsdf_eval_pdf_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo,
+                                                                                 P.its.u, P.its.v);
+                                const f3 bsdfVal = ep.val;
                                 if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
-                                    const float bsdfPdf = bsdf_pdf_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, P.its.u, P.its.v);
+                                    const float bsdfPdf = ep.pdf;
                                     const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
                                     const float weight = pa / (pa + pb);
                                     c = mul(mulv(mulv(P.thr, value), bsdfVal), weight);
