@@ -496,7 +496,7 @@ __device__ __forceinline__ float rp_prob_specular(GBsdf &b, glb_f32 *rt, float c
 }
 
 // RoughPlastic::eval (roughplastic.cpp:300-345)
-__device__ __noinline__ f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
     const Distr d = bsdf_distr<true>(b, u, v);
     f3 result = mk(0, 0, 0);
@@ -519,7 +519,7 @@ __device__ __noinline__ f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u,
 }
 
 // RoughPlastic::pdf (roughplastic.cpp:347-393)
-__device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (wi.z <= 0 || wo.z <= 0) return 0.0f;
     const Distr d = bsdf_distr<true>(b, u, v);
     const f3 H = normalize(add(wo, wi));
@@ -530,6 +530,20 @@ __device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float 
     float result = prob * dwh_dwo * probSpecular;
     result += probDiffuse * (D_INV_PI * wo.z);
     return result;
+}
+__device__ __noinline__ f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    return rp_eval_body(b, rt, wi, wo, u, v);
+}
+__device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    return rp_pdf_body(b, rt, wi, wo, u, v);
+}
+struct EvalPdf { f3 val; float pdf; };
+// eval, and pdf where the value is nonzero, of one query in one call (NEE)
+__device__ __noinline__ EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    EvalPdf r;
+    r.val = rp_eval_body(b, rt, wi, wo, u, v);
+    r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body(b, rt, wi, wo, u, v);
+    return r;
 }
 
 // ---- smooth (delta) BSDFs: conductor, dielectric, plastic ------------------
@@ -718,9 +732,11 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) 
 // BSDF::eval, then BSDF::pdf of the same query where the value is nonzero
 // (the NEE estimate of path.cpp:176-199 needs both): one out-of-line call, so
 // the caller's live registers are saved around one call instead of two
-struct EvalPdf { f3 val; float pdf; };
 template <bool EXT>
 BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if constexpr (EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval_pdf(b, rt, wi, wo, u, v);
+    }
     EvalPdf r;
     r.val = bsdf_eval_body<EXT>(b, rt, wi, wo, u, v);
     r.pdf = is_zero(r.val) ? 0.0f : bsdf_pdf_body<EXT>(b, rt, wi, wo, u, v);
