@@ -156,8 +156,14 @@ public:
         const std::string smpName = sampler->getClass()->getName();
         if (smpName != "SobolSampler" && smpName != "IndependentSampler")
             Log(EError, "%s supports the 'sobol' and 'independent' samplers", getClass()->getName().c_str());
-        if (sensor->getClass()->getName() != "PerspectiveCamera")
-            Log(EError, "only the 'perspective' sensor is supported");
+        /* The 'perspective' plugin registers the concrete class PerspectiveCameraImpl
+           (perspective.cpp:474) under the abstract PerspectiveCamera (sensor.cpp:319);
+           'perspective_rdist' (PerspectiveCameraRDist, perspective_rdist.cpp:556) derives
+           from it too but adds lens distortion, which the library does not model. */
+        if (!sensor->getClass()->derivesFrom(MTS_CLASS(PerspectiveCamera))
+            || sensor->getClass()->getName() != "PerspectiveCameraImpl")
+            Log(EError, "only the 'perspective' sensor is supported (got %s)",
+                sensor->getClass()->getName().c_str());
 #if GPU_INTEGRATOR == 1
         if (sensor->getMedium())
             Log(EError, "gpuvolpath: participating media are not supported");

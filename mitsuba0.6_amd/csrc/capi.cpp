@@ -113,11 +113,10 @@ int hip_fail(mtsgpu_ctx *ctx, hipError_t e, const char *what) {
 
 // Sobol direction numbers as 4-bit XOR tables: [dim][c][v] = XOR of columns
 // 4c..4c+3 of the dimension selected by the bits of v (sobolseq.h:43-57)
-const std::vector<uint32_t> &sobol_nibble_tables() {
-    static std::vector<uint32_t> T;
-    if (!T.empty()) return T;
+// (thread-safe: a static initialised once, group members upload concurrently)
+std::vector<uint32_t> build_sobol_nibble_tables() {
     const std::vector<uint32_t> &M = mtsg_sobol_matrices();
-    T.assign((size_t)MTSG_SOBOL_DIMS * MTSG_NIBBLES * 16, 0u);
+    std::vector<uint32_t> T((size_t)MTSG_SOBOL_DIMS * MTSG_NIBBLES * 16, 0u);
     for (int d = 0; d < MTSG_SOBOL_DIMS; ++d)
         for (int c = 0; c < MTSG_NIBBLES; ++c)
             for (int v = 0; v < 16; ++v) {
@@ -126,6 +125,11 @@ const std::vector<uint32_t> &sobol_nibble_tables() {
                     if ((v >> b) & 1) r ^= M[(size_t)d * MTSG_SOBOL_SIZE + 4 * c + b];
                 T[((size_t)d * MTSG_NIBBLES + c) * 16 + v] = r;
             }
+    return T;
+}
+
+const std::vector<uint32_t> &sobol_nibble_tables() {
+    static const std::vector<uint32_t> T = build_sobol_nibble_tables();
     return T;
 }
 
@@ -571,8 +575,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.ext = H.ext ? 1u : 0u;
     L.ana = H.analytic.empty() ? 0u : 1u;
     // gfx950 has 32 CUs per XCD; the hardware deals workgroups round-robin over
-    // the XCDs of the device (a CPX partition is one XCD: no remap)
-    L.xcds = (uint32_t)std::max(1, ctx->num_cus / 32);
+    // the XCDs of the device (a CPX partition is one XCD: no remap).  A CU count
+    // that is not a multiple of 32 is not a whole-XCD partition: no remap either.
+    L.xcds = (ctx->num_cus % 32 == 0) ? (uint32_t)std::max(1, ctx->num_cus / 32) : 1u;
     L.all_diffuse = std::getenv("MTSGPU_NO_DIFF_VARIANT") ? 0u : 1u;
     for (const MtsgBsdf &b : H.bsdfs) L.all_diffuse &= b.type == MTSGPU_BSDF_DIFFUSE ? 1u : 0u;
     // MIDirectIntegrator::configure / configureSampler (direct.cpp:128-143)
@@ -725,6 +730,9 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         } else {
             const uint64_t blocksNeeded = replay ? (L.units + 255) / 256 : (L.num_items + 255) / 256;
             const int grid = (int)std::min<uint64_t>((uint64_t)ctx->num_cus * bpc, std::max<uint64_t>(1, blocksNeeded));
+            // the replay renders one unit per lane (its own SFMT stream): every unit needs a resident lane
+            if (replay && (uint64_t)grid * 256 < L.units)
+                return fail(ctx, MTSGPU_EINVAL, "SFMT replay: more 32x32 blocks than resident lanes (crop too large)");
             if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
         }
         if ((e = mtsg_launch_reduce(L, stream)) != hipSuccess) return hip_fail(ctx, e, "reduce launch");
@@ -859,7 +867,10 @@ int build_kd_host(const HostScene &H, KdTree &kd, std::vector<MtsgTri> *tg, std:
             for (int k = 0; k < 3; ++k)   // prim_vtx is in global primitive order (only the TriAccel slots are in leaf order)
                 P[9 * (size_t)prim + 3 * v + k] = H.positions[3 * (size_t)H.prim_vtx[4 * (size_t)prim + v] + k];
     }
-    mtsg_build_kdtree(P.data(), (uint32_t)prims, kd, true);
+    if (!mtsg_build_kdtree(P.data(), (uint32_t)prims, kd, true)) {
+        err = "kd-tree: a child offset exceeds KDNode's 28-bit relative field (indirection nodes are not supported)";
+        return MTSGPU_EINVAL;
+    }
     return MTSGPU_OK;
 }
 
@@ -983,8 +994,10 @@ int mtsgpu_debug_sfmt(mtsgpu_ctx *ctx, uint64_t seed, int clone, uint64_t *out, 
     unsigned long long *dout = nullptr;
     hipError_t e;
     (void)hipSetDevice(ctx->device);
-    if ((e = hipMalloc(&dw, MTSG_SFMT_WORDS * 4)) != hipSuccess || (e = hipMalloc(&dout, (size_t)n * 8)) != hipSuccess)
+    if ((e = hipMalloc(&dw, MTSG_SFMT_WORDS * 4)) != hipSuccess || (e = hipMalloc(&dout, (size_t)n * 8)) != hipSuccess) {
+        if (dw) (void)hipFree(dw);
         return hip_fail(ctx, e, "malloc");
+    }
     e = hipMemcpy(dw, st.data(), MTSG_SFMT_WORDS * 4, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = mtsg_launch_sfmt_probe(dw, dout, n, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);

@@ -22,4 +22,6 @@ struct KdTree {
 // tri_positions: 9 floats per primitive (v0, v1, v2, world space), global order.
 // multicore: the reference machine builds above 65536 primitives in parallel
 // (subtrees handed to workers are never retracted).
-void mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, bool multicore = true);
+// false: a child offset exceeds KDNode's 28-bit relative field (the reference
+// then inserts indirection nodes, which are not restated here)
+bool mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, bool multicore = true);

@@ -486,7 +486,7 @@ int log2i(uint32_t v) {   // math::log2i: floor(log2 v)
 
 }  // namespace
 
-void mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, bool multicore) {
+bool mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, bool multicore) {
     out = KdTree();
     Builder B;
     B.P = tri_positions;
@@ -494,7 +494,7 @@ void mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, 
     B.cls.assign(prims, 0);
     if (prims == 0) {   // gkdtree.h:973-979
         out.nodes = {0x80000000u, 0u};
-        return;
+        return true;
     }
     // m_parallelBuild: on above the exact threshold, with more than one core (:981-982, 1036-1038)
     B.parallel = multicore && prims > kExactPrimThreshold;
@@ -530,6 +530,9 @@ void mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, 
             const uint32_t children = nodePtr;
             nodePtr += 2;
             const uint32_t rel = children - it.target;
+            // KDNode's 28-bit relative offset (gkdtree.h:489-505, ERelOffsetLimit); the
+            // reference's indirection nodes past it are not restated: refuse the tree
+            if (rel > (1u << 28) - 1) return false;
             t[0] = (uint32_t)pn.axis | (rel << 2);              // initInnerNode
             std::memcpy(&t[1], &pn.split, 4);
             stack.push_back({pn.left + 1, children + 1});
@@ -541,4 +544,5 @@ void mtsg_build_kdtree(const float *tri_positions, uint32_t prims, KdTree &out, 
     out.stats.nodes = nodePtr;
     out.stats.max_depth = B.maxDepth;
     for (int a = 0; a < 3; ++a) { out.aabb_min[a] = aabb.mn[a]; out.aabb_max[a] = aabb.mx[a]; }
+    return true;
 }

@@ -964,10 +964,10 @@ void envmap_bsphere(HostScene &S, const mtsgpu_sensor_desc &sensor) {
 }  // namespace
 
 // ---- Sobol ------------------------------------------------------------------
-const std::vector<uint32_t> &mtsg_sobol_matrices() {
-    static std::vector<uint32_t> M;
-    if (!M.empty()) return M;
-    M.assign((size_t)MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE, 0u);
+// Built once by a function-local static's initialiser, which C++11 runs
+// exactly once even when several group members upload concurrently.
+static std::vector<uint32_t> build_sobol_matrices() {
+    std::vector<uint32_t> M((size_t)MTSG_SOBOL_DIMS * MTSG_SOBOL_SIZE, 0u);
     for (int k = 0; k < MTSG_SOBOL_SIZE; ++k) M[k] = (uint32_t)(((uint64_t)1 << (MTSG_SOBOL_SIZE - 1 - k)) >> 20);
     const size_t n = sizeof(kJoeKuoParams) / sizeof(kJoeKuoParams[0]);
     size_t i = 0;
@@ -986,6 +986,11 @@ const std::vector<uint32_t> &mtsg_sobol_matrices() {
         for (int k = 0; k < MTSG_SOBOL_SIZE; ++k)
             M[(size_t)(d - 1) * MTSG_SOBOL_SIZE + k] = (uint32_t)((m[k] << (MTSG_SOBOL_SIZE - 1 - k)) >> 20);
     }
+    return M;
+}
+
+const std::vector<uint32_t> &mtsg_sobol_matrices() {
+    static const std::vector<uint32_t> M = build_sobol_matrices();
     return M;
 }
 

@@ -65,3 +65,38 @@ def test_group_rejects_row_stride_and_render_before_upload():
     assert b'row_stride' in g.L.mtsgpu_group_last_error(g.h)
     assert call(it.params(16, 16, 0, 0, 16, 16, 8, 1, 0)) == abi.OK
     g.close()
+
+
+_FRESH_GROUP = r'''
+import sys
+sys.path.insert(0, sys.argv[1])
+from pkgimport import mitsuba_amd
+mitsuba_amd()
+import numpy as np
+from mitsuba_amd import scenes
+from mitsuba_amd.integrator import Context, DeviceGroup
+sc, it = scenes.build('C1', width=64, height=48, spp=4)
+g = DeviceGroup([0, 0, 0, 0])      # first upload of the process: four members build the tables at once
+g.upload(sc)
+film_g, st_g = g.render(it)
+ctx = Context(0)
+ctx.upload(sc)
+film_1, _, _ = ctx.render(it)
+assert np.array_equal(film_g.view(np.uint32), film_1.view(np.uint32)), 'group film differs'
+g.close()
+print('fresh group ok')
+'''
+
+
+def test_group_first_upload_in_fresh_process():
+    """ADVICE r02: the first upload of a process going through a group builds
+    the Sobol tables on several host threads at once (capi.cpp
+    sobol_nibble_tables, scene_build.cpp mtsg_sobol_matrices).  Run it in a
+    fresh child process, with no prior single-context upload."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, '-c', _FRESH_GROUP, repo], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert 'fresh group ok' in r.stdout
