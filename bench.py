@@ -4,9 +4,10 @@
 Workload (BASELINE.json configs[1]): Cornell box, 1280x720, 512 spp, sobol,
 path maxDepth=-1 rrDepth=5, box filter.  One step = one full frame
 (471,859,200 samples = one pass of the hot path over the frame) rendered into
-an HBM-resident film; with N GPUs the frame's rows are sharded (row blocks
-interleaved over ranks, sized so every rank gets the same number of rows) and
-the films are summed onto rank 0 with one RCCL reduce over xGMI (the
+an HBM-resident film; with N GPUs the frame's 8x8 pixel tiles are dealt
+round-robin over the ranks (tile t to rank t % N, MTSGPU_FLAG_TILE_SHARD: every
+rank keeps whole tiles at any N, and the 14,400 tiles of a 1280x720 frame
+split evenly over 1-8 ranks) and the films are summed onto rank 0 with one RCCL reduce over xGMI (the
 reference's Film::put merge, renderproc.cpp:142-149).  Total work is fixed as
 N grows: scaling "strong".
 
@@ -17,7 +18,7 @@ torch.distributed environment, this process starts
 its status; under torch.distributed.run WORLD_SIZE must equal N.
 
 `--device cpu-oracle` is a launcher rehearsal for machines without a GPU (the
-CPU test suite): each rank renders its rows with the CPU oracle and the films
+CPU test suite): each rank renders its tiles with the CPU oracle and the films
 are reduced over gloo.  It is never selected implicitly; the GPU path fails
 loudly when the HIP library or the GPU is missing.
 """
@@ -107,10 +108,11 @@ def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
 
 
 def measured_profile(kind, cfg):
-    """The newest committed summary profiles/<round>_<kind>_<cfg>.json (traffic:
-    HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes,
-    tools/traffic_summary.py; valu: VALU-busy / issue fractions from SQ counters,
-    tools/valu_summary.py); None when none exists."""
+    """The newest committed summary profiles/<round>_<kind>_<cfg>.json, written
+    by tools/traffic_summary.py (traffic: HBM bytes per launch and per sample from
+    separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes; valu: VALU instructions per
+    sample, shader clock, VALU-busy and wait fractions from one SQ pass); None
+    when none exists."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_%s_%s.json' % (kind, cfg))))
     if not files:
@@ -118,6 +120,51 @@ def measured_profile(kind, cfg):
     t = json.load(open(files[-1]))
     t['source'] = os.path.basename(files[-1])
     return t
+
+
+def roofline_line(bps, launch_samples, kernel_s, cfg):
+    """The dominant kernel's roofline, from the live kernel time of this run and
+    per-sample work measured once per build by rocprofv3 (profiles/<round>_*):
+      hbm   -- measured HBM bytes per sample (separate FETCH_SIZE / WRITE_SIZE
+               passes, FETCH doubled per MI355X_MICROARCH.md) x samples / time,
+               against the 8 TB/s HBM3E peak;
+      valu  -- SQ_INSTS_VALU per sample x 64 lanes x samples / time, against the
+               VALU issue peak at the pass's measured shader clock (one wave64
+               VALU instruction per SIMD per 2 cycles = 32 lane-ops/cycle/SIMD,
+               1024 SIMDs; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time).
+    `bound` is the one of the two with the larger fraction; the other is kept,
+    and so is the SURVEY.md 8(d) no-reuse byte model (`hbm_model`)."""
+    traffic = measured_profile('traffic', cfg)
+    valu = measured_profile('valu', cfg)
+    model = {'achieved': round(bps * launch_samples / kernel_s / 1e9, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
+             'frac': round(bps * launch_samples / kernel_s / 1e9 / HBM_PEAK_GBPS, 5),
+             'algorithmic_bytes_per_sample': round(bps, 1),
+             'note': 'no-reuse model: BVH nodes 64 B, TriAccel 48 B, hit/NEE/Sobol/film bytes (bench.py)'}
+    hbm = None
+    if traffic and traffic.get('hbm_bytes_per_sample'):
+        a = traffic['hbm_bytes_per_sample'] * launch_samples / kernel_s / 1e9
+        hbm = {'achieved': round(a, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': round(a / HBM_PEAK_GBPS, 5),
+               'bytes_per_sample': round(traffic['hbm_bytes_per_sample'], 1),
+               'write_bytes_per_sample': traffic.get('write_bytes_per_sample'), 'source': traffic['source']}
+    vl = None
+    if valu and valu.get('valu_insts_per_sample') and valu.get('clock_hz'):
+        a = valu['valu_insts_per_sample'] * 64 * launch_samples / kernel_s / 1e12
+        pk = 1024 * 32 * valu['clock_hz'] / 1e12
+        vl = {'achieved': round(a, 3), 'peak': round(pk, 3), 'unit': 'Tlane-op/s', 'frac': round(a / pk, 5),
+              'valu_insts_per_sample': round(valu['valu_insts_per_sample'], 2),
+              'clock_mhz': round(valu['clock_hz'] / 1e6, 1),
+              'valu_busy_per_simd': round(valu['valu_busy_per_simd'], 4),
+              'wait_frac_per_wave': round(valu['wait_frac_per_wave'], 4), 'source': valu['source']}
+    cands = [(k, v) for k, v in (('hbm', hbm), ('valu', vl)) if v]
+    if not cands:
+        kind, top = 'hbm', model
+    else:
+        kind, top = max(cands, key=lambda kv: kv[1]['frac'])
+    line = {'bound': kind, 'achieved': top['achieved'], 'peak': top['peak'], 'unit': top['unit'], 'frac': top['frac'],
+            'traffic': round(traffic['hbm_bytes_per_sample'] * launch_samples) if hbm else None,
+            'traffic_unit': 'B per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)',
+            'hbm': hbm, 'valu': vl, 'hbm_model': model, 'kernel_ms_avg': round(kernel_s * 1e3, 3)}
+    return line
 
 
 def host_info():
@@ -137,28 +184,54 @@ def host_info():
     return model, os.cpu_count() or 1, avail
 
 
+def cgroup_cpus():
+    """The job's cgroup CPU quota in CPUs (/sys/fs/cgroup/cpu.max: "quota period",
+    or "max"), None when unlimited or unreadable."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else int(q) / int(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(scene, integ, threads):
     """The CPU restatement (oracle, OpenMP, glibc transcendentals as the
     reference) on a bounded sample of the same workload: the full frame at a
-    reduced spp (the first spp Sobol samples of every pixel).  Threads: all
+    reduced spp (the first spp Sobol samples of every pixel, sized by a pilot
+    pass to about 15 s of CPU work).  Threads: all
     cores this job may use -- OMP_NUM_THREADS when the host sets it (the GPU
     boxes give a job a 16-CPU share of a larger machine), else the affinity
-    mask."""
+    mask; never more than the cgroup's CPU quota, which the line records."""
     import copy
     import oracle.binding as ob
     model, ncpu, avail = host_info()
+    quota = cgroup_cpus()
     omp = os.environ.get('OMP_NUM_THREADS')
     if not threads:
         threads = int(omp) if omp and omp.isdigit() and int(omp) > 0 else avail
+        if quota:
+            threads = max(1, min(threads, int(quota)))
     it = copy.copy(integ)
-    it.sampleCount = min(integ.sampleCount, 256)
+    # size the sample to ~15 s of CPU work: a pilot pass (1/32 of the rows at
+    # 8 spp) measures this config's per-sample cost, then the full frame runs
+    # at the spp that fits (1..256, a power of two)
+    it.sampleCount = 8
+    t0 = time.perf_counter()
+    _, _, pst = ob.render(scene, it, libm_mode=0, threads=threads, row=(1, 32, 0))
+    rate = pst['samples'] / max(1e-6, time.perf_counter() - t0)
+    fit = 15.0 * rate / (scene.sensor.width * scene.sensor.height)
+    spp = 1
+    while spp * 2 <= min(integ.sampleCount, 256) and spp * 2 <= fit:
+        spp *= 2
+    it.sampleCount = spp
     t0 = time.perf_counter()
     _, _, st = ob.render(scene, it, libm_mode=0, threads=threads)
     dt = time.perf_counter() - t0
     return {'value': round(st['samples'] / dt / 1e6, 3), 'unit': 'Msamples/s', 'cores': threads, 'kind': 'port',
             'sample': '%dx%d at %d spp (%d samples, %.1f s)' % (scene.sensor.width, scene.sensor.height,
                                                                 it.sampleCount, st['samples'], dt),
-            'cpu_model': model, 'host_cpus': ncpu, 'affinity_cpus': avail, 'omp_num_threads': omp}
+            'cpu_model': model, 'host_cpus': ncpu, 'affinity_cpus': avail, 'omp_num_threads': omp,
+            'cgroup_cpu_quota': quota}
 
 
 def build_scene(args):
@@ -187,10 +260,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     scene, integ = build_scene(args)
     from mitsuba_amd import film_border
-    from mitsuba_amd.distributed import RowSharding
+    from mitsuba_amd.distributed import TileSharding
     W, H, spp = scene.sensor.width, scene.sensor.height, integ.sampleCount
     b = film_border(integ.rfilter, integ.rfilterParam)
-    shard = RowSharding.for_frame(rank, world, H)
+    shard = TileSharding.for_frame(rank, world, H)
     row = shard.row_params()
     gpu = args.device == 'gpu'
 
@@ -212,7 +285,7 @@ def main():
               for _ in range(max(args.steps, 1))]
 
         def step(k=None):   # mtsgpu_render_device clears the film on the stream
-            st = ctx.render_device(integ, film.data_ptr(), stream, row=row)
+            st = ctx.render_device(integ, film.data_ptr(), stream, row=row, tile_shard=shard.tile_shard)
             if k is not None:
                 ev[k][0].record()
             shard.reduce(film, dist)
@@ -231,7 +304,7 @@ def main():
         threads = max(1, (os.cpu_count() or 1) // world)
 
         def step(k=None):
-            f, _, st = ob.render(scene, integ, row=row, threads=threads)
+            f, _, st = ob.render(scene, integ, row=row, threads=threads, tile_shard=shard.tile_shard)
             film.copy_(torch.from_numpy(f.reshape(-1)))
             t = time.perf_counter()
             shard.reduce(film, dist)
@@ -299,16 +372,7 @@ def main():
             bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
             avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
             per_launch_samples = samples_rank / max(1, len(kernel_ms))
-            achieved = bps * per_launch_samples / avg_kernel_s / 1e9
-            traffic = measured_profile('traffic', args.config)
-            roofline = {'bound': 'hbm', 'achieved': round(achieved, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
-                        'frac': round(achieved / HBM_PEAK_GBPS, 5),
-                        'traffic': traffic and {'bytes_per_launch': traffic['hbm_bytes_per_launch'], 'unit': 'B',
-                                                'write_bytes_per_sample': traffic.get('write_bytes_per_sample'),
-                                                'source': traffic['source']},
-                        'valu': measured_profile('valu', args.config),
-                        'algorithmic_bytes_per_sample': round(bps, 1),
-                        'kernel_ms_avg': round(avg_kernel_s * 1e3, 3)}
+            roofline = roofline_line(bps, per_launch_samples, avg_kernel_s, args.config)
             if not args.no_cpu_baseline and world == 1:
                 cpu = cpu_baseline(scene, integ, args.cpu_threads)
         metric = BASELINE_METRIC if args.config == 'C2' and not args.size else \
@@ -320,8 +384,8 @@ def main():
             'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
             'config': {'workload': WORKLOADS.get(args.config, args.config), 'width': W, 'height': H, 'spp': spp,
                        'samples_per_frame': frame_samples,
-                       'parallelism': 'rows sharded x%d (row block %d) + %s film reduce' % (
-                           world, shard.row_block, 'RCCL' if gpu else 'gloo'),
+                       'parallelism': '8x8 tiles dealt over %d rank(s) + %s film reduce' % (
+                           world, 'RCCL' if gpu else 'gloo'),
                        'world_size_reported': dist.get_world_size() if world > 1 else 1,
                        'reduce_ms_max': round(float(r.item()) * 1e3, 3),
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},

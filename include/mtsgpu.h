@@ -234,6 +234,11 @@ enum { MTSGPU_SAMPLER_SOBOL = 0, MTSGPU_SAMPLER_INDEPENDENT = 1,
    the reference (the triangle tested last wins); runs in the wavefront engine,
    path / volpath, triangle scenes only */
 #define MTSGPU_FLAG_KDTREE 8u
+/* shard by 8x8 pixel tiles instead of row blocks: render the tiles t of the
+   window's 8x8 tile grid (row-major, t = (ly / 8) * ceil(width / 8) + lx / 8)
+   with t % row_stride == row_phase (row_block ignored).  Every rank then keeps
+   whole 8x8 tiles at any rank count (the multi-GPU bench's unit) */
+#define MTSGPU_FLAG_TILE_SHARD 16u
 
 /* Film layout produced by mtsgpu_render: an ImageBlock of the full crop
  * (film_width+2b) x (film_height+2b) pixels, 5 floats each {R,G,B,alpha,w},
@@ -339,6 +344,14 @@ int mtsgpu_kdtree_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t n
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */
 int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *out, int n);
 int mtsgpu_debug_scene_info(mtsgpu_ctx *ctx, uint32_t *info4);
+/* Diagnostics (tests/test_gpu_libm.py): out[i] = f(a[i], b[i]) by the kernels'
+ * own transcendentals (glibc's float libm restated, glibc_f32.h; double exp/log
+ * for math::fastexp/fastlog, include/mitsuba/core/math.h:185-199).  fn: 0 sin and
+ * 1 cos (of sincosf), 2 expf, 3 acosf, 4 atanf, 5 tanf, 6 atan2f(a, b),
+ * 7 powf(a, b), 8 fastexp, 9 fastlog.  With a == NULL, a[i] is the float whose
+ * bits are first + i (b may be NULL for the unary functions).  Host buffers. */
+int mtsgpu_debug_libm(mtsgpu_ctx *ctx, int fn, const float *a, const float *b, float *out, size_t n,
+                      uint32_t first);
 /* the 16 raw device counters of the last render (samples, rays, shadow rays,
    path lengths, node visits, TriAccel tests, dimension errors, hits, -, NEE
    samples, Sobol HBM words, diagnostic section cycles 11-15) */

@@ -93,6 +93,7 @@ FLAG_TRAVERSAL_STATS = 1
 FLAG_WAVEFRONT = 2
 FLAG_MEGAKERNEL = 4
 FLAG_KDTREE = 8                          # trace through the reference's kd-tree (wavefront engine)
+FLAG_TILE_SHARD = 16                     # row_stride/row_phase interleave 8x8 tiles, not row blocks
 
 
 class DevelopParams(C.Structure):

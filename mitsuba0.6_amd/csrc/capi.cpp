@@ -26,6 +26,8 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
+hipError_t mtsg_launch_libm_probe(int fn, const float *a, const float *b, float *out, size_t n, uint32_t first,
+                                  hipStream_t s);
 hipError_t mtsg_launch_trace(const MtsgDeviceScene &S, const float *rays, uint32_t n, float *out, bool shadow,
                              uint32_t stackDepth, int numCUs, hipStream_t stream);
 hipError_t mtsg_launch_trace_kd(const MtsgDeviceScene &S, const uint32_t *kdNodes, const uint32_t *kdIndices,
@@ -526,11 +528,19 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.row_block = P->row_block ? P->row_block : 1;
     L.row_stride = P->row_stride ? P->row_stride : 1;
     L.row_phase = P->row_phase % L.row_stride;
-    // work decomposition: compact rows (interleave) x columns in 8x8 tiles
-    const uint32_t rowsCompact = ((P->height + L.row_block - 1) / L.row_block + L.row_stride - 1) / L.row_stride * L.row_block;
+    // work decomposition: compact rows (interleave) x columns in 8x8 tiles, or
+    // (MTSGPU_FLAG_TILE_SHARD) every row_stride-th 8x8 tile of the window
+    L.tile_shard = (P->flags & MTSGPU_FLAG_TILE_SHARD) ? 1u : 0u;
     L.tiles_x = (P->width + 7) / 8;
-    const uint32_t tilesY = (rowsCompact + 7) / 8;
-    L.num_pixels = L.tiles_x * tilesY * 64;
+    if (L.tile_shard) {
+        const uint64_t tiles = (uint64_t)L.tiles_x * ((P->height + 7) / 8);
+        L.num_pixels = (uint32_t)((tiles + L.row_stride - 1) / L.row_stride * 64);
+    } else {
+        const uint32_t rowsCompact =
+            ((P->height + L.row_block - 1) / L.row_block + L.row_stride - 1) / L.row_stride * L.row_block;
+        const uint32_t tilesY = (rowsCompact + 7) / 8;
+        L.num_pixels = L.tiles_x * tilesY * 64;
+    }
     // Sobol index width: frame << 2m | 2m bits (sobolseq.h:93-125); 52 columns per dimension
     // the direct integrator's 2D sample arrays index the Sobol sequence at spp x count
     const bool direct = P->integrator == MTSGPU_INTEGRATOR_DIRECT;
@@ -980,6 +990,26 @@ int mtsgpu_debug_arith(mtsgpu_ctx *ctx, const float *a, const float *b, float *o
     if (e == hipSuccess) e = hipMemcpy(out, dout, (size_t)n * 32, hipMemcpyDeviceToHost);
     (void)hipFree(da); (void)hipFree(db); (void)hipFree(dout);
     return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "arith probe");
+}
+
+// diagnostics: the device's transcendentals over inputs (tests/test_gpu_libm.py)
+int mtsgpu_debug_libm(mtsgpu_ctx *ctx, int fn, const float *a, const float *b, float *out, size_t n,
+                      uint32_t first) {
+    if (!ctx || !out || n == 0 || fn < 0 || fn > 9 || ((fn == 6 || fn == 7) && a && !b)) return MTSGPU_EINVAL;
+    (void)hipSetDevice(ctx->device);
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc(&dout, n * 4);
+    if (e == hipSuccess && a) e = hipMalloc(&da, n * 4);
+    if (e == hipSuccess && b) e = hipMalloc(&db, n * 4);
+    if (e == hipSuccess && a) e = hipMemcpy(da, a, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess && b) e = hipMemcpy(db, b, n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mtsg_launch_libm_probe(fn, da, db, dout, n, first, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost);
+    if (da) (void)hipFree(da);
+    if (db) (void)hipFree(db);
+    if (dout) (void)hipFree(dout);
+    return e == hipSuccess ? MTSGPU_OK : hip_fail(ctx, e, "libm probe");
 }
 
 // diagnostics: n nextULong draws of the device's SFMT19937 from Random(seed), or

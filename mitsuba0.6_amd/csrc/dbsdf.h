@@ -22,6 +22,23 @@ enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
 #else
 #define BSDF_CALL __device__ __noinline__
 #endif
+// A/B experiments (profiles/r03_ab_*): BSDF-set-specialised builds
+#ifdef MTSG_SPEC_DISTR
+#define DTYPE(d) (MTSG_SPEC_DISTR)
+#else
+#define DTYPE(d) ((d).type)
+#endif
+#ifdef MTSG_HELPER_INLINE
+#define HELPER_CALL __device__ __forceinline__
+#else
+#define HELPER_CALL __device__ __noinline__
+#endif
+#ifndef MTSG_SPEC_HAS_RC
+#define MTSG_SPEC_HAS_RC 1
+#endif
+#ifndef MTSG_SPEC_HAS_RD
+#define MTSG_SPEC_HAS_RD 1
+#endif
 enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2, BSDF_ROUGHPLASTIC = 3,
        BSDF_CONDUCTOR = 4, BSDF_DIELECTRIC = 5, BSDF_PLASTIC = 6, BSDF_TWOSIDED = 7 };   // = MTSGPU_BSDF_*
 
@@ -55,7 +72,7 @@ __device__ __forceinline__ f3 square_to_cosine_hemisphere(float sx, float sy) {
 }
 
 // ---- math.cpp --------------------------------------------------------------
-__device__ __noinline__ float m_erfinv(float x) {
+HELPER_CALL float m_erfinv(float x) {
     float w = -d_fastlog(((float)1 - x) * ((float)1 + x));
     float p;
     if (w < (float)5) {
@@ -125,14 +142,14 @@ __device__ __forceinline__ float distr_interp_phong(const Distr &d, f3 v) {   //
     return d.expU * (v.x * v.x * inv) + d.expV * (v.y * v.y * inv);
 }
 
-__device__ __noinline__ float distr_eval(Distr d, f3 m) {   // :191-238
+HELPER_CALL float distr_eval(Distr d, f3 m) {   // :191-238
     if (m.z <= 0) return 0.0f;
     float cosTheta2 = m.z * m.z;
     float be = ((m.x * m.x) / (d.alphaU * d.alphaU) + (m.y * m.y) / (d.alphaV * d.alphaV)) / cosTheta2;
     float result;
-    if (d.type == DISTR_BECKMANN) {
+    if (DTYPE(d) == DISTR_BECKMANN) {
         result = d_fastexp(-be) / (D_PI * d.alphaU * d.alphaV * cosTheta2 * cosTheta2);
-    } else if (d.type == DISTR_GGX) {
+    } else if (DTYPE(d) == DISTR_GGX) {
         float root = ((float)1 + be) * cosTheta2;
         result = (float)1 / (D_PI * d.alphaU * d.alphaV * root * root);
     } else {
@@ -151,12 +168,12 @@ __device__ __forceinline__ float distr_project_roughness(const Distr &d, f3 v) {
     return dsqrt(cosPhi2 * d.alphaU * d.alphaU + sinPhi2 * d.alphaV * d.alphaV);
 }
 
-__device__ __noinline__ float distr_smithG1(Distr d, f3 v, f3 m) {   // :477-518
+HELPER_CALL float distr_smithG1(Distr d, f3 v, f3 m) {   // :477-518
     if (dot(v, m) * v.z <= 0) return 0.0f;
     float tanTheta = fabsf(tan_theta(v));
     if (tanTheta == 0.0f) return 1.0f;
     float alpha = distr_project_roughness(d, v);
-    if (d.type == DISTR_GGX) {
+    if (DTYPE(d) == DISTR_GGX) {
         float root = alpha * tanTheta;
         return 2.0f / (1.0f + m_hypot2((float)1.0f, root));
     }
@@ -175,7 +192,7 @@ __device__ __forceinline__ void distr_first_quadrant(const Distr &d, float u1, f
 
 __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy, float &pdf) {  // :287-402
     float cosThetaM = 0.0f, sinPhiM, cosPhiM, alphaSqr;
-    if (d.type != DISTR_PHONG) {
+    if (DTYPE(d) != DISTR_PHONG) {
         if (distr_iso(d)) {
             d_sincos((2.0f * D_PI) * sy, &sinPhiM, &cosPhiM);
             alphaSqr = d.alphaU * d.alphaU;
@@ -185,7 +202,7 @@ __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy,
             float cosSc = cosPhiM / d.alphaU, sinSc = sinPhiM / d.alphaV;
             alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
         }
-        if (d.type == DISTR_BECKMANN) {
+        if (DTYPE(d) == DISTR_BECKMANN) {
             float tanThetaMSqr = alphaSqr * -d_fastlog(1.0f - sx);
             cosThetaM = 1.0f / dsqrt(1.0f + tanThetaMSqr);
             pdf = (1.0f - sx) / (D_PI * d.alphaU * d.alphaV * cosThetaM * cosThetaM * cosThetaM);
@@ -226,7 +243,7 @@ __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy,
 __device__ __forceinline__ void distr_sample_visible11_impl(Distr d, float thetaI, float sx, float sy,
                                                            float &slx, float &sly) {   // :573-670
     const float SQRT_PI_INV = 1 / dsqrt(D_PI);
-    if (d.type == DISTR_BECKMANN) {
+    if (DTYPE(d) == DISTR_BECKMANN) {
         if (thetaI < 1e-4f) {
             float s, c;
             float r = dsqrt(-d_fastlog(1.0f - sx));
@@ -284,12 +301,12 @@ __device__ __forceinline__ void distr_sample_visible11_impl(Distr d, float theta
 // out-of-line entry points return their results by value (no stack round trip)
 struct F2 { float x, y; };
 struct MPdf { f3 m; float pdf; };
-__device__ __noinline__ F2 distr_sample_visible11(Distr d, float thetaI, float sx, float sy) {
+HELPER_CALL F2 distr_sample_visible11(Distr d, float thetaI, float sx, float sy) {
     F2 r;
     distr_sample_visible11_impl(d, thetaI, sx, sy, r.x, r.y);
     return r;
 }
-__device__ __noinline__ MPdf distr_sample_all(Distr d, float sx, float sy) {
+HELPER_CALL MPdf distr_sample_all(Distr d, float sx, float sy) {
     MPdf r;
     r.m = distr_sample_all_impl(d, sx, sy, r.pdf);
     return r;
@@ -334,7 +351,7 @@ __device__ __forceinline__ f3 distr_sample(const Distr &d, f3 wi, float sx, floa
 }
 __device__ __forceinline__ void distr_scale_alpha(Distr &d, float v) {              // :181-186
     d.alphaU *= v; d.alphaV *= v;
-    if (d.type == DISTR_PHONG) distr_phong_exp(d);
+    if (DTYPE(d) == DISTR_PHONG) distr_phong_exp(d);
 }
 
 // ---- Fresnel (util.cpp) -------------------------------------------------
@@ -351,7 +368,7 @@ __device__ __forceinline__ float fresnel_dielectric_ext(float cosThetaI_, float 
     return 0.5f * (Rs * Rs + Rp * Rp);
 }
 __device__ __forceinline__ f3 s_safe_sqrt(f3 a) { return mk(safe_sqrt(a.x), safe_sqrt(a.y), safe_sqrt(a.z)); }
-__device__ __noinline__ f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {   // util.cpp:739-761
+HELPER_CALL f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {   // util.cpp:739-761
     float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
     f3 temp1 = sub(sub(mulv(eta, eta), mulv(k, k)), mk(sinThetaI2, sinThetaI2, sinThetaI2));
     f3 a2pb2 = s_safe_sqrt(add(mulv(temp1, temp1), mul(mulv(mulv(mulv(k, k), eta), eta), 4)));
@@ -531,15 +548,15 @@ __device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
     result += probDiffuse * (D_INV_PI * wo.z);
     return result;
 }
-__device__ __noinline__ f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+BSDF_CALL f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     return rp_eval_body(b, rt, wi, wo, u, v);
 }
-__device__ __noinline__ float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+BSDF_CALL float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     return rp_pdf_body(b, rt, wi, wo, u, v);
 }
 struct EvalPdf { f3 val; float pdf; };
 // eval, and pdf where the value is nonzero, of one query in one call (NEE)
-__device__ __noinline__ EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+BSDF_CALL EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     EvalPdf r;
     r.val = rp_eval_body(b, rt, wi, wo, u, v);
     r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body(b, rt, wi, wo, u, v);
@@ -643,7 +660,7 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
         if (b.type == BSDF_ROUGHPLASTIC) return rp_eval(b, rt, wi, wo, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
     }
-    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:257-292
+    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:257-292
         if (wi.z <= 0 || wo.z <= 0) return zero;
         f3 H = normalize(add(wo, wi));
         Distr d = bsdf_distr<EXT>(b, u, v);
@@ -654,6 +671,7 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
         float model = D * G / (4.0f * wi.z);
         return mul(F, model);
     }
+    if (!MTSG_SPEC_HAS_RD) return zero;
     if (wi.z == 0) return zero;                                            // roughdielectric.cpp:270-346
     bool reflect = wi.z * wo.z > 0;
     f3 H;
@@ -691,13 +709,14 @@ __device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 
         if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf(b, rt, wi, wo, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
     }
-    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:294-319
+    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:294-319
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         f3 H = normalize(add(wo, wi));
         Distr d = bsdf_distr<EXT>(b, u, v);
         if (b.sample_visible) return distr_eval(d, H) * distr_smithG1(d, wi, H) / (4.0f * wi.z);
         return distr_pdf(d, wi, H) / (4 * absdot(wo, H));
     }
+    if (!MTSG_SPEC_HAS_RD) return 0.0f;
     bool reflect = wi.z * wo.z > 0;                                        // roughdielectric.cpp:348-405
     f3 H;
     float dwh_dwo;
@@ -748,7 +767,7 @@ BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, fl
 // the caller, which draws it from the sampler only for that BSDF.
 
 // RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458)
-__device__ __noinline__ BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v) {
+BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (wi.z <= 0) return r;
@@ -795,7 +814,7 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         if (b.type == BSDF_ROUGHPLASTIC) return rp_sample(b, rt, wi, sx, sy, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
     }
-    if (b.type == BSDF_ROUGHCONDUCTOR) {                                   // roughconductor.cpp:357-406
+    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:357-406
         if (wi.z < 0) return r;
         Distr d = bsdf_distr<EXT>(b, u, v);
         float pdf;
@@ -814,6 +833,7 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         r.weight = mul(F, weight);
         return r;
     }
+    if (!MTSG_SPEC_HAS_RD) return r;
     Distr d = bsdf_distr<EXT>(b, u, v);                                    // roughdielectric.cpp:525-615
     Distr sd = d;
     if (!b.sample_visible) distr_scale_alpha(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));

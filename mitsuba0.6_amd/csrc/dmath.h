@@ -3,13 +3,15 @@
 // Single-precision, evaluated in the reference's expression order (the whole
 // library is built with -ffp-contract=off: the reference's x86 SSE build has
 // no FMA).  Division and sqrt are IEEE correctly rounded
-// (-fhip-fp32-correctly-rounded-divide-sqrt).  Transcendentals the reference
-// takes from glibc are computed in double precision and rounded once to float
-// (math::fastexp/fastlog already are double in the reference,
-// include/mitsuba/core/math.h:175-216).
+// (-fhip-fp32-correctly-rounded-divide-sqrt).  The transcendentals the
+// reference takes from glibc are glibc's own algorithms (glibc_f32.h);
+// math::fastexp/fastlog are double precision in the reference too
+// (include/mitsuba/core/math.h:175-216).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "glibc_f32.h"
 
 #define D_EPSILON 1e-4f            // constants.h:28
 #define D_SHADOW_EPSILON 1e-3f     // constants.h:29
@@ -47,8 +49,9 @@ __device__ __forceinline__ float safe_sqrt(float v) { return dsqrt(smax(0.0f, v)
 __device__ __forceinline__ float signum(float v) { return copysignf(1.0f, v); }         // math.h:270
 __device__ __forceinline__ float smaxc(f3 s) { float r = s.x; r = smax(r, s.y); r = smax(r, s.z); return r; }
 
-// libm (glibc in the reference) -> double precision, rounded once
-#ifdef MTSG_ABL_FAST_LIBM   // timing ablation only (not parity-exact): single-precision libm
+// libm: glibc's float routines restated bit for bit (glibc_f32.h);
+// math::fastexp/fastlog are double exp/log in the reference (math.h:185-199)
+#ifdef MTSG_ABL_FAST_LIBM   // timing ablation only (not parity-exact): single-precision device libm
 __device__ __forceinline__ void d_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
 __device__ __forceinline__ float d_acos(float x) { return acosf(x); }
 __device__ __forceinline__ float d_atan2(float y, float x) { return atan2f(y, x); }
@@ -59,17 +62,13 @@ __device__ __forceinline__ float d_powf(float x, float y) { return powf(x, y); }
 __device__ __forceinline__ float d_fastexp(float x) { return expf(x); }
 __device__ __forceinline__ float d_fastlog(float x) { return logf(x); }
 #else
-__device__ __forceinline__ void d_sincos(float x, float *s, float *c) {
-    double sd, cd;
-    sincos((double)x, &sd, &cd);
-    *s = (float)sd; *c = (float)cd;
-}
-__device__ __forceinline__ float d_acos(float x) { return (float)acos((double)x); }
-__device__ __forceinline__ float d_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __forceinline__ float d_tan(float x) { return (float)tan((double)x); }
-__device__ __forceinline__ float d_atan(float x) { return (float)atan((double)x); }
-__device__ __forceinline__ float d_expf(float x) { return (float)exp((double)x); }
-__device__ __forceinline__ float d_powf(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __forceinline__ void d_sincos(float x, float *s, float *c) { glf_sincosf(x, s, c); }
+__device__ __forceinline__ float d_acos(float x) { return glf_acosf(x); }
+__device__ __forceinline__ float d_atan2(float y, float x) { return glf_atan2f(y, x); }
+__device__ __forceinline__ float d_tan(float x) { return glf_tanf(x); }
+__device__ __forceinline__ float d_atan(float x) { return glf_atanf(x); }
+__device__ __forceinline__ float d_expf(float x) { return glf_expf(x); }
+__device__ __forceinline__ float d_powf(float x, float y) { return glf_powf(x, y); }
 __device__ __forceinline__ float d_fastexp(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float d_fastlog(float x) { return (float)log((double)x); }
 #endif

@@ -233,6 +233,7 @@ struct MtsgLaunch {
     int32_t film_w, film_h, fw, fh;   // image size and film size incl. borders
     uint32_t x0, y0, width, height;
     uint32_t row_block, row_stride, row_phase;
+    uint32_t tile_shard;              // MTSGPU_FLAG_TILE_SHARD: row_stride/row_phase interleave 8x8 tiles
     // work decomposition: items = (sample j in [j0, j0 + chunk_spp)) x (compact pixel p in [0, num_pixels))
     uint32_t tiles_x;                 // 8x8 pixel tiles across the window
     uint32_t num_pixels;              // compact pixels incl. padding of partial tiles

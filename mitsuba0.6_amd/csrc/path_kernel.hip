@@ -917,9 +917,18 @@ __device__ __noinline__ EnvSample const_sample_direct(glb_env *E, f3 ref, f3 ref
     return r;
 }
 
-// compact pixel index (8x8 tiles over the window's active rows) -> image pixel
+// compact pixel index (8x8 tiles over the window's active rows, or the
+// window's every row_stride-th tile) -> image pixel
 __device__ __forceinline__ bool pixel_of(const MtsgLaunch &L, uint32_t p, int &px, int &py) {
     const uint32_t tile = p >> 6, in = p & 63;
+    if (L.tile_shard) {
+        const uint32_t t = tile * L.row_stride + L.row_phase;
+        const uint32_t lx = (t % L.tiles_x) * 8 + (in & 7), ly = (t / L.tiles_x) * 8 + (in >> 3);
+        if (lx >= L.width || ly >= L.height) return false;
+        px = (int)(L.x0 + lx);
+        py = (int)(L.y0 + ly);
+        return true;
+    }
     const uint32_t lx = (tile % L.tiles_x) * 8 + (in & 7);
     const uint32_t r = (tile / L.tiles_x) * 8 + (in >> 3);
     if (lx >= L.width) return false;

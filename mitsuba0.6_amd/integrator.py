@@ -30,7 +30,7 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_debug_sfmt', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
            'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
-           'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host']
+           'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm']
 
 _lib = None
 
@@ -64,6 +64,8 @@ def load_library(path=None):
     L.mtsgpu_debug_scene_info.argtypes = [C.c_void_p, P(C.c_uint32)]
     L.mtsgpu_debug_counters.argtypes = [C.c_void_p, P(C.c_uint64)]
     L.mtsgpu_debug_sfmt.argtypes = [C.c_void_p, C.c_uint64, C.c_int, P(C.c_uint64), C.c_int]
+    L.mtsgpu_debug_libm.argtypes = [C.c_void_p, C.c_int, P(C.c_float), P(C.c_float), P(C.c_float), C.c_size_t,
+                                    C.c_uint32]
     L.mtsgpu_trace_rays.argtypes = [C.c_void_p, P(C.c_float), C.c_uint32, C.c_int, P(C.c_float), P(C.c_double)]
     L.mtsgpu_check_scene.argtypes = [P(abi.SceneDesc), C.c_char_p, C.c_size_t]
     L.mtsgpu_develop.argtypes = [C.c_void_p, P(abi.DevelopParams), P(C.c_float), C.c_void_p]
@@ -173,16 +175,21 @@ class Context:
             return abi.FLAG_KDTREE
         raise ValueError('engine must be None, "wavefront", "megakernel" or "kdtree"')
 
-    def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False, engine=None):
+    def render(self, integ, window=None, samples=False, row=(0, 1, 0), traversal_stats=False, engine=None,
+               tile_shard=False):
         """Returns (film (H+2b, W+2b, 5) float32, per-sample records or None, stats dict).
         engine: None (the library's default), 'wavefront', 'megakernel' or 'kdtree'
-        (the wavefront engine tracing through the reference's kd-tree)."""
+        (the wavefront engine tracing through the reference's kd-tree).
+        row = (row_block, row_stride, row_phase); tile_shard: row_stride/row_phase
+        select 8x8 tiles (MTSGPU_FLAG_TILE_SHARD) instead of row blocks."""
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
         x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
         if traversal_stats:
             p.flags |= abi.FLAG_TRAVERSAL_STATS
+        if tile_shard:
+            p.flags |= abi.FLAG_TILE_SHARD
         p.flags |= self._engine_flags(engine)
         b = film_border(integ.rfilter, integ.rfilterParam)
         film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
@@ -193,11 +200,14 @@ class Context:
                                           C.byref(st)))
         return film, smp, st.as_dict()
 
-    def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0), engine=None):
+    def render_device(self, integ, film_ptr, stream_ptr=None, window=None, row=(0, 1, 0), engine=None,
+                      tile_shard=False):
         sc = self.scene
         W, H = sc.sensor.width, sc.sensor.height
         x0, y0, w, h = window if window else (integ.crop or (0, 0, W, H))
         p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+        if tile_shard:
+            p.flags |= abi.FLAG_TILE_SHARD
         p.flags |= self._engine_flags(engine)
         st = abi.Stats()
         self._check(self.L.mtsgpu_render_device(self.h, C.byref(p), C.c_void_p(film_ptr),
@@ -249,6 +259,24 @@ class Context:
         flags = (abi.TRACE_SHADOW if shadow else 0) | (abi.TRACE_KDTREE if kdtree else 0)
         self._check(self.L.mtsgpu_trace_rays_ex(self.h, abi.fptr(rays), n, flags, abi.fptr(hits), C.byref(ms)))
         return hits, ms.value
+
+    LIBM_FNS = ('sin', 'cos', 'expf', 'acosf', 'atanf', 'tanf', 'atan2f', 'powf', 'fastexp', 'fastlog')
+
+    def debug_libm(self, fn, a=None, b=None, first=0, n=None):
+        """The device's transcendental `fn` (LIBM_FNS name or id) over a (and b),
+        or over the n floats whose bits are first, first+1, ..."""
+        fid = self.LIBM_FNS.index(fn) if isinstance(fn, str) else int(fn)
+        P = C.POINTER(C.c_float)
+        if a is not None:
+            a = np.ascontiguousarray(a, np.float32)
+            n = a.size
+        if b is not None:
+            b = np.ascontiguousarray(b, np.float32)
+        out = np.empty(n, np.float32)
+        self._check(self.L.mtsgpu_debug_libm(self.h, fid, abi.fptr(a) if a is not None else P(),
+                                             abi.fptr(b) if b is not None else P(), abi.fptr(out), n,
+                                             C.c_uint32(first)))
+        return out
 
     def debug_arith(self, a, b):
         a = np.ascontiguousarray(a, np.float32)

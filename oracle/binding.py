@@ -127,11 +127,12 @@ def configure_rc(scene):
     return lib().oracle_configure(C.byref(d))
 
 
-def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row=(0, 1, 0), variant='strict',
-           kdtree=None):
+def render(scene, integ, window=None, libm_mode=0, threads=1, samples=False, row=(0, 1, 0), variant='strict',
+           kdtree=None, tile_shard=False):
     """Render with the oracle; returns (film (H+2b, W+2b, 5), samples or None, stats dict).
     variant='refflags' renders with the reference-flags build (lib()).
-    kdtree=(nodes, indices): every ray query traverses that kd-tree (Havran)."""
+    kdtree=(nodes, indices): every ray query traverses that kd-tree (Havran).
+    tile_shard: row = (-, stride, phase) selects 8x8 tiles t % stride == phase."""
     import sys
     sys.path.insert(0, os.path.dirname(HERE))
     from pkgimport import mitsuba_amd
@@ -140,6 +141,8 @@ def render(scene, integ, window=None, libm_mode=1, threads=1, samples=False, row
     W, H = scene.sensor.width, scene.sensor.height
     x0, y0, w, h = window if window else (getattr(integ, 'crop', None) or (0, 0, W, H))
     p = integ.params(W, H, x0, y0, w, h, row[0], row[1], row[2])
+    if tile_shard:
+        p.flags |= m.abi.FLAG_TILE_SHARD
     b = m.film_border(integ.rfilter, integ.rfilterParam)
     film = np.zeros((H + 2 * b, W + 2 * b, 5), np.float32)
     smp = np.zeros((w * h * integ.sampleCount, m.abi.SAMPLE_RECORD_FLOATS), np.float32) if samples else None

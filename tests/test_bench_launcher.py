@@ -1,9 +1,10 @@
 """bench.py's N-rank launcher (the driver's `python bench.py --gpus N`), rehearsed
 on CPU: the parent starts torch.distributed.run with N ranks before touching a
-GPU, each rank renders its row blocks (here with the CPU oracle,
-`--device cpu-oracle`; on the GPUs the HIP path with the same row parameters)
+GPU, each rank renders its 8x8 tiles (here with the CPU oracle,
+`--device cpu-oracle`; on the GPUs the HIP path with the same tile parameters)
 and the films are reduced onto rank 0 (gloo here, RCCL on the GPUs).  The
-reduced film must equal the single-process frame bit for bit."""
+reduced film must equal the single-process frame bit for bit, at 2, 4 and 8
+ranks."""
 import json
 import os
 import subprocess
@@ -27,13 +28,14 @@ def _bench(tmp_path, gpus, name):
     return json.loads(lines[0]), np.load(out)
 
 
-def test_two_rank_launch_equals_single_process(tmp_path):
-    r2, f2 = _bench(tmp_path, 2, 'f2.npy')
+def test_multi_rank_launch_equals_single_process(tmp_path):
     r1, f1 = _bench(tmp_path, 1, 'f1.npy')
-    assert r2['n_gpus'] == 2 and r2['config']['world_size_reported'] == 2
     assert r1['n_gpus'] == 1
-    assert r2['config']['samples_per_frame'] == r1['config']['samples_per_frame'] == 40 * 36 * 4
-    assert np.array_equal(f1.view(np.uint32), f2.view(np.uint32))
+    for n in (2, 4, 8):
+        rn, fn = _bench(tmp_path, n, 'f%d.npy' % n)
+        assert rn['n_gpus'] == n and rn['config']['world_size_reported'] == n
+        assert rn['config']['samples_per_frame'] == r1['config']['samples_per_frame'] == 40 * 36 * 4
+        assert np.array_equal(f1.view(np.uint32), fn.view(np.uint32)), n
 
 
 def test_world_size_mismatch_fails(tmp_path):

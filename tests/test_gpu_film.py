@@ -54,7 +54,7 @@ def test_develop_rendered_film_and_exr(gpu_ctx, oracle, tmp_path):
     it.rfilter = 'gaussian'
     gpu_ctx.upload(sc)
     film_g, _, _ = gpu_ctx.render(it)
-    film_o, _, _ = oracle.render(sc, it, libm_mode=1)
+    film_o, _, _ = oracle.render(sc, it, libm_mode=0)
     from mitsuba_amd.scene import film_border
     b = film_border(it.rfilter, it.rfilterParam)
     hf = F.HDRFilm(banner=False)

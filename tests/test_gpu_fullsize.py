@@ -41,7 +41,7 @@ def test_c1_full_frame_bitexact(gpu_ctx, oracle):
     assert (sc.sensor.width, sc.sensor.height, it.sampleCount) == (512, 512, 64)
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1, threads=THREADS)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0, threads=THREADS)
     assert st_g['samples'] == st_o['samples'] == 512 * 512 * 64
     _records_equal(smp_g, smp_o)
     for k in ('rays', 'shadow_rays', 'path_length_sum'):
@@ -57,7 +57,7 @@ def test_full_resolution_row_band_bitexact(gpu_ctx, oracle, cfg, rows):
     win = (0, rows[0], W, rows[1])
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, window=win, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, window=win, samples=True, libm_mode=1, threads=THREADS)
+    film_o, smp_o, st_o = oracle.render(sc, it, window=win, samples=True, libm_mode=0, threads=THREADS)
     assert st_g['samples'] == st_o['samples'] == W * rows[1] * it.sampleCount
     _records_equal(smp_g, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']

@@ -2,8 +2,9 @@
 sample sequences.
 
 Bar: per-sample Li (RGB), alpha, sample position and path
-depth bit-identical to the oracle run with correctly-rounded transcendentals
-(libm_mode=1, the device's libm); the film bit-identical except pixels that
+depth bit-identical to the oracle run with glibc's transcendentals
+(libm_mode=0, as the reference calls them; the device computes glibc's
+algorithms, csrc/glibc_f32.h); the film bit-identical except pixels that
 received spill splats (|u| within 1e-5 of a pixel edge), which match to 1e-6
 relative (float atomics change the summation order).
 """
@@ -39,7 +40,7 @@ def test_cornell_small_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C1', width=64, height=48, spp=8)
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['samples'] == st_o['samples'] == 64 * 48 * 8
     assert st_g['rays'] == st_o['rays']
@@ -53,7 +54,7 @@ def test_cornell_window_and_gaussian(gpu_ctx, oracle):
     gpu_ctx.upload(sc)
     win = (17, 9, 40, 33)
     film_g, smp_g, _ = gpu_ctx.render(it, window=win, samples=True)
-    film_o, smp_o, _ = oracle.render(sc, it, window=win, samples=True, libm_mode=1)
+    film_o, smp_o, _ = oracle.render(sc, it, window=win, samples=True, libm_mode=0)
     assert np.all(_bits(smp_g) == _bits(smp_o))
     np.testing.assert_allclose(film_g, film_o, rtol=2e-6, atol=1e-6)
 
@@ -75,7 +76,7 @@ def test_rough_bsdfs_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C1', width=48, height=40, spp=16, materials='rough')
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -88,7 +89,7 @@ def test_rough_bsdfs_all_materials(gpu_ctx, oracle):
         sc.meshes[6].bsdf = 3 + mi
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
-        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
+        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o, repr(mi))
 
 
@@ -104,7 +105,7 @@ def test_envmap_bitexact(gpu_ctx, oracle):
     sc, it = _c3_small()
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -117,7 +118,7 @@ def test_envmap_variants(gpu_ctx, oracle):
         it.hideEmitters = hide
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
-        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
+        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o, repr((kw, hide)))
 
 
@@ -127,7 +128,7 @@ def test_atrium_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C4', width=48, height=27, spp=4)
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1, threads=8)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0, threads=8)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -140,7 +141,7 @@ def test_xml_scene_bitexact(gpu_ctx, oracle, tmp_path):
     sc2, it2 = load_scene(save_scene(sc, it, str(tmp_path)))
     gpu_ctx.upload(sc2)
     film_g, smp_g, _ = gpu_ctx.render(it2, samples=True)
-    film_o, smp_o, _ = oracle.render(sc2, it2, samples=True, libm_mode=1)
+    film_o, smp_o, _ = oracle.render(sc2, it2, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
 
 
@@ -151,7 +152,7 @@ def test_roughplastic_and_textures_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C1', width=48, height=40, spp=16, materials='plastic')
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -162,7 +163,7 @@ def test_c5_textured_roughplastic_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C5', width=48, height=27, spp=8, env_size=(128, 64), blob=(60, 38))
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
 
 
@@ -173,7 +174,7 @@ def test_smooth_bsdfs_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C1', width=48, height=40, spp=16, materials='smooth')
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -186,7 +187,7 @@ def test_smooth_bsdfs_all_materials(gpu_ctx, oracle):
         sc.meshes[6].bsdf = 3 + mi
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
-        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
+        film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o, repr(mi))
 
 
@@ -197,7 +198,7 @@ def test_analytic_shapes_bitexact(gpu_ctx, oracle):
     sc, it = scenes.build('C1', width=48, height=48, spp=16, materials='shapes')
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -214,7 +215,7 @@ def test_analytic_shapes_under_envmap(gpu_ctx, oracle):
                           bsdf=b))
     gpu_ctx.upload(sc)
     film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=0)
     _assert_records_equal(smp_g, smp_o)
 
 
@@ -229,7 +230,7 @@ def test_constant_emitter_bitexact(gpu_ctx, oracle):
     sc.meshes.append(Mesh(shape='sphere', center=(-1.6, 0.7, 0.3), radius=0.7, bsdf=len(sc.bsdfs) - 1))
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -243,7 +244,7 @@ def test_direct_integrator_bitexact(gpu_ctx, oracle, counts):
     d = DirectIntegrator(sampleCount=8, rfilter='box', emitterSamples=counts[0], bsdfSamples=counts[1])
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(d, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, d, samples=True, libm_mode=1)
+    film_o, smp_o, st_o = oracle.render(sc, d, samples=True, libm_mode=0)
     _compare(film_g, smp_g, film_o, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
@@ -259,7 +260,7 @@ def test_independent_sampler_bitexact(gpu_ctx, oracle, materials):
                DirectIntegrator(sampleCount=8, rfilter='box', sampler='independent', emitterSamples=3,
                                 bsdfSamples=2)):
         film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-        film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1)
+        film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o)
         assert st_g['rays'] == st_o['rays']
 
@@ -273,7 +274,7 @@ def test_volpath_bitexact(gpu_ctx, oracle):
         v = VolpathIntegrator(sampleCount=8, rfilter='box', strictNormals=True)
         gpu_ctx.upload(sc)
         film_g, smp_g, st_g = gpu_ctx.render(v, samples=True)
-        film_o, smp_o, st_o = oracle.render(sc, v, samples=True, libm_mode=1)
+        film_o, smp_o, st_o = oracle.render(sc, v, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o)
         assert st_g['path_length_sum'] == st_o['path_length_sum']
 
@@ -284,7 +285,7 @@ def test_direct_integrator_envmap_and_shapes(gpu_ctx, oracle):
         d = DirectIntegrator(sampleCount=4, rfilter='box', emitterSamples=2, bsdfSamples=2)
         gpu_ctx.upload(sc)
         film_g, smp_g, _ = gpu_ctx.render(d, samples=True)
-        film_o, smp_o, _ = oracle.render(sc, d, samples=True, libm_mode=1)
+        film_o, smp_o, _ = oracle.render(sc, d, samples=True, libm_mode=0)
         _assert_records_equal(smp_g, smp_o)
 
 

@@ -48,7 +48,7 @@ def test_sfmt_replay_bitexact(gpu_ctx, oracle, sampler, case):
         it = PathIntegrator(sampleCount=4, rfilter='box', sampler=sampler)
     gpu_ctx.upload(sc)
     film_g, smp_g, st_g = gpu_ctx.render(it, samples=True)
-    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=1, threads=8)
+    film_o, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0, threads=8)
     same = np.all(_bits(smp_g) == _bits(smp_o), axis=1)
     bad = np.nonzero(~same)[0]
     assert same.all(), '%d of %d records differ, first %s: %s vs %s' % (

@@ -37,7 +37,7 @@ def _check(gpu_ctx, oracle, sc, it, what, window=None):
     gpu_ctx.upload(sc)
     film_w, smp_w, st_w = gpu_ctx.render(it, window=window, samples=True, engine='wavefront')
     film_m, smp_m, st_m = gpu_ctx.render(it, window=window, samples=True, engine='megakernel')
-    film_o, smp_o, st_o = oracle.render(sc, it, window=window, samples=True, libm_mode=1, threads=THREADS)
+    film_o, smp_o, st_o = oracle.render(sc, it, window=window, samples=True, libm_mode=0, threads=THREADS)
     _records_equal(smp_w, smp_o, what + ' wavefront vs oracle')
     _records_equal(smp_m, smp_o, what + ' megakernel vs oracle')
     for k in ('samples', 'rays', 'shadow_rays', 'path_length_sum'):

@@ -89,8 +89,8 @@ def test_oracle_render_over_kdtree_matches_bvh(oracle):
     exact-t tie decides a hit (the Cornell box has none at these samples)."""
     sc, it = scenes.build('C1', width=32, height=24, spp=4)
     nodes, idx, _ = kdtree_host(sc)
-    f_kd, s_kd, st_kd = oracle.render(sc, it, samples=True, libm_mode=1, kdtree=(nodes, idx))
-    f_bvh, s_bvh, st_bvh = oracle.render(sc, it, samples=True, libm_mode=1)
+    f_kd, s_kd, st_kd = oracle.render(sc, it, samples=True, libm_mode=0, kdtree=(nodes, idx))
+    f_bvh, s_bvh, st_bvh = oracle.render(sc, it, samples=True, libm_mode=0)
     same = np.all(s_kd.view(np.uint32) == s_bvh.view(np.uint32), axis=1)
     assert same.mean() > 0.999
     assert st_kd['samples'] == st_bvh['samples']

@@ -18,7 +18,7 @@ for kw in ({'md': -1}, {'md': -1}, {'md': 2}, {'md': 3}, {'md': -1, 'hide': True
         it.rrDepth = kw['rr']
     ctx.upload(sc)
     fg, sg, _ = ctx.render(it, samples=True)
-    fo, so, _ = ob.render(sc, it, samples=True, libm_mode=1)
+    fo, so, _ = ob.render(sc, it, samples=True, libm_mode=0)
     bad = ~np.all(sg.view(np.uint32) == so.view(np.uint32), axis=1)
     print(kw, 'mismatch', bad.sum(), 'of', len(bad))
     if prev is not None and kw == {'md': -1}:

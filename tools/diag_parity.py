@@ -97,7 +97,7 @@ def main():
     for name, sc, it in cases():
         if only and name not in only:
             continue
-        _, smp_o, _ = ob.render(sc, it, samples=True, libm_mode=1, threads=8)
+        _, smp_o, _ = ob.render(sc, it, samples=True, libm_mode=0, threads=8)
         for vn, _ in variants:
             c = ctxs[vn]
             c.upload(sc)

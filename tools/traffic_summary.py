@@ -44,6 +44,7 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
         out = {'config': cfg, 'kernel': 'path_kernel', 'launches': len(fetch), 'FETCH_SIZE_KiB': f, 'WRITE_SIZE_KiB': w,
                'hbm_bytes_per_launch': 2 * f * 1024 + w * 1024,
                'hbm_bytes_per_launch_fetch_raw': f * 1024 + w * 1024,
+               'hbm_bytes_per_sample': (2 * f * 1024 + w * 1024) / samples if samples else None,
                'write_bytes_per_sample': w * 1024 / samples if samples else None,
                'read_bytes_per_sample_raw': f * 1024 / samples if samples else None,
                'note': 'one full frame (tools/prof_run.py %s 1 1). hbm_bytes_per_launch doubles FETCH_SIZE '
@@ -70,6 +71,14 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
         continue
     c = {n: sum(x) / len(x) for n, x in v.items()}
     wc = c['SQ_WAVE_CYCLES']
+    # the pass's kernel durations (its --kernel-trace) give the shader clock:
+    # GRBM_GUI_ACTIVE / 8 XCDs cycles over the dispatch's duration
+    durs = []
+    for f in glob.glob(os.path.join(src, 'pmc_%s_SQ' % cfg, '**', '*kernel_trace.csv'), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if 'path_kernel' in r['Kernel_Name']:
+                durs.append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-9)
+    pass_samples = SAMPLES[cfg] // 4          # tools/prof_run.py <cfg> 1 4: a quarter of the rows
     out = {'config': cfg, 'kernel': 'path_kernel', 'counters': c,
            'valu_busy_per_simd': 4 * c['SQ_ACTIVE_INST_VALU'] / (SIMDS * c['GRBM_GUI_ACTIVE'] / XCDS),
            'valu_issue_frac_per_wave': c['SQ_ACTIVE_INST_VALU'] / wc,
@@ -77,6 +86,9 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
            'wait_frac_per_wave': c['SQ_WAIT_ANY'] / wc,
            'issue_stall_frac_per_wave': c['SQ_WAIT_INST_ANY'] / wc,
            'valu_insts_per_wave': c['SQ_INSTS_VALU'] / max(1.0, c['SQ_WAVES']),
+           'valu_insts_per_sample': c['SQ_INSTS_VALU'] / pass_samples,
+           'kernel_s': sum(durs) / len(durs) if durs else None,
+           'clock_hz': c['GRBM_GUI_ACTIVE'] / XCDS / (sum(durs) / len(durs)) if durs else None,
            'note': '1/4 of the rows (tools/prof_run.py %s 1 4); SQ cycle counters in quad-cycles' % cfg}
     json.dump(out, open(os.path.join(prof, '%s_valu_%s.json' % (rnd, cfg)), 'w'), indent=1)
     print(cfg, {k: out[k] for k in out if k.endswith('frac_per_wave') or k.startswith('valu_busy')})
