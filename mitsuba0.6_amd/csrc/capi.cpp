@@ -590,6 +590,20 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.xcds = (ctx->num_cus % 32 == 0) ? (uint32_t)std::max(1, ctx->num_cus / 32) : 1u;
     L.all_diffuse = std::getenv("MTSGPU_NO_DIFF_VARIANT") ? 0u : 1u;
     for (const MtsgBsdf &b : H.bsdfs) L.all_diffuse &= b.type == MTSGPU_BSDF_DIFFUSE ? 1u : 0u;
+    // the scene's BSDF set, for the specialised megakernel variants (dbsdf.h BSet)
+    {
+        bool ggx = true, rc = false, rd = false;
+        for (const MtsgBsdf &b : H.bsdfs) {
+            const bool rough = b.type == MTSGPU_BSDF_ROUGHCONDUCTOR || b.type == MTSGPU_BSDF_ROUGHDIELECTRIC ||
+                               b.type == MTSGPU_BSDF_ROUGHPLASTIC;
+            if (rough && b.distr != MTSGPU_DISTR_GGX) ggx = false;
+            rc |= b.type == MTSGPU_BSDF_ROUGHCONDUCTOR;
+            rd |= b.type == MTSGPU_BSDF_ROUGHDIELECTRIC;
+        }
+        L.bset = std::getenv("MTSGPU_NO_BSDF_SETS") ? 0u
+                 : (ggx ? (uint32_t)MTSG_FEAT_GGX : 0u) | (rc ? 0u : (uint32_t)MTSG_FEAT_NORC) |
+                       (rd ? 0u : (uint32_t)MTSG_FEAT_NORD);
+    }
     // MIDirectIntegrator::configure / configureSampler (direct.cpp:128-143)
     L.integrator = P->integrator;
     L.array_end = 5;
@@ -623,8 +637,15 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     }
     if (const char *env = std::getenv("MTSGPU_SOBOL_LDS_DIMS"))
         L.lds_dims = (uint32_t)std::min(1024l, std::max(0l, std::strtol(env, nullptr, 10)));
-    // own-pixel splat buffer [5][chunk][pixels]; spp processed in chunks that fit the budget
+    // own-pixel splat buffer [chunk][pixels] of float4; spp processed in chunks
+    // that fit the budget: a quarter of the device's free HBM, at most 32 GiB
+    // (C5's 1280x720x1024 splats, 15 GB, then run as one launch, one tail)
     size_t budget = (size_t)8 << 30;
+    {
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB / 4 > budget)
+            budget = std::min<size_t>(freeB / 4 + ctx->contrib.bytes, (size_t)32 << 30);
+    }
     if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);
     const size_t perSample = (size_t)L.num_pixels * 4 * 4;   // float4 per sample
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));

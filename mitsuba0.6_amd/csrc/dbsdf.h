@@ -22,22 +22,12 @@ enum { DISTR_BECKMANN = 0, DISTR_GGX = 1, DISTR_PHONG = 2 };
 #else
 #define BSDF_CALL __device__ __noinline__
 #endif
-// A/B experiments (profiles/r03_ab_*): BSDF-set-specialised builds
-#ifdef MTSG_SPEC_DISTR
-#define DTYPE(d) (MTSG_SPEC_DISTR)
-#else
-#define DTYPE(d) ((d).type)
-#endif
+// out-of-line microfacet / Fresnel helpers of the generic BSDF set
+// (MTSG_HELPER_INLINE: every set inlines them, an A/B knob)
 #ifdef MTSG_HELPER_INLINE
 #define HELPER_CALL __device__ __forceinline__
 #else
 #define HELPER_CALL __device__ __noinline__
-#endif
-#ifndef MTSG_SPEC_HAS_RC
-#define MTSG_SPEC_HAS_RC 1
-#endif
-#ifndef MTSG_SPEC_HAS_RD
-#define MTSG_SPEC_HAS_RD 1
 #endif
 enum { BSDF_DIFFUSE = 0, BSDF_ROUGHCONDUCTOR = 1, BSDF_ROUGHDIELECTRIC = 2, BSDF_ROUGHPLASTIC = 3,
        BSDF_CONDUCTOR = 4, BSDF_DIELECTRIC = 5, BSDF_PLASTIC = 6, BSDF_TWOSIDED = 7 };   // = MTSGPU_BSDF_*
@@ -119,6 +109,26 @@ __device__ __forceinline__ float m_hypot2(float a, float b) {
 
 // ---- MicrofacetDistribution -----------------------------------------------
 struct Distr { int type; float alphaU, alphaV; int sampleVisible; float expU, expV; };
+
+// ---- the compile-time BSDF set of a kernel variant ------------------------
+// BS = the variant's MTSG_FEAT_* bits that select BSDF code (BSET_BITS): EXT
+// (roughplastic, textures, smooth BSDFs, twosided), DIFF (every BSDF diffuse),
+// GGX (every rough BSDF of the scene uses the GGX distribution), NORC / NORD
+// (no roughconductor / roughdielectric).  The reference dispatches per vertex
+// through BSDF's virtual eval/sample (src/integrators/path/path.cpp:171-211);
+// here the scene's set is known before the launch, so a specialised variant
+// compiles only the lobes and the distribution the scene has, and inlines the
+// microfacet helpers that the generic set calls out of line
+// (profiles/r03_ab_spec_C*.log).
+#define BSET_BITS (MTSG_FEAT_EXT | MTSG_FEAT_DIFF | MTSG_FEAT_GGX | MTSG_FEAT_NORC | MTSG_FEAT_NORD)
+template <int BS> struct BSet {
+    static constexpr bool EXT = (BS & MTSG_FEAT_EXT) != 0, DIFF = (BS & MTSG_FEAT_DIFF) != 0;
+    static constexpr bool GGX = (BS & MTSG_FEAT_GGX) != 0;
+    static constexpr bool RC = (BS & MTSG_FEAT_NORC) == 0, RD = (BS & MTSG_FEAT_NORD) == 0;
+    static constexpr bool INL = GGX;   // helpers inline in specialised sets
+};
+// the distribution type as the variant knows it
+template <int BS> __device__ __forceinline__ int dtype(const Distr &d) { return BSet<BS>::GGX ? (int)DISTR_GGX : d.type; }
 // BSDF records are read straight from global memory (no generic/flat loads)
 typedef const __attribute__((address_space(1))) MtsgBsdf GBsdf;
 
@@ -142,14 +152,15 @@ __device__ __forceinline__ float distr_interp_phong(const Distr &d, f3 v) {   //
     return d.expU * (v.x * v.x * inv) + d.expV * (v.y * v.y * inv);
 }
 
-HELPER_CALL float distr_eval(Distr d, f3 m) {   // :191-238
+template <int BS>
+__device__ __forceinline__ float distr_eval_b(Distr d, f3 m) {   // :191-238
     if (m.z <= 0) return 0.0f;
     float cosTheta2 = m.z * m.z;
     float be = ((m.x * m.x) / (d.alphaU * d.alphaU) + (m.y * m.y) / (d.alphaV * d.alphaV)) / cosTheta2;
     float result;
-    if (DTYPE(d) == DISTR_BECKMANN) {
+    if (dtype<BS>(d) == DISTR_BECKMANN) {
         result = d_fastexp(-be) / (D_PI * d.alphaU * d.alphaV * cosTheta2 * cosTheta2);
-    } else if (DTYPE(d) == DISTR_GGX) {
+    } else if (dtype<BS>(d) == DISTR_GGX) {
         float root = ((float)1 + be) * cosTheta2;
         result = (float)1 / (D_PI * d.alphaU * d.alphaV * root * root);
     } else {
@@ -158,6 +169,11 @@ HELPER_CALL float distr_eval(Distr d, f3 m) {   // :191-238
     }
     if (result * m.z < 1e-20f) result = 0;
     return result;
+}
+template <int BS> HELPER_CALL float distr_eval_o(Distr d, f3 m) { return distr_eval_b<BS>(d, m); }
+template <int BS> __device__ __forceinline__ float distr_eval(Distr d, f3 m) {
+    if constexpr (BSet<BS>::INL) return distr_eval_b<BS>(d, m);
+    else return distr_eval_o<BS>(d, m);
 }
 
 __device__ __forceinline__ float distr_project_roughness(const Distr &d, f3 v) {   // :526-536
@@ -168,12 +184,13 @@ __device__ __forceinline__ float distr_project_roughness(const Distr &d, f3 v) {
     return dsqrt(cosPhi2 * d.alphaU * d.alphaU + sinPhi2 * d.alphaV * d.alphaV);
 }
 
-HELPER_CALL float distr_smithG1(Distr d, f3 v, f3 m) {   // :477-518
+template <int BS>
+__device__ __forceinline__ float distr_smithG1_b(Distr d, f3 v, f3 m) {   // :477-518
     if (dot(v, m) * v.z <= 0) return 0.0f;
     float tanTheta = fabsf(tan_theta(v));
     if (tanTheta == 0.0f) return 1.0f;
     float alpha = distr_project_roughness(d, v);
-    if (DTYPE(d) == DISTR_GGX) {
+    if (dtype<BS>(d) == DISTR_GGX) {
         float root = alpha * tanTheta;
         return 2.0f / (1.0f + m_hypot2((float)1.0f, root));
     }
@@ -181,6 +198,11 @@ HELPER_CALL float distr_smithG1(Distr d, f3 v, f3 m) {   // :477-518
     if (a >= 1.6f) return 1.0f;
     float aSqr = a * a;
     return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+}
+template <int BS> HELPER_CALL float distr_smithG1_o(Distr d, f3 v, f3 m) { return distr_smithG1_b<BS>(d, v, m); }
+template <int BS> __device__ __forceinline__ float distr_smithG1(Distr d, f3 v, f3 m) {
+    if constexpr (BSet<BS>::INL) return distr_smithG1_b<BS>(d, v, m);
+    else return distr_smithG1_o<BS>(d, v, m);
 }
 
 __device__ __forceinline__ void distr_first_quadrant(const Distr &d, float u1, float &phi, float &exponent) {
@@ -190,9 +212,10 @@ __device__ __forceinline__ void distr_first_quadrant(const Distr &d, float u1, f
     exponent = d.expU * c * c + d.expV * s * s;
 }
 
+template <int BS>
 __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy, float &pdf) {  // :287-402
     float cosThetaM = 0.0f, sinPhiM, cosPhiM, alphaSqr;
-    if (DTYPE(d) != DISTR_PHONG) {
+    if (dtype<BS>(d) != DISTR_PHONG) {
         if (distr_iso(d)) {
             d_sincos((2.0f * D_PI) * sy, &sinPhiM, &cosPhiM);
             alphaSqr = d.alphaU * d.alphaU;
@@ -202,7 +225,7 @@ __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy,
             float cosSc = cosPhiM / d.alphaU, sinSc = sinPhiM / d.alphaV;
             alphaSqr = 1.0f / (cosSc * cosSc + sinSc * sinSc);
         }
-        if (DTYPE(d) == DISTR_BECKMANN) {
+        if (dtype<BS>(d) == DISTR_BECKMANN) {
             float tanThetaMSqr = alphaSqr * -d_fastlog(1.0f - sx);
             cosThetaM = 1.0f / dsqrt(1.0f + tanThetaMSqr);
             pdf = (1.0f - sx) / (D_PI * d.alphaU * d.alphaV * cosThetaM * cosThetaM * cosThetaM);
@@ -240,10 +263,11 @@ __device__ __forceinline__ f3 distr_sample_all_impl(Distr d, float sx, float sy,
     return mk(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
 }
 
+template <int BS>
 __device__ __forceinline__ void distr_sample_visible11_impl(Distr d, float thetaI, float sx, float sy,
                                                            float &slx, float &sly) {   // :573-670
     const float SQRT_PI_INV = 1 / dsqrt(D_PI);
-    if (DTYPE(d) == DISTR_BECKMANN) {
+    if (dtype<BS>(d) == DISTR_BECKMANN) {
         if (thetaI < 1e-4f) {
             float s, c;
             float r = dsqrt(-d_fastlog(1.0f - sx));
@@ -301,17 +325,36 @@ __device__ __forceinline__ void distr_sample_visible11_impl(Distr d, float theta
 // out-of-line entry points return their results by value (no stack round trip)
 struct F2 { float x, y; };
 struct MPdf { f3 m; float pdf; };
-HELPER_CALL F2 distr_sample_visible11(Distr d, float thetaI, float sx, float sy) {
+template <int BS> HELPER_CALL F2 distr_sample_visible11_o(Distr d, float thetaI, float sx, float sy) {
     F2 r;
-    distr_sample_visible11_impl(d, thetaI, sx, sy, r.x, r.y);
+    distr_sample_visible11_impl<BS>(d, thetaI, sx, sy, r.x, r.y);
     return r;
 }
-HELPER_CALL MPdf distr_sample_all(Distr d, float sx, float sy) {
+template <int BS> __device__ __forceinline__ F2 distr_sample_visible11(Distr d, float thetaI, float sx, float sy) {
+    if constexpr (BSet<BS>::INL) {
+        F2 r;
+        distr_sample_visible11_impl<BS>(d, thetaI, sx, sy, r.x, r.y);
+        return r;
+    } else {
+        return distr_sample_visible11_o<BS>(d, thetaI, sx, sy);
+    }
+}
+template <int BS> HELPER_CALL MPdf distr_sample_all_o(Distr d, float sx, float sy) {
     MPdf r;
-    r.m = distr_sample_all_impl(d, sx, sy, r.pdf);
+    r.m = distr_sample_all_impl<BS>(d, sx, sy, r.pdf);
     return r;
+}
+template <int BS> __device__ __forceinline__ MPdf distr_sample_all(Distr d, float sx, float sy) {
+    if constexpr (BSet<BS>::INL) {
+        MPdf r;
+        r.m = distr_sample_all_impl<BS>(d, sx, sy, r.pdf);
+        return r;
+    } else {
+        return distr_sample_all_o<BS>(d, sx, sy);
+    }
 }
 
+template <int BS>
 __device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float sx, float sy) {  // :421-460
     f3 wi = normalize(mk(d.alphaU * _wi.x, d.alphaV * _wi.y, _wi.z));
     float theta = 0, phi = 0;
@@ -321,7 +364,7 @@ __device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float
     }
     float sinPhi, cosPhi;
     d_sincos(phi, &sinPhi, &cosPhi);
-    const F2 sl = distr_sample_visible11(d, theta, sx, sy);
+    const F2 sl = distr_sample_visible11<BS>(d, theta, sx, sy);
     const float slx = sl.x, sly = sl.y;
     float nx = cosPhi * slx - sinPhi * sly;
     float ny = sinPhi * slx + cosPhi * sly;
@@ -331,27 +374,31 @@ __device__ __forceinline__ f3 distr_sample_visible(const Distr &d, f3 _wi, float
     return mk(-nx * normalization, -ny * normalization, normalization);
 }
 
+template <int BS>
 __device__ __forceinline__ float distr_pdf_visible(const Distr &d, f3 wi, f3 m) {   // :462-466
     if (wi.z == 0) return 0.0f;
-    return distr_smithG1(d, wi, m) * absdot(wi, m) * distr_eval(d, m) / fabsf(wi.z);
+    return distr_smithG1<BS>(d, wi, m) * absdot(wi, m) * distr_eval<BS>(d, m) / fabsf(wi.z);
 }
+template <int BS>
 __device__ __forceinline__ float distr_pdf(const Distr &d, f3 wi, f3 m) {           // :270-276
-    if (d.sampleVisible) return distr_pdf_visible(d, wi, m);
-    return distr_eval(d, m) * m.z;
+    if (d.sampleVisible) return distr_pdf_visible<BS>(d, wi, m);
+    return distr_eval<BS>(d, m) * m.z;
 }
+template <int BS>
 __device__ __forceinline__ f3 distr_sample(const Distr &d, f3 wi, float sx, float sy, float &pdf) {
     if (d.sampleVisible) {                                                          // :243-253
-        f3 m = distr_sample_visible(d, wi, sx, sy);
-        pdf = distr_pdf_visible(d, wi, m);
+        f3 m = distr_sample_visible<BS>(d, wi, sx, sy);
+        pdf = distr_pdf_visible<BS>(d, wi, m);
         return m;
     }
-    const MPdf r = distr_sample_all(d, sx, sy);
+    const MPdf r = distr_sample_all<BS>(d, sx, sy);
     pdf = r.pdf;
     return r.m;
 }
+template <int BS>
 __device__ __forceinline__ void distr_scale_alpha(Distr &d, float v) {              // :181-186
     d.alphaU *= v; d.alphaV *= v;
-    if (DTYPE(d) == DISTR_PHONG) distr_phong_exp(d);
+    if (dtype<BS>(d) == DISTR_PHONG) distr_phong_exp(d);
 }
 
 // ---- Fresnel (util.cpp) -------------------------------------------------
@@ -368,7 +415,7 @@ __device__ __forceinline__ float fresnel_dielectric_ext(float cosThetaI_, float 
     return 0.5f * (Rs * Rs + Rp * Rp);
 }
 __device__ __forceinline__ f3 s_safe_sqrt(f3 a) { return mk(safe_sqrt(a.x), safe_sqrt(a.y), safe_sqrt(a.z)); }
-HELPER_CALL f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {   // util.cpp:739-761
+__device__ __forceinline__ f3 fresnel_conductor_exact_b(float cosThetaI, f3 eta, f3 k) {   // util.cpp:739-761
     float cosThetaI2 = cosThetaI * cosThetaI, sinThetaI2 = 1 - cosThetaI2, sinThetaI4 = sinThetaI2 * sinThetaI2;
     f3 temp1 = sub(sub(mulv(eta, eta), mulv(k, k)), mk(sinThetaI2, sinThetaI2, sinThetaI2));
     f3 a2pb2 = s_safe_sqrt(add(mulv(temp1, temp1), mul(mulv(mulv(mulv(k, k), eta), eta), 4)));
@@ -380,6 +427,11 @@ HELPER_CALL f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {   // uti
     f3 term4 = mul(term2, sinThetaI2);
     f3 Rp2 = divv(mulv(Rs2, sub(term3, term4)), add(term3, term4));
     return mul(add(Rp2, Rs2), 0.5f);
+}
+HELPER_CALL f3 fresnel_conductor_exact_o(float cosThetaI, f3 eta, f3 k) { return fresnel_conductor_exact_b(cosThetaI, eta, k); }
+template <int BS> __device__ __forceinline__ f3 fresnel_conductor_exact(float cosThetaI, f3 eta, f3 k) {
+    if constexpr (BSet<BS>::INL) return fresnel_conductor_exact_b(cosThetaI, eta, k);
+    else return fresnel_conductor_exact_o(cosThetaI, eta, k);
 }
 __device__ __forceinline__ f3 reflect_v(f3 wi, f3 n) { return sub(mul(n, 2 * dot(wi, n)), wi); }
 __device__ __forceinline__ f3 refract_v(f3 wi, f3 n, float eta, float cosThetaT) {
@@ -410,16 +462,16 @@ __device__ __forceinline__ f3 tex_eval(GTex &t, float u, float v) {
 __device__ __forceinline__ float avg3(f3 s) { float r = 0.0f; r += s.x; r += s.y; r += s.z; return r * (1.0f / 3); }
 
 // reflectance / diffuseReflectance at the hit (texture or constant)
-template <bool EXT>
+template <int BS>
 __device__ __forceinline__ f3 bsdf_refl(GBsdf &b, float u, float v) {
-    if constexpr (EXT) { if (b.refl_tex.type) return tex_eval(b.refl_tex, u, v); }
+    if constexpr (BSet<BS>::EXT) { if (b.refl_tex.type) return tex_eval(b.refl_tex, u, v); }
     return ld3(b.refl);
 }
 // the rough BSDF's distribution at the hit: m_alpha->eval(its).average() for a
 // textured alpha (MicrofacetDistribution(type, alpha, sampleVisible) clamps)
-template <bool EXT>
+template <int BS>
 __device__ __forceinline__ Distr bsdf_distr(GBsdf &b, float u, float v) {
-    if constexpr (EXT) {
+    if constexpr (BSet<BS>::EXT) {
         if (b.alpha_tex.type) {
             const float a = avg3(tex_eval(b.alpha_tex, u, v));
             return distr_make(b.distr, a, a, b.sample_visible);
@@ -513,20 +565,21 @@ __device__ __forceinline__ float rp_prob_specular(GBsdf &b, glb_f32 *rt, float c
 }
 
 // RoughPlastic::eval (roughplastic.cpp:300-345)
+template <int BS>
 __device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
-    const Distr d = bsdf_distr<true>(b, u, v);
+    const Distr d = bsdf_distr<BS>(b, u, v);
     f3 result = mk(0, 0, 0);
     {
         const f3 H = normalize(add(wo, wi));
-        const float D = distr_eval(d, H);
+        const float D = distr_eval<BS>(d, H);
         float ct;
         const float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
-        const float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+        const float G = distr_smithG1<BS>(d, wi, H) * distr_smithG1<BS>(d, wo, H);
         const float value = F * D * G / (4.0f * wi.z);
         result = add(result, mul(ld3(b.spec_r), value));
     }
-    f3 diff = bsdf_refl<true>(b, u, v);
+    f3 diff = bsdf_refl<BS>(b, u, v);
     const float T12 = rt_eval(b, rt, wi.z, d.alphaU);
     const float T21 = rt_eval(b, rt, wo.z, d.alphaU);
     const float Fdr = 1 - rt_eval_diffuse(b, rt, d.alphaU);
@@ -536,30 +589,34 @@ __device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, 
 }
 
 // RoughPlastic::pdf (roughplastic.cpp:347-393)
+template <int BS>
 __device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (wi.z <= 0 || wo.z <= 0) return 0.0f;
-    const Distr d = bsdf_distr<true>(b, u, v);
+    const Distr d = bsdf_distr<BS>(b, u, v);
     const f3 H = normalize(add(wo, wi));
     const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
     const float probDiffuse = 1 - probSpecular;
     const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
-    const float prob = distr_pdf(d, wi, H);
+    const float prob = distr_pdf<BS>(d, wi, H);
     float result = prob * dwh_dwo * probSpecular;
     result += probDiffuse * (D_INV_PI * wo.z);
     return result;
 }
+template <int BS>
 BSDF_CALL f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return rp_eval_body(b, rt, wi, wo, u, v);
+    return rp_eval_body<BS>(b, rt, wi, wo, u, v);
 }
+template <int BS>
 BSDF_CALL float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return rp_pdf_body(b, rt, wi, wo, u, v);
+    return rp_pdf_body<BS>(b, rt, wi, wo, u, v);
 }
 struct EvalPdf { f3 val; float pdf; };
 // eval, and pdf where the value is nonzero, of one query in one call (NEE)
+template <int BS>
 BSDF_CALL EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     EvalPdf r;
-    r.val = rp_eval_body(b, rt, wi, wo, u, v);
-    r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body(b, rt, wi, wo, u, v);
+    r.val = rp_eval_body<BS>(b, rt, wi, wo, u, v);
+    r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body<BS>(b, rt, wi, wo, u, v);
     return r;
 }
 
@@ -573,7 +630,7 @@ __device__ __forceinline__ float fresnel_dielectric_ext2(float cosThetaI, float 
     return fresnel_dielectric_ext(cosThetaI, ct, eta);
 }
 __device__ __forceinline__ f3 sp_diffuse(GBsdf &b, float u, float v) {   // diff /= ... (plastic.cpp:276-280)
-    f3 diff = bsdf_refl<true>(b, u, v);
+    f3 diff = bsdf_refl<MTSG_FEAT_EXT>(b, u, v);
     if (b.nonlinear) diff = divv(diff, sub(mk(1.0f, 1.0f, 1.0f), mul(diff, b.fdr_int)));
     else diff = divs(diff, 1 - b.fdr_int);
     return diff;
@@ -604,7 +661,7 @@ __device__ __noinline__ BSample sm_sample(GBsdf &b, f3 wi, float sx, float sy, f
         r.wo = mk(-wi.x, -wi.y, wi.z);
         r.eta = 1.0f;
         r.pdf = 1;
-        r.weight = mulv(ld3(b.spec_r), fresnel_conductor_exact(wi.z, ld3(b.eta3), ld3(b.k3)));
+        r.weight = mulv(ld3(b.spec_r), fresnel_conductor_exact<0>(wi.z, ld3(b.eta3), ld3(b.k3)));
         return r;
     }
     if (b.type == BSDF_DIELECTRIC) {
@@ -649,29 +706,29 @@ __device__ __noinline__ BSample sm_sample(GBsdf &b, f3 wi, float sx, float sy, f
 }
 
 // ---- BSDF::eval / pdf / sample --------------------------------------------
-template <bool EXT>
+template <int BS>
 __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     const f3 zero = mk(0, 0, 0);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
         if (wi.z <= 0 || wo.z <= 0) return zero;
-        return mul(bsdf_refl<EXT>(b, u, v), D_INV_PI * wo.z);
+        return mul(bsdf_refl<BS>(b, u, v), D_INV_PI * wo.z);
     }
-    if constexpr (EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval(b, rt, wi, wo, u, v);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval<BS>(b, rt, wi, wo, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
     }
-    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:257-292
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:257-292
         if (wi.z <= 0 || wo.z <= 0) return zero;
         f3 H = normalize(add(wo, wi));
-        Distr d = bsdf_distr<EXT>(b, u, v);
-        float D = distr_eval(d, H);
+        Distr d = bsdf_distr<BS>(b, u, v);
+        float D = distr_eval<BS>(d, H);
         if (D == 0) return zero;
-        f3 F = mulv(fresnel_conductor_exact(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
-        float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+        f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+        float G = distr_smithG1<BS>(d, wi, H) * distr_smithG1<BS>(d, wo, H);
         float model = D * G / (4.0f * wi.z);
         return mul(F, model);
     }
-    if (!MTSG_SPEC_HAS_RD) return zero;
+    if (!BSet<BS>::RD) return zero;
     if (wi.z == 0) return zero;                                            // roughdielectric.cpp:270-346
     bool reflect = wi.z * wo.z > 0;
     f3 H;
@@ -682,12 +739,12 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
         H = normalize(add(wi, mul(wo, eta)));
     }
     H = mul(H, signum(H.z));
-    Distr d = bsdf_distr<EXT>(b, u, v);
-    float D = distr_eval(d, H);
+    Distr d = bsdf_distr<BS>(b, u, v);
+    float D = distr_eval<BS>(d, H);
     if (D == 0) return zero;
     float ct;
     float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
-    float G = distr_smithG1(d, wi, H) * distr_smithG1(d, wo, H);
+    float G = distr_smithG1<BS>(d, wi, H) * distr_smithG1<BS>(d, wo, H);
     if (reflect) {
         float value = F * D * G / (4.0f * fabsf(wi.z));
         return mul(ld3(b.spec_r), value);
@@ -699,24 +756,24 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
     return mul(ld3(b.spec_t), fabsf(value * factor * factor));
 }
 
-template <bool EXT>
+template <int BS>
 __device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
     }
-    if constexpr (EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf(b, rt, wi, wo, u, v);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf<BS>(b, rt, wi, wo, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
     }
-    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:294-319
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:294-319
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         f3 H = normalize(add(wo, wi));
-        Distr d = bsdf_distr<EXT>(b, u, v);
-        if (b.sample_visible) return distr_eval(d, H) * distr_smithG1(d, wi, H) / (4.0f * wi.z);
-        return distr_pdf(d, wi, H) / (4 * absdot(wo, H));
+        Distr d = bsdf_distr<BS>(b, u, v);
+        if (b.sample_visible) return distr_eval<BS>(d, H) * distr_smithG1<BS>(d, wi, H) / (4.0f * wi.z);
+        return distr_pdf<BS>(d, wi, H) / (4 * absdot(wo, H));
     }
-    if (!MTSG_SPEC_HAS_RD) return 0.0f;
+    if (!BSet<BS>::RD) return 0.0f;
     bool reflect = wi.z * wo.z > 0;                                        // roughdielectric.cpp:348-405
     f3 H;
     float dwh_dwo;
@@ -730,35 +787,35 @@ __device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 
         dwh_dwo = (eta * eta * dot(wo, H)) / (sqrtDenom * sqrtDenom);
     }
     H = mul(H, signum(H.z));
-    Distr d = bsdf_distr<EXT>(b, u, v);
-    if (!b.sample_visible) distr_scale_alpha(d, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
-    float prob = distr_pdf(d, mul(wi, signum(wi.z)), H);
+    Distr d = bsdf_distr<BS>(b, u, v);
+    if (!b.sample_visible) distr_scale_alpha<BS>(d, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
+    float prob = distr_pdf<BS>(d, mul(wi, signum(wi.z)), H);
     float ct;
     float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
     prob *= reflect ? F : (1 - F);
     return fabsf(prob * dwh_dwo);
 }
 
-template <bool EXT>
+template <int BS>
 BSDF_CALL f3 bsdf_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return bsdf_eval_body<EXT>(b, rt, wi, wo, u, v);
+    return bsdf_eval_body<BS>(b, rt, wi, wo, u, v);
 }
-template <bool EXT>
+template <int BS>
 BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return bsdf_pdf_body<EXT>(b, rt, wi, wo, u, v);
+    return bsdf_pdf_body<BS>(b, rt, wi, wo, u, v);
 }
 
 // BSDF::eval, then BSDF::pdf of the same query where the value is nonzero
 // (the NEE estimate of path.cpp:176-199 needs both): one out-of-line call, so
 // the caller's live registers are saved around one call instead of two
-template <bool EXT>
+template <int BS>
 BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    if constexpr (EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval_pdf(b, rt, wi, wo, u, v);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval_pdf<BS>(b, rt, wi, wo, u, v);
     }
     EvalPdf r;
-    r.val = bsdf_eval_body<EXT>(b, rt, wi, wo, u, v);
-    r.pdf = is_zero(r.val) ? 0.0f : bsdf_pdf_body<EXT>(b, rt, wi, wo, u, v);
+    r.val = bsdf_eval_body<BS>(b, rt, wi, wo, u, v);
+    r.pdf = is_zero(r.val) ? 0.0f : bsdf_pdf_body<BS>(b, rt, wi, wo, u, v);
     return r;
 }
 
@@ -767,12 +824,13 @@ BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, fl
 // the caller, which draws it from the sampler only for that BSDF.
 
 // RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458)
+template <int BS>
 BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (wi.z <= 0) return r;
     bool choseSpecular = true;
-    const Distr d = bsdf_distr<true>(b, u, v);
+    const Distr d = bsdf_distr<BS>(b, u, v);
     const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
     if (sy < probSpecular) {
         sy /= probSpecular;
@@ -782,7 +840,7 @@ BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, fl
     }
     if (choseSpecular) {
         float mpdf;
-        const f3 m = distr_sample(d, wi, sx, sy, mpdf);
+        const f3 m = distr_sample<BS>(d, wi, sx, sy, mpdf);
         r.wo = reflect_v(wi, m);
         r.sampledType = MTSG_F_GLOSSY_REFL;
         if (r.wo.z <= 0) return r;
@@ -791,13 +849,13 @@ BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, fl
         r.wo = square_to_cosine_hemisphere(sx, sy);
     }
     r.eta = 1.0f;
-    r.pdf = rp_pdf(b, rt, wi, r.wo, u, v);
+    r.pdf = rp_pdf<BS>(b, rt, wi, r.wo, u, v);
     if (r.pdf == 0) return r;
-    r.weight = divs(rp_eval(b, rt, wi, r.wo, u, v), r.pdf);
+    r.weight = divs(rp_eval<BS>(b, rt, wi, r.wo, u, v), r.pdf);
     return r;
 }
 
-template <bool EXT>
+template <int BS>
 BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
@@ -807,38 +865,38 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         r.eta = 1.0f;
         r.sampledType = MTSG_F_DIFF_REFL;
         r.pdf = D_INV_PI * r.wo.z;
-        r.weight = bsdf_refl<EXT>(b, u, v);
+        r.weight = bsdf_refl<BS>(b, u, v);
         return r;
     }
-    if constexpr (EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample(b, rt, wi, sx, sy, u, v);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample<BS>(b, rt, wi, sx, sy, u, v);
         if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
     }
-    if (MTSG_SPEC_HAS_RC && (!MTSG_SPEC_HAS_RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:357-406
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:357-406
         if (wi.z < 0) return r;
-        Distr d = bsdf_distr<EXT>(b, u, v);
+        Distr d = bsdf_distr<BS>(b, u, v);
         float pdf;
-        f3 m = distr_sample(d, wi, sx, sy, pdf);
+        f3 m = distr_sample<BS>(d, wi, sx, sy, pdf);
         r.pdf = pdf;
         if (pdf == 0) return r;
         r.wo = reflect_v(wi, m);
         r.eta = 1.0f;
         r.sampledType = MTSG_F_GLOSSY_REFL;
         if (r.wo.z <= 0) return r;
-        f3 F = mulv(fresnel_conductor_exact(dot(wi, m), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+        f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, m), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
         float weight;
-        if (b.sample_visible) weight = distr_smithG1(d, r.wo, m);
-        else weight = distr_eval(d, m) * (distr_smithG1(d, wi, m) * distr_smithG1(d, r.wo, m)) * dot(wi, m) / (pdf * wi.z);
+        if (b.sample_visible) weight = distr_smithG1<BS>(d, r.wo, m);
+        else weight = distr_eval<BS>(d, m) * (distr_smithG1<BS>(d, wi, m) * distr_smithG1<BS>(d, r.wo, m)) * dot(wi, m) / (pdf * wi.z);
         r.pdf = pdf / (4.0f * dot(r.wo, m));
         r.weight = mul(F, weight);
         return r;
     }
-    if (!MTSG_SPEC_HAS_RD) return r;
-    Distr d = bsdf_distr<EXT>(b, u, v);                                    // roughdielectric.cpp:525-615
+    if (!BSet<BS>::RD) return r;
+    Distr d = bsdf_distr<BS>(b, u, v);                                    // roughdielectric.cpp:525-615
     Distr sd = d;
-    if (!b.sample_visible) distr_scale_alpha(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
+    if (!b.sample_visible) distr_scale_alpha<BS>(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
     float microfacetPDF;
-    f3 m = distr_sample(sd, mul(wi, signum(wi.z)), sx, sy, microfacetPDF);
+    f3 m = distr_sample<BS>(sd, mul(wi, signum(wi.z)), sx, sy, microfacetPDF);
     if (microfacetPDF == 0) return r;
     float pdf = microfacetPDF;
     float cosThetaT;
@@ -866,8 +924,8 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         float sqrtDenom = dot(wi, m) + r.eta * dot(r.wo, m);
         dwh_dwo = (r.eta * r.eta * dot(r.wo, m)) / (sqrtDenom * sqrtDenom);
     }
-    if (b.sample_visible) weight = mul(weight, distr_smithG1(d, r.wo, m));
-    else weight = mul(weight, fabsf(distr_eval(d, m) * (distr_smithG1(d, wi, m) * distr_smithG1(d, r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z)));
+    if (b.sample_visible) weight = mul(weight, distr_smithG1<BS>(d, r.wo, m));
+    else weight = mul(weight, fabsf(distr_eval<BS>(d, m) * (distr_smithG1<BS>(d, wi, m) * distr_smithG1<BS>(d, r.wo, m)) * dot(wi, m) / (microfacetPDF * wi.z)));
     r.pdf = pdf * fabsf(dwh_dwo);
     r.weight = weight;
     return r;
@@ -879,48 +937,48 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
 // scratch around them; otherwise the out-of-line functions above are called.
 // (Inlining the diffuse case in front of the calls for every scene cost C3-C5
 // 2-4%: profiles/r02_ab_diffuse_fast.log.)
-template <bool EXT, bool DIFF_ONLY>
+template <int BS>
 __device__ __forceinline__ f3 bsdf_eval_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    if constexpr (DIFF_ONLY) {
+    if constexpr (BSet<BS>::DIFF) {
         if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
-        return mul(bsdf_refl<EXT>(b, u, v), D_INV_PI * wo.z);
+        return mul(bsdf_refl<BS>(b, u, v), D_INV_PI * wo.z);
     } else {
-        return bsdf_eval<EXT>(b, rt, wi, wo, u, v);
+        return bsdf_eval<BS>(b, rt, wi, wo, u, v);
     }
 }
-template <bool EXT, bool DIFF_ONLY>
+template <int BS>
 __device__ __forceinline__ float bsdf_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    if constexpr (DIFF_ONLY) {
+    if constexpr (BSet<BS>::DIFF) {
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return D_INV_PI * wo.z;
     } else {
-        return bsdf_pdf<EXT>(b, rt, wi, wo, u, v);
+        return bsdf_pdf<BS>(b, rt, wi, wo, u, v);
     }
 }
-template <bool EXT, bool DIFF_ONLY>
+template <int BS>
 __device__ __forceinline__ EvalPdf bsdf_eval_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    if constexpr (DIFF_ONLY) {
+    if constexpr (BSet<BS>::DIFF) {
         EvalPdf r;
-        r.val = bsdf_eval_fast<EXT, true>(b, rt, wi, wo, u, v);
-        r.pdf = bsdf_pdf_fast<EXT, true>(b, rt, wi, wo, u, v);
+        r.val = bsdf_eval_fast<BS>(b, rt, wi, wo, u, v);
+        r.pdf = bsdf_pdf_fast<BS>(b, rt, wi, wo, u, v);
         return r;
     } else {
-        return bsdf_eval_pdf<EXT>(b, rt, wi, wo, u, v);
+        return bsdf_eval_pdf<BS>(b, rt, wi, wo, u, v);
     }
 }
-template <bool EXT, bool DIFF_ONLY>
+template <int BS>
 __device__ __forceinline__ BSample bsdf_sample_fast(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d,
                                                     float u, float v) {
-    if constexpr (DIFF_ONLY) {
+    if constexpr (BSet<BS>::DIFF) {
         BSample r;
         r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
         if (wi.z <= 0) return r;
         r.wo = square_to_cosine_hemisphere(sx, sy);
         r.sampledType = MTSG_F_DIFF_REFL;
         r.pdf = D_INV_PI * r.wo.z;
-        r.weight = bsdf_refl<EXT>(b, u, v);
+        r.weight = bsdf_refl<BS>(b, u, v);
         return r;
     } else {
-        return bsdf_sample<EXT>(b, rt, wi, sx, sy, u1d, u, v);
+        return bsdf_sample<BS>(b, rt, wi, sx, sy, u1d, u, v);
     }
 }

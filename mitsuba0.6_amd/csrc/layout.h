@@ -80,7 +80,10 @@ struct MtsgBsdf {            // configured BSDF (after ctor + configure)
 
 enum { MTSG_EMITTER_AREA = 0, MTSG_EMITTER_ENVMAP = 1, MTSG_EMITTER_CONSTANT = 2 };
 enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4,
-       MTSG_FEAT_DIFF = 8 };   // DIFF: every BSDF is diffuse (path megakernel, FEAT 0 scenes only)
+       MTSG_FEAT_DIFF = 8,     // DIFF: every BSDF is diffuse (path megakernel, FEAT 0 scenes only)
+       // BSDF-set specialisation of the megakernel (dbsdf.h BSet): every rough
+       // BSDF uses GGX / no roughdielectric / no roughconductor in the scene
+       MTSG_FEAT_GGX = 16, MTSG_FEAT_NORD = 32, MTSG_FEAT_NORC = 64 };
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
 enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
        MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*
@@ -251,6 +254,7 @@ struct MtsgLaunch {
     uint32_t ext;                     // kernel variant: roughplastic / textured BSDFs present
     uint32_t ana;                     // kernel variant: analytic shapes present (implies ext)
     uint32_t all_diffuse;             // kernel variant: every BSDF is diffuse (MTSG_FEAT_DIFF)
+    uint32_t bset;                    // the scene's MTSG_FEAT_GGX / NORD / NORC bits (capi.cpp)
     uint32_t xcds;                    // XCDs the device's CUs span (workgroup -> XCD remap; 1: none)
     // MTSGPU_FLAG_KDTREE (wavefront engine): wf_trace traverses the reference's kd-tree
     const uint32_t *kd_nodes;         // KDNode words (2 per node), null: the BVH

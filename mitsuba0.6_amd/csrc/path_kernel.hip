@@ -1090,6 +1090,7 @@ struct PathShader {
     static constexpr bool STATS = INSTR;
     static constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
                           ANA = (FEAT & MTSG_FEAT_ANA) != 0, DIFF = (FEAT & MTSG_FEAT_DIFF) != 0;
+    static constexpr int BSF = FEAT & BSET_BITS;   // the variant's BSDF set (dbsdf.h BSet)
     const MtsgLaunch &L;
     const HitSrc<SCENE_LDS> &hs;
     const SobolCtx &SC;
@@ -1372,7 +1373,7 @@ struct PathShader {
                                         if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
                                     }
                                 }
-                                const EvalPdf ep = bsdf_eval_pdf_fast<EXT, DIFF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo,
+                                const EvalPdf ep = bsdf_eval_pdf_fast<BSF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo,
                                                                                  P.its.u, P.its.v);
                                 const f3 bsdfVal = ep.val;
                                 if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
@@ -1409,11 +1410,11 @@ struct PathShader {
                         const bool flip = P.its.wi.z < 0;
                         f3 qwi = P.its.wi;
                         if (flip) qwi.z = -qwi.z;
-                        bs = bsdf_sample_fast<EXT, DIFF>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
+                        bs = bsdf_sample_fast<BSF>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
                                               bx2, by2, u1d, P.its.u, P.its.v);
                         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
                     } else {
-                        bs = bsdf_sample_fast<EXT, DIFF>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                        bs = bsdf_sample_fast<BSF>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
                     }
                     if (!is_zero(bs.weight) && !smp.err) {
                         P.scattered |= bs.sampledType != MTSG_F_NULL;
@@ -1498,6 +1499,25 @@ __device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const P
     if (c.err) atomicAdd(L.counters + 6, (unsigned long long)c.err);
 }
 
+// diagnostic build (-DMTSG_MK_STAMPS): wave cycles per megakernel section,
+// summed into counters 11-14 (start, shadow trace, closest trace, shade) by
+// lane 0 of each wave.  s_memtime without draining the memory counters: a
+// section's loads are consumed inside it (traversal, shading), so the split is
+// close; read shares, not times (tools/mk_stamps.py)
+#ifdef MTSG_MK_STAMPS
+#define MK_STAMP(acc, t0)                                                        \
+    do {                                                                         \
+        unsigned long long t1_;                                                  \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                       \
+        acc += t1_ - t0;                                                         \
+        t0 = t1_;                                                                \
+    } while (0)
+#else
+#define MK_STAMP(acc, t0) (void)0
+#endif
+
 // The persistent megakernel: grid = CUs x resident blocks; every lane runs
 // PathShader steps with both traversals inline
 template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
@@ -1526,6 +1546,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     st.haveRay = st.primary = st.haveShadow = false;
     st.ro = mk(0, 0, 0); st.rd = mk(0, 0, 1); st.sd = mk(0, 0, 1);
     st.rmint = st.rmaxt = st.smaxt = 0;
+#ifdef MTSG_MK_STAMPS
+    unsigned long long mkT[4] = {0, 0, 0, 0}, mkT0;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(mkT0)::"memory");
+#endif
 
     while (true) {
         // ---- A: start the next sample
@@ -1546,6 +1570,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             sh.start(st, it);
         }
         if (__all(done)) break;
+        MK_STAMP(mkT[0], mkT0);
 
         // ---- B: trace the shadow ray, then the closest-hit ray ---------------
         bool occluded = false;
@@ -1600,6 +1625,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
             st.haveShadow = false;
         }
+        MK_STAMP(mkT[1], mkT0);
         if (st.active && st.haveRay) {
             c.rays++;
             float mint, maxt;
@@ -1620,10 +1646,17 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
             st.haveShadow = false;
         }
 
+        MK_STAMP(mkT[2], mkT0);
+
         // ---- C: shade -------------------------------------------------------
         if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
+        MK_STAMP(mkT[3], mkT0);
     }
     path_counters_flush<STATS>(L, c);
+#ifdef MTSG_MK_STAMPS
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
+        for (int k = 0; k < 4; ++k) atomicAdd(L.counters + 11 + k, mkT[k]);
+#endif
 }
 
 // ===========================================================================
@@ -2145,8 +2178,8 @@ __device__ __forceinline__ void bsdf_eval_pdf_2s(const MtsgDeviceScene &S, GBsdf
             if (flip) { qwi.z = -qwi.z; qwo.z = -qwo.z; }
         }
     }
-    val = bsdf_eval_fast<EXT, false>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
-    if (pdf) *pdf = bsdf_pdf_fast<EXT, false>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+    val = bsdf_eval_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
+    if (pdf) *pdf = bsdf_pdf_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(*qb, (glb_f32 *)S.rtrans, qwi, qwo, h.u, h.v);
 }
 template <bool EXT>
 __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsdf &bsdf, const Hit &h, float bx,
@@ -2155,12 +2188,12 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
         const bool flip = h.wi.z < 0;
         f3 qwi = h.wi;
         if (flip) qwi.z = -qwi.z;
-        BSample bs = bsdf_sample_fast<EXT, false>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
+        BSample bs = bsdf_sample_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
                                       u1d, h.u, h.v);
         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
         return bs;
     }
-    return bsdf_sample_fast<EXT, false>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
+    return bsdf_sample_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
 }
 
 // direct_kernel's shadow rays: the any-hit traversal as a separate (not
@@ -2535,8 +2568,36 @@ static void launch_path_w(const MtsgLaunch &L, int grid, bool instr, hipStream_t
     else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, FEAT, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
 }
 
+int mtsg_path_features(const MtsgLaunch &L) {
+    return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | ((L.ext || L.ana) ? MTSG_FEAT_EXT : 0) |
+           (L.ana ? MTSG_FEAT_ANA : 0);
+}
+
+// the specialised BSDF sets compiled for the large-scene megakernel: the
+// scene's features (ENV / EXT / ANA) must match, and the set's restrictions
+// (GGX / NORD / NORC) must hold for the scene (L.bset); dbsdf.h BSet
+#define MTSG_SPEC_BITS (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)
+#define MTSG_SPEC_SETS(X)                                                                         \
+    X(MTSG_FEAT_ENV | MTSG_FEAT_GGX | MTSG_FEAT_NORD)             /* rough conductors, envmap  */ \
+    X(MTSG_FEAT_GGX | MTSG_FEAT_NORC)                             /* rough glass, area lights  */ \
+    X(MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC) /* plastic */
+static int spec_variant(const MtsgLaunch &L) {
+    if (L.scene_lds || L.integrator == MTSG_INTEGRATOR_DIRECT) return 0;
+    const int f = mtsg_path_features(L);
+#define MTSG_SPEC_PICK(V) \
+    if (((V) & ~MTSG_SPEC_BITS) == f && ((V) & MTSG_SPEC_BITS & ~(int)L.bset) == 0) return (V);
+    MTSG_SPEC_SETS(MTSG_SPEC_PICK)
+#undef MTSG_SPEC_PICK
+    return 0;
+}
+
 template <int FEAT>
 static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
+    if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {   // large scenes only (spec_variant)
+        if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
+        else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+        return;
+    }
     if (L.scene_lds) {
         if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {   // no calls: room for 4 waves (capi.cpp)
             if (L.waves == 4) { launch_path_w<true, FEAT, 4>(L, grid, instr, stream); return; }
@@ -2547,10 +2608,6 @@ static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t s
     else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
 }
 
-int mtsg_path_features(const MtsgLaunch &L) {
-    return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | ((L.ext || L.ana) ? MTSG_FEAT_EXT : 0) |
-           (L.ana ? MTSG_FEAT_ANA : 0);
-}
 
 template <int FEAT>
 static void launch_direct(const MtsgLaunch &L, int grid, hipStream_t stream) {
@@ -2571,6 +2628,13 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
             default: launch_direct<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, stream); break;
         }
         return hipGetLastError();
+    }
+    switch (spec_variant(L)) {
+#define MTSG_SPEC_CASE(V) \
+        case (V): launch_path<(V)>(L, grid, instr, stream); return hipGetLastError();
+        MTSG_SPEC_SETS(MTSG_SPEC_CASE)
+#undef MTSG_SPEC_CASE
+        default: break;
     }
     switch (mtsg_path_features(L)) {
         case 0:
@@ -2736,6 +2800,10 @@ static int occupancy_w(const MtsgLaunch &L, int *bpc) {
 }
 template <int FEAT>
 static int occupancy_e(const MtsgLaunch &L, int *bpc) {
+    if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {
+        if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
+        return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
+    }
     if (L.scene_lds) {
         if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {
             if (L.waves == 4) return occupancy_w<true, FEAT, 4>(L, bpc);
@@ -2746,6 +2814,13 @@ static int occupancy_e(const MtsgLaunch &L, int *bpc) {
     return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
 }
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
+    switch (spec_variant(L)) {
+#define MTSG_SPEC_CASE(V) \
+        case (V): return occupancy_e<(V)>(L, blocksPerCU);
+        MTSG_SPEC_SETS(MTSG_SPEC_CASE)
+#undef MTSG_SPEC_CASE
+        default: break;
+    }
     switch (mtsg_path_features(L)) {
         case 0: return L.all_diffuse ? occupancy_e<MTSG_FEAT_DIFF>(L, blocksPerCU) : occupancy_e<0>(L, blocksPerCU);
         case MTSG_FEAT_ENV: return occupancy_e<MTSG_FEAT_ENV>(L, blocksPerCU);

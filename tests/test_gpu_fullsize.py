@@ -61,3 +61,20 @@ def test_full_resolution_row_band_bitexact(gpu_ctx, oracle, cfg, rows):
     assert st_g['samples'] == st_o['samples'] == W * rows[1] * it.sampleCount
     _records_equal(smp_g, smp_o)
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
+@pytest.mark.parametrize('cfg', ['C3', 'C4', 'C5'])
+def test_bsdf_set_variant_equals_generic(gpu_ctx, cfg, monkeypatch):
+    """C3-C5 render through a megakernel specialised to the scene's BSDF set
+    (dbsdf.h BSet: GGX only, no roughdielectric / roughconductor); with
+    MTSGPU_NO_BSDF_SETS=1 the generic all-BSDF variant runs.  Both give the same
+    per-sample records bit for bit (the rows above check the specialised
+    variant against the oracle)."""
+    sc, it = scenes.build(cfg)
+    win = (0, 200, sc.sensor.width, 2)
+    gpu_ctx.upload(sc)
+    _, smp_s, st_s = gpu_ctx.render(it, window=win, samples=True)
+    monkeypatch.setenv('MTSGPU_NO_BSDF_SETS', '1')
+    _, smp_g, st_g = gpu_ctx.render(it, window=win, samples=True)
+    _records_equal(smp_s, smp_g)
+    assert st_s['rays'] == st_g['rays'] and st_s['shadow_rays'] == st_g['shadow_rays']

@@ -70,6 +70,30 @@ def test_row_interleave_sums_to_full(gpu_ctx):
     np.testing.assert_allclose(acc, full, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize('world', [3, 8])
+def test_tile_shards_bitexact_and_sum_to_full(gpu_ctx, oracle, world):
+    """MTSGPU_FLAG_TILE_SHARD (the multi-GPU bench's decomposition): each shard's
+    per-sample records equal the oracle's for the same tiles, the shards cover
+    every sample once, and the box-filter films sum to the full frame bit for bit
+    (a 67x45 window: partial tiles at the right and bottom edges)."""
+    sc, it = scenes.build('C1', width=80, height=56, spp=4)
+    gpu_ctx.upload(sc)
+    win = (5, 3, 67, 45)
+    full, smp_full, _ = gpu_ctx.render(it, window=win, samples=True)
+    acc = np.zeros_like(full)
+    seen = np.zeros(smp_full.shape[0], bool)
+    for k in range(world):
+        f, smp, st = gpu_ctx.render(it, window=win, samples=True, row=(8, world, k), tile_shard=True)
+        fo, smpo, _ = oracle.render(sc, it, window=win, samples=True, row=(8, world, k), tile_shard=True)
+        assert np.all(_bits(smp) == _bits(smpo))
+        mine = np.any(smp != 0, axis=1)
+        assert not (seen & mine).any()
+        seen |= mine
+        acc += f
+    assert seen.sum() == np.any(smp_full != 0, axis=1).sum()
+    np.testing.assert_array_equal(acc.view(np.uint32), full.view(np.uint32))
+
+
 def test_rough_bsdfs_bitexact(gpu_ctx, oracle):
     """roughconductor (GGX/Beckmann/Phong, visible and all-normal sampling) and
     roughdielectric (incl. the extra lobe-choice sample) on the Cornell blocks."""

@@ -10,7 +10,7 @@ OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
-for cfg in ${CONFIGS:-C2 C3 C4}; do
+for cfg in ${CONFIGS:-C2 C3 C4 C5}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench_$cfg -o bench --output-format csv \
       -- python3 $ROOT/bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_$cfg.log 2>&1
   for ctr in FETCH_SIZE WRITE_SIZE; do

@@ -32,8 +32,8 @@ def counter(path_glob, name):
     return vals
 
 
-# samples per profiled launch (one full frame; C5's 1024 spp renders as two 512-spp launches)
-SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 512}
+# samples per profiled launch (one full frame = one launch; C5's 1024 spp fit one splat buffer since r03)
+SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 1024}
 
 for cfg in ('C2', 'C3', 'C4', 'C5'):
     fetch = counter(os.path.join(src, 'pmc_%s_FETCH_SIZE' % cfg, '**', '*counter_collection.csv'), 'FETCH_SIZE')
