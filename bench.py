@@ -128,10 +128,14 @@ def roofline_line(bps, launch_samples, kernel_s, cfg):
       hbm   -- measured HBM bytes per sample (separate FETCH_SIZE / WRITE_SIZE
                passes, FETCH doubled per MI355X_MICROARCH.md) x samples / time,
                against the 8 TB/s HBM3E peak;
-      valu  -- SQ_INSTS_VALU per sample x 64 lanes x samples / time, against the
-               VALU issue peak at the pass's measured shader clock (one wave64
-               VALU instruction per SIMD per 2 cycles = 32 lane-ops/cycle/SIMD,
-               1024 SIMDs; clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time).
+      valu  -- VALU-busy SIMD cycles per sample (4 x SQ_ACTIVE_INST_VALU, which
+               counts quad-cycles) x samples / time, against the SIMD cycles
+               available (1024 SIMDs x the pass's measured shader clock, clock =
+               GRBM_GUI_ACTIVE / 8 XCDs / kernel time): the fraction of cycles
+               the vector ALUs are busy.  The issue-based rate (SQ_INSTS_VALU x
+               64 lanes against one wave64 VALU instruction per SIMD per 2
+               cycles) is kept beside it: the gap is multi-cycle instructions
+               (f64, transcendentals, correctly rounded division).
     `bound` is the one of the two with the larger fraction; the other is kept,
     and so is the SURVEY.md 8(d) no-reuse byte model (`hbm_model`)."""
     traffic = measured_profile('traffic', cfg)
@@ -147,13 +151,16 @@ def roofline_line(bps, launch_samples, kernel_s, cfg):
                'bytes_per_sample': round(traffic['hbm_bytes_per_sample'], 1),
                'write_bytes_per_sample': traffic.get('write_bytes_per_sample'), 'source': traffic['source']}
     vl = None
-    if valu and valu.get('valu_insts_per_sample') and valu.get('clock_hz'):
-        a = valu['valu_insts_per_sample'] * 64 * launch_samples / kernel_s / 1e12
-        pk = 1024 * 32 * valu['clock_hz'] / 1e12
-        vl = {'achieved': round(a, 3), 'peak': round(pk, 3), 'unit': 'Tlane-op/s', 'frac': round(a / pk, 5),
-              'valu_insts_per_sample': round(valu['valu_insts_per_sample'], 2),
+    if valu and valu.get('valu_busy_cycles_per_sample') and valu.get('clock_hz'):
+        a = valu['valu_busy_cycles_per_sample'] * launch_samples / kernel_s / 1e9
+        pk = 1024 * valu['clock_hz'] / 1e9
+        ia = valu['valu_insts_per_sample'] * 64 * launch_samples / kernel_s / 1e12
+        ipk = 1024 * 32 * valu['clock_hz'] / 1e12
+        vl = {'achieved': round(a, 1), 'peak': round(pk, 1), 'unit': 'G VALU-busy SIMD-cycles/s',
+              'frac': round(a / pk, 5),
+              'issue': {'achieved': round(ia, 3), 'peak': round(ipk, 3), 'unit': 'Tlane-op/s',
+                        'frac': round(ia / ipk, 5), 'valu_insts_per_sample': round(valu['valu_insts_per_sample'], 2)},
               'clock_mhz': round(valu['clock_hz'] / 1e6, 1),
-              'valu_busy_per_simd': round(valu['valu_busy_per_simd'], 4),
               'wait_frac_per_wave': round(valu['wait_frac_per_wave'], 4), 'source': valu['source']}
     cands = [(k, v) for k, v in (('hbm', hbm), ('valu', vl)) if v]
     if not cands:
@@ -198,7 +205,7 @@ def cpu_baseline(scene, integ, threads):
     """The CPU restatement (oracle, OpenMP, glibc transcendentals as the
     reference) on a bounded sample of the same workload: the full frame at a
     reduced spp (the first spp Sobol samples of every pixel, sized by a pilot
-    pass to about 15 s of CPU work).  Threads: all
+    pass to about 25 s of CPU work).  Threads: all
     cores this job may use -- OMP_NUM_THREADS when the host sets it (the GPU
     boxes give a job a 16-CPU share of a larger machine), else the affinity
     mask; never more than the cgroup's CPU quota, which the line records."""
@@ -212,14 +219,14 @@ def cpu_baseline(scene, integ, threads):
         if quota:
             threads = max(1, min(threads, int(quota)))
     it = copy.copy(integ)
-    # size the sample to ~15 s of CPU work: a pilot pass (1/32 of the rows at
+    # size the sample to ~25 s of CPU work: a pilot pass (1/32 of the rows at
     # 8 spp) measures this config's per-sample cost, then the full frame runs
     # at the spp that fits (1..256, a power of two)
     it.sampleCount = 8
     t0 = time.perf_counter()
     _, _, pst = ob.render(scene, it, libm_mode=0, threads=threads, row=(1, 32, 0))
     rate = pst['samples'] / max(1e-6, time.perf_counter() - t0)
-    fit = 15.0 * rate / (scene.sensor.width * scene.sensor.height)
+    fit = 25.0 * rate / (scene.sensor.width * scene.sensor.height)
     spp = 1
     while spp * 2 <= min(integ.sampleCount, 256) and spp * 2 <= fit:
         spp *= 2

@@ -87,6 +87,7 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
            'issue_stall_frac_per_wave': c['SQ_WAIT_INST_ANY'] / wc,
            'valu_insts_per_wave': c['SQ_INSTS_VALU'] / max(1.0, c['SQ_WAVES']),
            'valu_insts_per_sample': c['SQ_INSTS_VALU'] / pass_samples,
+           'valu_busy_cycles_per_sample': 4 * c['SQ_ACTIVE_INST_VALU'] / pass_samples,
            'kernel_s': sum(durs) / len(durs) if durs else None,
            'clock_hz': c['GRBM_GUI_ACTIVE'] / XCDS / (sum(durs) / len(durs)) if durs else None,
            'note': '1/4 of the rows (tools/prof_run.py %s 1 4); SQ cycle counters in quad-cycles' % cfg}
