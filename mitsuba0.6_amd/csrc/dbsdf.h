@@ -556,9 +556,36 @@ __device__ __forceinline__ float rt_eval_diffuse(GBsdf &b, glb_f32 *rt, float al
     return smin(1.0f, smax(0.0f, result));
 }
 
+// RoughPlastic's per-vertex rough-transmittance terms.  eval() forms T12 =
+// m_externalRoughTransmittance->eval(cosTheta(wi), alpha) and Fdr = 1 -
+// m_internalRoughTransmittance->evalDiffuse(alpha), pdf() and sample() form the
+// same T12 for probSpecular (roughplastic.cpp:300-458; rtrans.h:184-208,
+// 236-247): they depend only on the vertex (wi and the roughness at the hit),
+// so the kernel forms them once per vertex and hands them to every query there
+// -- the same values, from 2 instead of 7 table lookups per bounce
+struct RpPre { float twi, fdr; };
+template <int BS>
+__device__ __forceinline__ RpPre rp_pre(GBsdf &b, glb_f32 *rt, f3 wi, float u, float v) {
+    const Distr d = bsdf_distr<BS>(b, u, v);
+    RpPre p;
+    p.twi = rt_eval(b, rt, wi.z, d.alphaU);
+    p.fdr = 1 - rt_eval_diffuse(b, rt, d.alphaU);
+    return p;
+}
+
+// the terms for the BSDF `b` queried with `wi` (zero for any other BSDF)
+template <int BS>
+__device__ __forceinline__ RpPre rp_pre_for(GBsdf &b, glb_f32 *rt, f3 wi, float u, float v) {
+    RpPre p = {0.0f, 0.0f};
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) p = rp_pre<BS>(b, rt, wi, u, v);
+    }
+    return p;
+}
+
 // probSpecular of roughplastic's pdf()/sample() (roughplastic.cpp:371-378, 424-431)
-__device__ __forceinline__ float rp_prob_specular(GBsdf &b, glb_f32 *rt, float cosThetaI, float alpha) {
-    float probSpecular = 1 - rt_eval(b, rt, cosThetaI, alpha);
+__device__ __forceinline__ float rp_prob_specular(GBsdf &b, float twi) {
+    float probSpecular = 1 - twi;
     probSpecular = (probSpecular * b.spec_weight) /
                    (probSpecular * b.spec_weight + (1 - probSpecular) * (1 - b.spec_weight));
     return probSpecular;
@@ -566,7 +593,7 @@ __device__ __forceinline__ float rp_prob_specular(GBsdf &b, glb_f32 *rt, float c
 
 // RoughPlastic::eval (roughplastic.cpp:300-345)
 template <int BS>
-__device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
     if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
     const Distr d = bsdf_distr<BS>(b, u, v);
     f3 result = mk(0, 0, 0);
@@ -580,9 +607,9 @@ __device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, 
         result = add(result, mul(ld3(b.spec_r), value));
     }
     f3 diff = bsdf_refl<BS>(b, u, v);
-    const float T12 = rt_eval(b, rt, wi.z, d.alphaU);
+    const float T12 = pre.twi;
     const float T21 = rt_eval(b, rt, wo.z, d.alphaU);
-    const float Fdr = 1 - rt_eval_diffuse(b, rt, d.alphaU);
+    const float Fdr = pre.fdr;
     if (b.nonlinear) diff = divv(diff, sub(mk(1.0f, 1.0f, 1.0f), mul(diff, Fdr)));
     else diff = divs(diff, 1 - Fdr);
     return add(result, mul(diff, D_INV_PI * wo.z * T12 * T21 * b.inv_eta2));
@@ -590,11 +617,11 @@ __device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, 
 
 // RoughPlastic::pdf (roughplastic.cpp:347-393)
 template <int BS>
-__device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
     if (wi.z <= 0 || wo.z <= 0) return 0.0f;
     const Distr d = bsdf_distr<BS>(b, u, v);
     const f3 H = normalize(add(wo, wi));
-    const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
+    const float probSpecular = rp_prob_specular(b, pre.twi);
     const float probDiffuse = 1 - probSpecular;
     const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
     const float prob = distr_pdf<BS>(d, wi, H);
@@ -603,20 +630,20 @@ __device__ __forceinline__ float rp_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
     return result;
 }
 template <int BS>
-BSDF_CALL f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return rp_eval_body<BS>(b, rt, wi, wo, u, v);
+BSDF_CALL f3 rp_eval(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
+    return rp_eval_body<BS>(b, rt, wi, wo, u, v, pre);
 }
 template <int BS>
-BSDF_CALL float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    return rp_pdf_body<BS>(b, rt, wi, wo, u, v);
+BSDF_CALL float rp_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
+    return rp_pdf_body<BS>(b, rt, wi, wo, u, v, pre);
 }
 struct EvalPdf { f3 val; float pdf; };
 // eval, and pdf where the value is nonzero, of one query in one call (NEE)
 template <int BS>
-BSDF_CALL EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+BSDF_CALL EvalPdf rp_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
     EvalPdf r;
-    r.val = rp_eval_body<BS>(b, rt, wi, wo, u, v);
-    r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body<BS>(b, rt, wi, wo, u, v);
+    r.val = rp_eval_body<BS>(b, rt, wi, wo, u, v, pre);
+    r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body<BS>(b, rt, wi, wo, u, v, pre);
     return r;
 }
 
@@ -714,7 +741,7 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
         return mul(bsdf_refl<BS>(b, u, v), D_INV_PI * wo.z);
     }
     if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval<BS>(b, rt, wi, wo, u, v);
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
         if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
     }
     if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:257-292
@@ -763,7 +790,7 @@ __device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 
         return D_INV_PI * wo.z;
     }
     if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf<BS>(b, rt, wi, wo, u, v);
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
         if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
     }
     if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:294-319
@@ -809,9 +836,9 @@ BSDF_CALL float bsdf_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) 
 // (the NEE estimate of path.cpp:176-199 needs both): one out-of-line call, so
 // the caller's live registers are saved around one call instead of two
 template <int BS>
-BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
     if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval_pdf<BS>(b, rt, wi, wo, u, v);
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval_pdf<BS>(b, rt, wi, wo, u, v, pre);
     }
     EvalPdf r;
     r.val = bsdf_eval_body<BS>(b, rt, wi, wo, u, v);
@@ -825,13 +852,13 @@ BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, fl
 
 // RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458)
 template <int BS>
-BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v) {
+BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v, RpPre pre) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (wi.z <= 0) return r;
     bool choseSpecular = true;
     const Distr d = bsdf_distr<BS>(b, u, v);
-    const float probSpecular = rp_prob_specular(b, rt, wi.z, d.alphaU);
+    const float probSpecular = rp_prob_specular(b, pre.twi);
     if (sy < probSpecular) {
         sy /= probSpecular;
     } else {
@@ -849,14 +876,15 @@ BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, fl
         r.wo = square_to_cosine_hemisphere(sx, sy);
     }
     r.eta = 1.0f;
-    r.pdf = rp_pdf<BS>(b, rt, wi, r.wo, u, v);
+    r.pdf = rp_pdf<BS>(b, rt, wi, r.wo, u, v, pre);
     if (r.pdf == 0) return r;
-    r.weight = divs(rp_eval<BS>(b, rt, wi, r.wo, u, v), r.pdf);
+    r.weight = divs(rp_eval<BS>(b, rt, wi, r.wo, u, v, pre), r.pdf);
     return r;
 }
 
 template <int BS>
-BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v) {
+BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v,
+                              RpPre pre) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150
@@ -869,7 +897,7 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
         return r;
     }
     if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample<BS>(b, rt, wi, sx, sy, u, v);
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample<BS>(b, rt, wi, sx, sy, u, v, pre);
         if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
     }
     if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:357-406
@@ -956,19 +984,20 @@ __device__ __forceinline__ float bsdf_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 
     }
 }
 template <int BS>
-__device__ __forceinline__ EvalPdf bsdf_eval_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ EvalPdf bsdf_eval_pdf_fast(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v,
+                                                      RpPre pre) {
     if constexpr (BSet<BS>::DIFF) {
         EvalPdf r;
         r.val = bsdf_eval_fast<BS>(b, rt, wi, wo, u, v);
         r.pdf = bsdf_pdf_fast<BS>(b, rt, wi, wo, u, v);
         return r;
     } else {
-        return bsdf_eval_pdf<BS>(b, rt, wi, wo, u, v);
+        return bsdf_eval_pdf<BS>(b, rt, wi, wo, u, v, pre);
     }
 }
 template <int BS>
 __device__ __forceinline__ BSample bsdf_sample_fast(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d,
-                                                    float u, float v) {
+                                                    float u, float v, RpPre pre) {
     if constexpr (BSet<BS>::DIFF) {
         BSample r;
         r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
@@ -979,6 +1008,6 @@ __device__ __forceinline__ BSample bsdf_sample_fast(GBsdf &b, glb_f32 *rt, f3 wi
         r.weight = bsdf_refl<BS>(b, u, v);
         return r;
     } else {
-        return bsdf_sample<BS>(b, rt, wi, sx, sy, u1d, u, v);
+        return bsdf_sample<BS>(b, rt, wi, sx, sy, u1d, u, v, pre);
     }
 }

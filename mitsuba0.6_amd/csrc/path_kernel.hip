@@ -435,6 +435,178 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
 
 #endif
 
+// A bounce's shadow ray and closest-hit ray through the BVH together (the
+// BVH analogue of scan_pair): one traversal whose stack entries carry a 2-bit
+// mask of the rays that still need the subtree (bit 0 closest, bit 1 shadow,
+// in the low bits of the bf16 entry distance -- truncating it further keeps it
+// a lower bound), so the nodes both rays visit are fetched and tested once and
+// the two chains of dependent node loads overlap.  Results equal the separate
+// traversals': the closest hit is the smallest t (ties: larger primitive
+// index) over every triangle whose leaf the closest ray reaches, culling only
+// by the closest ray's own entry distance; the shadow ray's answer is whether
+// any triangle in its interval is hit (ShapeKDTree::rayIntersect(ray), its
+// traversal stops at the first hit).  Each ray keeps its own origin.
+template <bool STATS, typename NodeT, typename TriT>
+__device__ __forceinline__ void tri_test(TriT *tr, f3 o, f3 d, float mint, float maxt, bool &hit, float &t_, float &u_,
+                                         float &v_, uint32_t &prim) {
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+    const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
+    const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
+    const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
+    const uint32_t k = __float_as_uint(q0.x);
+    hit = false;
+    float o_u, o_v, o_k, d_u, d_v, d_k;   // TriAccel::rayIntersect (triaccel.h:92-160)
+    if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
+    else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
+    else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+    const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
+    const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+    if (t < mint || t > maxt) return;
+    const float hu = o_u + t * d_u - q1.x;
+    const float hv = o_v + t * d_v - q1.y;
+    const float u = hv * q1.z + hu * q1.w;
+    const float v = hu * q2.x + hv * q2.y;
+    if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+        hit = true; t_ = t; u_ = u; v_ = v; prim = __float_as_uint(q2.z);
+    }
+}
+
+template <bool STATS, typename NodeT, typename TriT>
+__device__ __forceinline__ void traverse_pair(NodeT *nodesArr, TriT *trisArr, f3 oc, f3 dc, float mintC, float maxtC,
+                                              bool actC, f3 os, f3 ds, float mintS, float maxtS, bool actS,
+                                              lds_stk_n *stkN, lds_stk_d *stkD, bool &found, uint32_t &bestSlot,
+                                              float &bu, float &bv, float &bt, bool &occluded,
+                                              unsigned long long &nodes, unsigned long long &tests) {
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
+    const float icx = (dc.x == 0.0f) ? copysignf(1e30f, dc.x) : 1.0f / dc.x;
+    const float icy = (dc.y == 0.0f) ? copysignf(1e30f, dc.y) : 1.0f / dc.y;
+    const float icz = (dc.z == 0.0f) ? copysignf(1e30f, dc.z) : 1.0f / dc.z;
+    const float ocx = oc.x * icx, ocy = oc.y * icy, ocz = oc.z * icz;
+    const float isx = (ds.x == 0.0f) ? copysignf(1e30f, ds.x) : 1.0f / ds.x;
+    const float isy = (ds.y == 0.0f) ? copysignf(1e30f, ds.y) : 1.0f / ds.y;
+    const float isz = (ds.z == 0.0f) ? copysignf(1e30f, ds.z) : 1.0f / ds.z;
+    const float osx = os.x * isx, osy = os.y * isy, osz = os.z * isz;
+    constexpr int DONE = 0x7fffffff;
+    found = false;
+    occluded = false;
+    uint32_t bestPrim = 0;
+    bt = maxtC;
+    uint32_t live = (actC ? 1u : 0u) | (actS ? 2u : 0u);   // rays not finished
+    int sp = 0;
+    int node = live ? 0 : DONE, leaf = 0;
+    uint32_t m = live, lm = 0;   // masks of `node` and of the parked leaf
+    auto pop = [&](uint32_t &pm) -> int {
+        while (sp > 0) {
+            --sp;
+            const uint32_t h = stkD[sp * BLOCK];
+            uint32_t em = h & 3u & live;
+            if ((em & 1u) && dist_up16((uint16_t)(h & ~3u)) > bt) em &= ~1u;
+            if (em) { pm = em; return stkN[sp * BLOCK]; }
+        }
+        pm = 0;
+        return DONE;
+    };
+    while (node != DONE || leaf < 0) {
+        while ((uint32_t)node < (uint32_t)DONE) {
+            m &= live;   // the shadow ray may have been answered since this entry was pushed
+            if (m == 0) {
+                node = pop(m);
+                if (node < 0 && leaf == 0) { leaf = node; lm = m; node = pop(m); }
+                if (!__any(leaf == 0)) break;
+                continue;
+            }
+            if (STATS) nodes++;
+            NodeT *n = nodesArr + node;
+            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
+            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
+            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
+            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+            // closest ray: slab tests (boxes conservatively inflated on the host)
+            float t0x = __builtin_fmaf(a.x, icx, -ocx), t1x = __builtin_fmaf(a.y, icx, -ocx);
+            float t0y = __builtin_fmaf(a.z, icy, -ocy), t1y = __builtin_fmaf(a.w, icy, -ocy);
+            float t0z = __builtin_fmaf(c.x, icz, -ocz), t1z = __builtin_fmaf(c.y, icz, -ocz);
+            const float n0c = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mintC));
+            const float f0c = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            t0x = __builtin_fmaf(b.x, icx, -ocx); t1x = __builtin_fmaf(b.y, icx, -ocx);
+            t0y = __builtin_fmaf(b.z, icy, -ocy); t1y = __builtin_fmaf(b.w, icy, -ocy);
+            t0z = __builtin_fmaf(c.z, icz, -ocz); t1z = __builtin_fmaf(c.w, icz, -ocz);
+            const float n1c = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mintC));
+            const float f1c = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+            // shadow ray
+            t0x = __builtin_fmaf(a.x, isx, -osx); t1x = __builtin_fmaf(a.y, isx, -osx);
+            t0y = __builtin_fmaf(a.z, isy, -osy); t1y = __builtin_fmaf(a.w, isy, -osy);
+            t0z = __builtin_fmaf(c.x, isz, -osz); t1z = __builtin_fmaf(c.y, isz, -osz);
+            const float n0s = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mintS));
+            const float f0s = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), maxtS));
+            t0x = __builtin_fmaf(b.x, isx, -osx); t1x = __builtin_fmaf(b.y, isx, -osx);
+            t0y = __builtin_fmaf(b.z, isy, -osy); t1y = __builtin_fmaf(b.w, isy, -osy);
+            t0z = __builtin_fmaf(c.z, isz, -osz); t1z = __builtin_fmaf(c.w, isz, -osz);
+            const float n1s = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mintS));
+            const float f1s = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), maxtS));
+            const uint32_t m0 = m & ((n0c <= f0c ? 1u : 0u) | (n0s <= f0s ? 2u : 0u));
+            const uint32_t m1 = m & ((n1c <= f1c ? 1u : 0u) | (n1s <= f1s ? 2u : 0u));
+            if (m0 && m1) {
+                // near child first by the closest ray's entry distance where it enters
+                // both, else by the shadow ray's
+                const bool swap = ((m0 & m1 & 1u) ? n1c < n0c : n1s < n0s);
+                const int nearC = swap ? e.y : e.x, farC = swap ? e.x : e.y;
+                const uint32_t nm = swap ? m1 : m0, fm = swap ? m0 : m1;
+                const float farT = (fm & 1u) ? (swap ? n0c : n1c) : 0.0f;
+                stkN[sp * BLOCK] = farC;
+                stkD[sp * BLOCK] = (uint16_t)((dist_down16(farT) & ~3u) | fm);
+                ++sp;
+                node = nearC;
+                m = nm;
+            } else if (m0) {
+                node = e.x; m = m0;
+            } else if (m1) {
+                node = e.y; m = m1;
+            } else {
+                node = pop(m);
+            }
+            // park the first leaf reached and keep descending
+            if (node < 0 && leaf == 0) {
+                leaf = node;
+                lm = m;
+                node = pop(m);
+            }
+            if (!__any(leaf == 0)) break;
+        }
+        // leaves
+        while (leaf < 0) {
+            const uint32_t ref = (uint32_t)(~leaf);
+            const uint32_t first = ref >> 4, count = ref & 15u;
+            lm &= live;
+            for (uint32_t i = first; i < first + count && lm; ++i) {
+                TriT *tr = trisArr + i;
+                if (lm & 1u) {
+                    if (STATS) tests++;
+                    bool h; float t, u, v; uint32_t prim;
+                    tri_test<STATS, NodeT>(tr, oc, dc, mintC, bt, h, t, u, v, prim);
+                    // ties (t == bt): the larger primitive index wins
+                    if (h && (!found || t < bt || prim > bestPrim)) {
+                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
+                    }
+                }
+                if (lm & 2u) {
+                    if (STATS) tests++;
+                    bool h; float t, u, v; uint32_t prim;
+                    tri_test<STATS, NodeT>(tr, os, ds, mintS, maxtS, h, t, u, v, prim);
+                    if (h) { occluded = true; live &= ~2u; lm &= ~2u; }
+                }
+            }
+            leaf = 0;
+            if (live == 0) { node = DONE; break; }   // no closest ray, shadow answered
+            if (node < 0) {   // the next stack entry is a leaf too: take it now
+                leaf = node;
+                lm = m;
+                node = pop(m);
+            }
+        }
+    }
+}
+
 typedef __attribute__((address_space(4))) const MtsgTri cst_tri;
 // one projection axis' records: the coordinate permutation is a compile-time
 // constant, so the loop is straight-line code around the correctly rounded
@@ -1285,6 +1457,22 @@ struct PathShader {
             } else {
                 auto &sh = hs.shapes[P.its.shape];
                 GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
+                // roughplastic's per-vertex transmittance terms (dbsdf.h rp_pre), formed
+                // at the first query of this vertex and reused for the same BSDF and wi
+                RpPre rpc = {0.0f, 0.0f};
+                GBsdf *rpB = nullptr;
+                float rpZ = 0.0f;
+                auto rpPre = [&](GBsdf *qb, f3 qwi) -> RpPre {
+                    if constexpr (EXT) {
+                        if (qb->type == BSDF_ROUGHPLASTIC &&
+                            !(rpB == qb && __float_as_uint(rpZ) == __float_as_uint(qwi.z))) {
+                            rpc = rp_pre<BSF>(*qb, (glb_f32 *)S.rtrans, qwi, P.its.u, P.its.v);
+                            rpB = qb;
+                            rpZ = qwi.z;
+                        }
+                    }
+                    return rpc;
+                };
                 if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
                     P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
                 // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
@@ -1374,7 +1562,7 @@ struct PathShader {
                                     }
                                 }
                                 const EvalPdf ep = bsdf_eval_pdf_fast<BSF>(*qb, (glb_f32 *)S.rtrans, qwi, qwo,
-                                                                                 P.its.u, P.its.v);
+                                                                           P.its.u, P.its.v, rpPre(qb, qwi));
                                 const f3 bsdfVal = ep.val;
                                 if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
                                     const float bsdfPdf = ep.pdf;
@@ -1410,11 +1598,13 @@ struct PathShader {
                         const bool flip = P.its.wi.z < 0;
                         f3 qwi = P.its.wi;
                         if (flip) qwi.z = -qwi.z;
-                        bs = bsdf_sample_fast<BSF>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi,
-                                              bx2, by2, u1d, P.its.u, P.its.v);
+                        GBsdf *nb = &((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
+                        bs = bsdf_sample_fast<BSF>(*nb, (glb_f32 *)S.rtrans, qwi, bx2, by2, u1d, P.its.u, P.its.v,
+                                                   rpPre(nb, qwi));
                         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
                     } else {
-                        bs = bsdf_sample_fast<BSF>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v);
+                        bs = bsdf_sample_fast<BSF>(bsdf, (glb_f32 *)S.rtrans, P.its.wi, bx2, by2, u1d, P.its.u, P.its.v,
+                                                   rpPre(&bsdf, P.its.wi));
                     }
                     if (!is_zero(bs.weight) && !smp.err) {
                         P.scattered |= bs.sampledType != MTSG_F_NULL;
@@ -1518,6 +1708,16 @@ __device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const P
 #define MK_STAMP(acc, t0) (void)0
 #endif
 
+// -DMTSG_PAIR_TRAVERSAL: a bounce's shadow and closest-hit rays through the
+// BVH in one traversal (traverse_pair).  Off: its second ray's registers made
+// the large-scene variants spill (C4 35 -> 127 VGPRs) and it lost C3 -9%,
+// C4 -19%, C5 -4% (profiles/r03_ab_pair_C*.log)
+#ifdef MTSG_PAIR_TRAVERSAL
+#define PAIR_TRAVERSAL true
+#else
+#define PAIR_TRAVERSAL false
+#endif
+
 // The persistent megakernel: grid = CUs x resident blocks; every lane runs
 // PathShader steps with both traversals inline
 template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
@@ -1599,6 +1799,28 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                                  prim, hu, hv, ht, c.tests);
             hit = hit && okC;
             occluded = occluded && okS;
+        } else if (PAIR_TRAVERSAL && !ANA) {
+            // both rays of the bounce in one BVH traversal (traverse_pair)
+            float minS = 0, maxS = 0, minC = 0, maxC = 0;
+            bool okS = false, okC = false;
+            if (st.active && st.haveShadow) {
+                c.shadow++;
+#ifndef MTSG_ABL_NO_SHADOW
+                if (!is_zero(st.P.neeC)) okS = ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, minS, maxS);
+#endif
+            }
+            if (st.active && st.haveRay) {
+                c.rays++;
+                okC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
+            }
+            if (SCENE_LDS)
+                traverse_pair<STATS>(ldsNodes, ldsTris, st.ro, st.rd, minC, maxC, okC, st.P.its.p, st.sd, minS, maxS,
+                                     okS, stkN, stkD, hit, slot, hu, hv, ht, occluded, c.nodes, c.tests);
+            else
+                traverse_pair<STATS>((glb_node *)S.nodes, (glb_tri *)S.tris, st.ro, st.rd, minC, maxC, okC,
+                                     st.P.its.p, st.sd, minS, maxS, okS, stkN, stkD, hit, slot, hu, hv, ht, occluded,
+                                     c.nodes, c.tests);
+            if (hit) prim = SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
         } else {
         if (st.active && st.haveShadow) {
             c.shadow++;
@@ -2188,12 +2410,16 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
         const bool flip = h.wi.z < 0;
         f3 qwi = h.wi;
         if (flip) qwi.z = -qwi.z;
-        BSample bs = bsdf_sample_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]], (glb_f32 *)S.rtrans, qwi, bx, by,
-                                      u1d, h.u, h.v);
+        constexpr int BS = EXT ? (int)MTSG_FEAT_EXT : 0;
+        GBsdf &nb = ((GBsdf *)S.bsdfs)[bsdf.nested[flip ? 1 : 0]];
+        BSample bs = bsdf_sample_fast<BS>(nb, (glb_f32 *)S.rtrans, qwi, bx, by, u1d, h.u, h.v,
+                                          rp_pre_for<BS>(nb, (glb_f32 *)S.rtrans, qwi, h.u, h.v));
         if (flip && !is_zero(bs.weight) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
         return bs;
     }
-    return bsdf_sample_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v);
+    return bsdf_sample_fast<(EXT ? (int)MTSG_FEAT_EXT : 0)>(
+        bsdf, (glb_f32 *)S.rtrans, h.wi, bx, by, u1d, h.u, h.v,
+        rp_pre_for<(EXT ? (int)MTSG_FEAT_EXT : 0)>(bsdf, (glb_f32 *)S.rtrans, h.wi, h.u, h.v));
 }
 
 // direct_kernel's shadow rays: the any-hit traversal as a separate (not

@@ -582,12 +582,27 @@ struct BuildPrim { BBox box; float c[3]; uint32_t id; };
 
 const uint32_t kMaxDepth = 28;   // traversal stack (LDS) holds < 32 entries
 
+// SAH knobs (A/B only; results never depend on them): MTSGPU_SAH_BINS (128: C3 +3.4%,
+// C4 +0.7% over 32, profiles/r03_ab_sah_C*.log),
+// MTSGPU_SAH_CI (cost of a triangle test per node visit, 1), MTSGPU_LEAF_MAX (8, <= 15)
+static int env_int(const char *k, int def, int lo, int hi) {
+    const char *v = std::getenv(k);
+    return v ? std::max(lo, std::min(hi, std::atoi(v))) : def;
+}
+static float env_float(const char *k, float def) {
+    const char *v = std::getenv(k);
+    return v ? (float)std::atof(v) : def;
+}
+
 struct Builder {
     std::vector<BuildPrim> &prims;
     std::vector<MtsgNode> &nodes;
     std::vector<uint32_t> order;
     float absEps;
     uint32_t maxDepth = 0;
+    const int nbins = env_int("MTSGPU_SAH_BINS", 128, 4, 1024);
+    const float ci = env_float("MTSGPU_SAH_CI", 1.0f);
+    const uint32_t leafMax = (uint32_t)env_int("MTSGPU_LEAF_MAX", MTSG_LEAF_MAX, 1, 15);
     explicit Builder(std::vector<BuildPrim> &p, std::vector<MtsgNode> &n) : prims(p), nodes(n) {}
 
     void inflate(BBox &b) const {
@@ -604,7 +619,7 @@ struct Builder {
     // returns child reference for the range
     int32_t build(uint32_t first, uint32_t count, uint32_t depth) {
         maxDepth = std::max(maxDepth, depth);
-        if (count <= 2 || (count <= MTSG_LEAF_MAX && depth >= kMaxDepth - 1))
+        if (count <= 2 || (count <= leafMax && depth >= kMaxDepth - 1))
             return mtsg_leaf_ref(first, count);
         // switch to median splits early enough that depth stays <= kMaxDepth
         uint32_t lg = 0;
@@ -612,14 +627,16 @@ struct Builder {
         const bool forceMedian = depth + lg + 2 >= kMaxDepth;
         BBox cb; cb.reset();
         for (uint32_t i = first; i < first + count; ++i) cb.growp(prims[order[i]].c);
-        const int NB = 32;
+        const int NB = nbins;
         float bestCost = FLT_MAX; int bestAxis = -1, bestSplit = -1;
         const BBox nb = bounds(first, count);
-        const float leafCost = (float)count;
+        const float leafCost = ci * (float)count;
+        std::vector<BBox> bb(NB), lb(NB);
+        std::vector<uint32_t> bc(NB), lc(NB);
         for (int axis = 0; axis < 3; ++axis) {
             const float ext = cb.hi[axis] - cb.lo[axis];
             if (!(ext > 0)) continue;
-            BBox bb[NB]; uint32_t bc[NB] = {0};
+            std::fill(bc.begin(), bc.end(), 0u);
             for (int i = 0; i < NB; ++i) bb[i].reset();
             const float k = NB / ext;
             for (uint32_t i = first; i < first + count; ++i) {
@@ -627,20 +644,19 @@ struct Builder {
                 int bi = std::min(NB - 1, (int)((p.c[axis] - cb.lo[axis]) * k));
                 bb[bi].grow(p.box); bc[bi]++;
             }
-            BBox lb[NB]; uint32_t lc[NB];
             BBox acc; acc.reset(); uint32_t n = 0;
             for (int i = 0; i < NB; ++i) { acc.grow(bb[i]); n += bc[i]; lb[i] = acc; lc[i] = n; }
             acc.reset(); n = 0;
             for (int i = NB - 1; i > 0; --i) {
                 acc.grow(bb[i]); n += bc[i];
                 if (lc[i - 1] == 0 || n == 0) continue;
-                const float cost = 1.0f + (lb[i - 1].area() * lc[i - 1] + acc.area() * n) / std::max(nb.area(), 1e-30f);
+                const float cost = 1.0f + ci * (lb[i - 1].area() * lc[i - 1] + acc.area() * n) / std::max(nb.area(), 1e-30f);
                 if (cost < bestCost) { bestCost = cost; bestAxis = axis; bestSplit = i; }
             }
         }
         uint32_t mid;
-        if (bestAxis < 0 || (count <= MTSG_LEAF_MAX && bestCost >= leafCost)) {
-            if (count <= MTSG_LEAF_MAX) return mtsg_leaf_ref(first, count);
+        if (bestAxis < 0 || (count <= leafMax && bestCost >= leafCost)) {
+            if (count <= leafMax) return mtsg_leaf_ref(first, count);
             // degenerate centroids: median split on index order
             mid = first + count / 2;
         } else {

@@ -112,6 +112,10 @@ def smooth_materials():
                                  BSDF('roughconductor', distribution='ggx', alpha=0.2, material='Au')]),
         BSDF('conductor', material='none', specularReflectance=0.8),
         BSDF('dielectric', intIOR=1.33, extIOR=1.0, specularTransmittance=(0.9, 0.8, 0.7)),
+        # roughplastic inside twosided: its per-vertex transmittance terms are
+        # formed for the nested BSDF and the side's wi (path_kernel rpPre)
+        BSDF('twosided', nested=[BSDF('roughplastic', distribution='ggx', alpha=0.2,
+                                      diffuseReflectance=(0.6, 0.3, 0.2))]),
     ]
 
 
@@ -138,14 +142,15 @@ def cornell_box(width=512, height=512, spp=64, rfilter='box', max_depth=-1, mate
         floor_b, short_b, tall_b, back_b = base + 4, base + 1, base + 0, base + 5
     if materials == 'shapes':
         return _cornell_shapes(width, height, spp, rfilter, max_depth)
-    green_b, flip_back = 2, False
+    green_b, red_b, flip_back = 2, 1, False
     if materials == 'smooth':
         # the back wall shows its back side (flipped normals) through twosided
         base = len(bsdfs)
         bsdfs += smooth_materials()
         floor_b, short_b, tall_b, back_b, green_b, flip_back = base + 3, base + 0, base + 1, base + 5, base + 4, True
+        red_b = base + 8
     uv = materials in ('rough', 'plastic', 'smooth')   # UV tangents (anisotropic BSDFs) and texture coordinates
-    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, back_b), (_GREEN, green_b), (_RED, 1)):
+    for quad, b in ((_FLOOR, floor_b), (_CEIL, 0), (_BACK, back_b), (_GREEN, green_b), (_RED, red_b)):
         m = _quads_mesh([quad], inward=True, uv=uv)
         meshes.append(Mesh(m[0], m[1], texcoords=m[2] if uv else None, bsdf=b,
                            flipNormals=flip_back and quad is _BACK))
