@@ -280,6 +280,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                         float at, alx, aly;
                         if (k == MTSG_K_ANALYTIC &&
                             ana_intersect<ANY>(((GAna *)anaArr)[__float_as_uint(q0.y)], o, d, mint, bt, at, alx, aly)) {
+#ifdef MTSG_ANYHIT_XC_SLOT   // diagnostic build: which test accepted the shadow ray
+                            if (ANY) { bestSlot = i | 0x80000000u; bu = at; bv = alx; bt = aly; }
+#endif
                             if (ANY) return true;
                             const uint32_t prim = __float_as_uint(q2.z);
                             if (!found || at < bt || prim > bestPrim) {
@@ -299,6 +302,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 const float u = hv * b_nu + hu * b_nv;
                 const float v = hu * c_nu + hv * c_nv;
                 if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+#ifdef MTSG_ANYHIT_XC_SLOT
+                    if (ANY) { bestSlot = i; bu = t; bv = u; bt = v; }
+#endif
                     if (ANY) return true;
                     const uint32_t prim = __float_as_uint(q2.z);
                     // ties (t == bt): the larger primitive index wins
@@ -394,6 +400,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                         float at, alx, aly;
                         if (k == MTSG_K_ANALYTIC &&
                             ana_intersect<ANY>(((GAna *)anaArr)[__float_as_uint(q0.y)], o, d, mint, bt, at, alx, aly)) {
+#ifdef MTSG_ANYHIT_XC_SLOT   // diagnostic build: which test accepted the shadow ray
+                            if (ANY) { bestSlot = i | 0x80000000u; bu = at; bv = alx; bt = aly; }
+#endif
                             if (ANY) return true;
                             const uint32_t prim = __float_as_uint(q2.z);
                             if (!found || at < bt || prim > bestPrim) {
@@ -413,6 +422,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 const float u = hv * b_nu + hu * b_nv;
                 const float v = hu * c_nu + hv * c_nv;
                 if (u >= 0 && v >= 0 && u + v <= 1.0f) {
+#ifdef MTSG_ANYHIT_XC_SLOT
+                    if (ANY) { bestSlot = i; bu = t; bv = u; bt = v; }
+#endif
                     if (ANY) return true;
                     const uint32_t prim = __float_as_uint(q2.z);
                     // ties (t == bt): the larger primitive index wins
@@ -2428,14 +2440,31 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
 // samples of the analytic-shape scene; the same source is exact at -O1, as a
 // call, with the NaN-aware (closest-hit) form of the sphere predicate, and
 // inlined into path_kernel / trace_kernel (DESIGN.md 4 has the bisection)
+#ifdef MTSG_ANYHIT_INLINE   // diagnostic build: the round-1 inlined form (tools/diag_parity.py)
+#define SHADOW_ANY_CALL __device__ __forceinline__
+#else
+#define SHADOW_ANY_CALL __device__ __noinline__
+#endif
 template <bool ANA, typename NodeT, typename TriT>
-__device__ __noinline__ bool shadow_any(NodeT *nodes, TriT *tris, f3 o, f3 d, float mint, float maxt,
+SHADOW_ANY_CALL bool shadow_any(NodeT *nodes, TriT *tris, f3 o, f3 d, float mint, float maxt,
                                         lds_stk_n *stkN, lds_stk_d *stkD, unsigned long long &cN,
                                         unsigned long long &cT, const MtsgAnalytic *ana) {
     uint32_t sl = 0;
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
     return traverse<true, false, ANA>(nodes, tris, o, d, mint, maxt, stkN, stkD, sl, a0, a1, a2, cN, cT, ana);
 }
+#ifdef MTSG_ANYHIT_CROSSCHECK   // diagnostic build: the inlined any-hit query beside the call, disagreements printed
+template <bool ANA, typename NodeT, typename TriT>
+__device__ __forceinline__ bool shadow_any_inl(NodeT *nodes, TriT *tris, f3 o, f3 d, float mint, float maxt,
+                                               lds_stk_n *stkN, lds_stk_d *stkD, unsigned long long &cN,
+                                               unsigned long long &cT, const MtsgAnalytic *ana, uint32_t &sl,
+                                               float &a0, float &a1, float &a2) {
+    sl = 0xffffffffu;
+    a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    return traverse<true, false, ANA>(nodes, tris, o, d, mint, maxt, stkN, stkD, sl, a0, a1, a2, cN, cT, ana);
+}
+__device__ unsigned int g_anyhit_xc;
+#endif
 template <bool SCENE_LDS, int FEAT>
 __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLaunch L) {
     constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
@@ -2541,6 +2570,30 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
             uint32_t sl; float a0, a1, a2;
             return scan_tris<true, false>(L, o, d, mint, maxt, sl, a0, a1, a2, cT);
         }
+#ifdef MTSG_ANYHIT_CROSSCHECK
+        {
+            uint32_t xs;
+            float x0, x1, x2;
+            const bool ri = SCENE_LDS ? shadow_any_inl<ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, cN, cT,
+                                                            S.analytic, xs, x0, x1, x2)
+                                      : shadow_any_inl<ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt,
+                                                            stkN, stkD, cN, cT, S.analytic, xs, x0, x1, x2);
+            const bool rc = SCENE_LDS ? shadow_any<ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, cN, cT,
+                                                        S.analytic)
+                                      : shadow_any<ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt,
+                                                        stkN, stkD, cN, cT, S.analytic);
+            if (ri != rc) {
+                const unsigned int k = atomicAdd(&g_anyhit_xc, 1u);
+                if (k < 48)
+                    printf("XC %u inl %d call %d o %08x %08x %08x d %08x %08x %08x dist %08x mint %08x maxt %08x "
+                           "lane %u slot %08x a %.9g %.9g %.9g\n", k, (int)ri, (int)rc, __float_as_uint(o.x),
+                           __float_as_uint(o.y), __float_as_uint(o.z), __float_as_uint(d.x), __float_as_uint(d.y),
+                           __float_as_uint(d.z), __float_as_uint(dist), __float_as_uint(mint), __float_as_uint(maxt),
+                           threadIdx.x, xs, x0, x1, x2);
+            }
+            return rc;
+        }
+#endif
         if (SCENE_LDS) return shadow_any<ANA>(ldsNodes, ldsTris, o, d, mint, maxt, stkN, stkD, cN, cT, S.analytic);
         return shadow_any<ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, o, d, mint, maxt, stkN, stkD, cN, cT,
                                S.analytic);
@@ -2822,16 +2875,16 @@ static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t s
     if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {   // large scenes only (spec_variant)
         if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
         else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
-        return;
-    }
-    if (L.scene_lds) {
-        if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {   // no calls: room for 4 waves (capi.cpp)
-            if (L.waves == 4) { launch_path_w<true, FEAT, 4>(L, grid, instr, stream); return; }
+    } else {
+        if (L.scene_lds) {
+            if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {   // no calls: room for 4 waves (capi.cpp)
+                if (L.waves == 4) { launch_path_w<true, FEAT, 4>(L, grid, instr, stream); return; }
+            }
+            launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
         }
-        launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
+        else if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
+        else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
     }
-    else if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
-    else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
 }
 
 
@@ -3029,15 +3082,16 @@ static int occupancy_e(const MtsgLaunch &L, int *bpc) {
     if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {
         if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
         return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
-    }
-    if (L.scene_lds) {
-        if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {
-            if (L.waves == 4) return occupancy_w<true, FEAT, 4>(L, bpc);
+    } else {
+        if (L.scene_lds) {
+            if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {
+                if (L.waves == 4) return occupancy_w<true, FEAT, 4>(L, bpc);
+            }
+            return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
         }
-        return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
+        if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
+        return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
     }
-    if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
-    return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
 }
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
     switch (spec_variant(L)) {
