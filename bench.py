@@ -204,8 +204,8 @@ def cgroup_cpus():
 def cpu_baseline(scene, integ, threads):
     """The CPU restatement (oracle, OpenMP, glibc transcendentals as the
     reference) on a bounded sample of the same workload: the full frame at a
-    reduced spp (the first spp Sobol samples of every pixel, sized by a pilot
-    pass to about 25 s of CPU work).  Threads: all
+    reduced spp (the first spp Sobol samples of every pixel, sized by two
+    pilot passes to about 20 s of CPU work).  Threads: all
     cores this job may use -- OMP_NUM_THREADS when the host sets it (the GPU
     boxes give a job a 16-CPU share of a larger machine), else the affinity
     mask; never more than the cgroup's CPU quota, which the line records."""
@@ -219,16 +219,21 @@ def cpu_baseline(scene, integ, threads):
         if quota:
             threads = max(1, min(threads, int(quota)))
     it = copy.copy(integ)
-    # size the sample to ~25 s of CPU work: a pilot pass (1/32 of the rows at
-    # 8 spp) measures this config's per-sample cost, then the full frame runs
-    # at the spp that fits (1..256, a power of two)
-    it.sampleCount = 8
-    t0 = time.perf_counter()
-    _, _, pst = ob.render(scene, it, libm_mode=0, threads=threads, row=(1, 32, 0))
-    rate = pst['samples'] / max(1e-6, time.perf_counter() - t0)
-    fit = 25.0 * rate / (scene.sensor.width * scene.sensor.height)
+    # size the sample to ~20 s of CPU work: two pilot passes (1/8 of the rows
+    # at 4 and 12 spp) give this config's marginal per-sample cost without the
+    # per-render setup, then the full frame runs at the power-of-two spp
+    # (1..256) nearest, in ratio, to the spp that fits
+    def pilot(spp):
+        it.sampleCount = spp
+        t0 = time.perf_counter()
+        _, _, pst = ob.render(scene, it, libm_mode=0, threads=threads, row=(1, 8, 0))
+        return pst['samples'], time.perf_counter() - t0
+    s1, t1 = pilot(4)
+    s2, t2 = pilot(12)
+    rate = (s2 - s1) / max(1e-6, t2 - t1) if t2 > t1 else s2 / max(1e-6, t2)
+    fit = 20.0 * rate / (scene.sensor.width * scene.sensor.height)
     spp = 1
-    while spp * 2 <= min(integ.sampleCount, 256) and spp * 2 <= fit:
+    while spp * 2 <= min(integ.sampleCount, 256) and spp * 2 <= fit * 1.41421356:
         spp *= 2
     it.sampleCount = spp
     t0 = time.perf_counter()

@@ -81,7 +81,7 @@ struct mtsgpu_ctx {
     MtsgDeviceScene dscene;
     DevBuf scan_tris;   // k-grouped TriAccel records of scan-sized scenes
     uint32_t scan_n[3] = {0, 0, 0};
-    DevBuf nodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
+    DevBuf nodes, hnodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
@@ -196,7 +196,8 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     HostScene &H = ctx->host;
     hipStream_t s = ctx->stream;
-    if ((e = upload(ctx->nodes, H.nodes, s)) != hipSuccess || (e = upload(ctx->tris, H.tris, s)) != hipSuccess ||
+    if ((e = upload(ctx->nodes, H.nodes, s)) != hipSuccess || (e = upload(ctx->hnodes, H.hnodes, s)) != hipSuccess ||
+        (e = upload(ctx->tris, H.tris, s)) != hipSuccess ||
         (e = upload(ctx->prim_vtx, H.prim_vtx, s)) != hipSuccess || (e = upload(ctx->dpdu, H.dpdu, s)) != hipSuccess ||
         (e = upload(ctx->positions, H.positions, s)) != hipSuccess || (e = upload(ctx->normals, H.normals, s)) != hipSuccess ||
         (e = upload(ctx->shapes, H.shapes, s)) != hipSuccess || (e = upload(ctx->bsdfs, H.bsdfs, s)) != hipSuccess ||
@@ -245,6 +246,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     MtsgDeviceScene &D = ctx->dscene;
     std::memset(&D, 0, sizeof D);
     D.nodes = (const MtsgNode *)ctx->nodes.p;
+    D.hnodes = (const MtsgHNode *)ctx->hnodes.p;
     D.tris = (const MtsgTri *)ctx->tris.p;
     D.prim_vtx = (const uint32_t *)ctx->prim_vtx.p;
     D.dpdu = (const float *)ctx->dpdu.p;
@@ -600,7 +602,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             rc |= b.type == MTSGPU_BSDF_ROUGHCONDUCTOR;
             rd |= b.type == MTSGPU_BSDF_ROUGHDIELECTRIC;
         }
-        L.bset = std::getenv("MTSGPU_NO_BSDF_SETS") ? 0u
+        // the set variants traverse half-float node boxes (layout.h MtsgHNode): a
+        // scene beyond half range would get infinite (still exact, but useless) boxes
+        float extent = 0.0f;
+        for (int a = 0; a < 3; ++a) extent = std::max(extent, std::max(std::fabs(H.aabb_min[a]), std::fabs(H.aabb_max[a])));
+        L.bset = (std::getenv("MTSGPU_NO_BSDF_SETS") || !(extent < 32768.0f)) ? 0u
                  : (ggx ? (uint32_t)MTSG_FEAT_GGX : 0u) | (rc ? 0u : (uint32_t)MTSG_FEAT_NORC) |
                        (rd ? 0u : (uint32_t)MTSG_FEAT_NORD);
     }
@@ -863,7 +869,7 @@ const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() :
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->hnodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,

@@ -34,6 +34,16 @@ struct MtsgNode {            // 64 B (Aila-Laine layout)
     int32_t c0, c1, pad0, pad1;
 };
 
+// The same BVH2 node with its child boxes as IEEE half floats rounded outward
+// (lo toward -inf, hi toward +inf), so a box never shrinks and every exact
+// triangle / shape test, hence every hit, is unchanged; 32 B, two 16 B loads.
+// box[k] packs two halves (low half first) in MtsgNode's order:
+// {c0lox c0hix}{c0loy c0hiy}{c1lox c1hix}{c1loy c1hiy}{c0loz c0hiz}{c1loz c1hiz}
+struct MtsgHNode {
+    uint32_t box[6];
+    int32_t c0, c1;
+};
+
 struct MtsgTri {             // 48 B
     uint32_t k;
     float n_u, n_v, n_d;
@@ -170,6 +180,7 @@ struct MtsgEnv {
 
 struct MtsgDeviceScene {
     const MtsgNode *nodes;
+    const MtsgHNode *hnodes;    // the same nodes, half-float boxes (large scenes)
     const MtsgTri *tris;
     const uint32_t *prim_vtx;   // 4 per primitive: v0, v1, v2, shape
     const float *dpdu;          // 3 per primitive

@@ -49,6 +49,36 @@ typedef __attribute__((address_space(3))) const vf4 lds_f4;
 typedef __attribute__((address_space(1))) const vf4 glb_f4;
 typedef __attribute__((address_space(3))) const vi4 lds_i4;
 typedef __attribute__((address_space(1))) const vi4 glb_i4;
+typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const vu4 glb_u4;
+typedef __attribute__((address_space(1))) const MtsgHNode glb_hnode;
+
+// one BVH2 node's two child boxes and child references: the 64 B MtsgNode
+// (LDS or HBM) in four 16 B loads, or the 32 B MtsgHNode in two, its half
+// bounds widened exactly to float (the conversions fold into the slab FMAs)
+__device__ __forceinline__ float half_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu)); }
+__device__ __forceinline__ float half_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)); }
+template <typename NodeT>
+__device__ __forceinline__ void load_node(NodeT *n, vf4 &a, vf4 &b, vf4 &c, int &c0, int &c1) {
+    if constexpr (std::is_same<NodeT, glb_hnode>::value) {
+        const vu4 p = *reinterpret_cast<glb_u4 *>(&n->box[0]);
+        const vu4 q = *reinterpret_cast<glb_u4 *>(&n->box[4]);
+        a = vf4{half_lo(p.x), half_hi(p.x), half_lo(p.y), half_hi(p.y)};
+        b = vf4{half_lo(p.z), half_hi(p.z), half_lo(p.w), half_hi(p.w)};
+        c = vf4{half_lo(q.x), half_hi(q.x), half_lo(q.y), half_hi(q.y)};
+        c0 = (int)q.z;
+        c1 = (int)q.w;
+    } else {
+        typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
+        typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
+        a = *reinterpret_cast<F4 *>(&n->c0lox);
+        b = *reinterpret_cast<F4 *>(&n->c1lox);
+        c = *reinterpret_cast<F4 *>(&n->c0loz);
+        const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+        c0 = e.x;
+        c1 = e.y;
+    }
+}
 
 template <int NIB, typename T>
 __device__ __forceinline__ uint32_t sobol_bits(T *tab, uint64_t index) {
@@ -188,7 +218,6 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                                          float &bt, unsigned long long &nodes, unsigned long long &tests,
                                          const MtsgAnalytic *anaArr = nullptr, uint2 *ovf = nullptr) {
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
-    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_i4, glb_i4>::type I4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
     const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
     const float iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
@@ -215,11 +244,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         // inner nodes
         while ((uint32_t)node < (uint32_t)DONE) {
             if (STATS) nodes++;
-            NodeT *n = nodesArr + node;
-            const vf4 a = *reinterpret_cast<F4 *>(&n->c0lox);
-            const vf4 b = *reinterpret_cast<F4 *>(&n->c1lox);
-            const vf4 c = *reinterpret_cast<F4 *>(&n->c0loz);
-            const vi4 e = *reinterpret_cast<I4 *>(&n->c0);
+            vf4 a, b, c;
+            int ec0, ec1;
+            load_node(nodesArr + node, a, b, c, ec0, ec1);
             // slab tests; node boxes are conservatively inflated on the host
             const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
             const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
@@ -233,9 +260,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
             const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
             const bool h0 = n0 <= f0, h1 = n1 <= f1;
             if (h0 && h1) {
-                int nearC = e.x, farC = e.y;
+                int nearC = ec0, farC = ec1;
                 float farT = n1;
-                if (n1 < n0) { nearC = e.y; farC = e.x; farT = n0; }
+                if (n1 < n0) { nearC = ec1; farC = ec0; farT = n0; }
                 if (LDSK == 0 || sp < LDSK) {
                     stkN[sp * BLOCK] = farC;
                     stkD[sp * BLOCK] = dist_down16(farT);
@@ -245,9 +272,9 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 ++sp;
                 node = nearC;
             } else if (h0) {
-                node = e.x;
+                node = ec0;
             } else if (h1) {
-                node = e.y;
+                node = ec1;
             } else {
                 node = pop();
             }
@@ -1736,6 +1763,11 @@ template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
     constexpr bool STATS = INSTR;
     constexpr bool ANA = (FEAT & MTSG_FEAT_ANA) != 0;
+#ifndef MTSG_FULL_NODES   // the BSDF-set variants (large scenes) traverse the 32 B half-box nodes
+    constexpr bool HNODES = (FEAT & (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)) != 0;
+#else
+    constexpr bool HNODES = false;
+#endif
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
     const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
@@ -1847,6 +1879,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 if (SCENE_LDS)
                     occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
                                                           sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
+                else if constexpr (HNODES)
+                    occluded = traverse<true, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
+                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
+                                                          S.analytic);
                 else
                     occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
                                                           mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
@@ -1867,6 +1903,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
                                                       hu, hv, ht, c.nodes, c.tests, S.analytic);
+                else if constexpr (HNODES)
+                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
+                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
+                                                      S.analytic);
                 else
                     hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,

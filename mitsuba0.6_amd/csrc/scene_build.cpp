@@ -739,6 +739,29 @@ float half_to_float(uint16_t h) {
     return f;
 }
 
+// x as a half rounded toward +inf (up) or -inf (down): BVH box bounds that never shrink
+static uint16_t half_outward(float x, bool up) {
+    const uint16_t h = float_to_half(x);
+    const float y = half_to_float(h);
+    if (up ? !(y < x) : !(y > x)) return h;
+    const bool neg = (h & 0x8000u) != 0;
+    if (up) return neg ? (uint16_t)(h - 1) : (uint16_t)(h + 1);   // toward +inf (0x7bff + 1 = +inf)
+    if ((h & 0x7fffu) == 0) return 0x8001u;                        // +0 -> the negative subnormal
+    return neg ? (uint16_t)(h + 1) : (uint16_t)(h - 1);
+}
+
+// MtsgNode -> MtsgHNode (layout.h): same children, half boxes rounded outward
+static MtsgHNode half_node(const MtsgNode &n) {
+    const float lo[6] = {n.c0lox, n.c0loy, n.c1lox, n.c1loy, n.c0loz, n.c1loz};
+    const float hi[6] = {n.c0hix, n.c0hiy, n.c1hix, n.c1hiy, n.c0hiz, n.c1hiz};
+    MtsgHNode h;
+    for (int k = 0; k < 6; ++k)
+        h.box[k] = (uint32_t)half_outward(lo[k], false) | ((uint32_t)half_outward(hi[k], true) << 16);
+    h.c0 = n.c0;
+    h.c1 = n.c1;
+    return h;
+}
+
 // LanczosSincFilter::eval with lobes = 2 (rfilters/lanczos.cpp:43-55)
 float lanczos2(float x) {
     x = std::fabs(x);
@@ -1437,6 +1460,8 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     }
     S.bvh_depth = B.maxDepth;
     if (B.maxDepth + 1 >= 32) { err = "BVH too deep for the traversal stack"; return MTSGPU_EINVAL; }
+    S.hnodes.resize(S.nodes.size());
+    for (size_t i = 0; i < S.nodes.size(); ++i) S.hnodes[i] = half_node(S.nodes[i]);
     // triangles in leaf order
     S.tris.resize(prims);
     for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];

@@ -26,6 +26,7 @@ int mtsg_rtrans_check(const MtsgRTrans &t, float eta, float alphaMin, float alph
 
 struct HostScene {
     std::vector<MtsgNode> nodes;
+    std::vector<MtsgHNode> hnodes;   // the same BVH, half-float boxes
     std::vector<MtsgTri> tris;
     std::vector<uint32_t> prim_vtx;
     std::vector<float> dpdu, positions, normals;

@@ -43,10 +43,15 @@ for name, path in variants:
     with_env(name, lambda: c.render(it, row=(8, stride, 0)))   # warm up
     ctxs[name] = c
 res = {n: [] for n, _ in variants}
+films = {}
 for r in range(rounds):
     for name, _ in variants:
-        _, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0)))
+        film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0)))
+        films.setdefault(name, film)
         res[name].append(st['samples'] / st['kernel_ms'] / 1e3)
+first = variants[0][0]
 for name, v in res.items():
     v = sorted(v)
-    print('%-14s median %8.1f  min %8.1f  max %8.1f Msamples/s' % (name, v[len(v) // 2], v[0], v[-1]))
+    same = films[name].tobytes() == films[first].tobytes()
+    print('%-14s median %8.1f  min %8.1f  max %8.1f Msamples/s  film bit-identical to %s: %s' % (
+        name, v[len(v) // 2], v[0], v[-1], first, same))
