@@ -81,7 +81,7 @@ struct mtsgpu_ctx {
     MtsgDeviceScene dscene;
     DevBuf scan_tris;   // k-grouped TriAccel records of scan-sized scenes
     uint32_t scan_n[3] = {0, 0, 0};
-    DevBuf nodes, hnodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
+    DevBuf nodes, hnodes, qnodes, trav_ovf, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
@@ -197,6 +197,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     HostScene &H = ctx->host;
     hipStream_t s = ctx->stream;
     if ((e = upload(ctx->nodes, H.nodes, s)) != hipSuccess || (e = upload(ctx->hnodes, H.hnodes, s)) != hipSuccess ||
+        (e = upload(ctx->qnodes, H.qnodes, s)) != hipSuccess ||
         (e = upload(ctx->tris, H.tris, s)) != hipSuccess ||
         (e = upload(ctx->prim_vtx, H.prim_vtx, s)) != hipSuccess || (e = upload(ctx->dpdu, H.dpdu, s)) != hipSuccess ||
         (e = upload(ctx->positions, H.positions, s)) != hipSuccess || (e = upload(ctx->normals, H.normals, s)) != hipSuccess ||
@@ -247,6 +248,7 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     std::memset(&D, 0, sizeof D);
     D.nodes = (const MtsgNode *)ctx->nodes.p;
     D.hnodes = (const MtsgHNode *)ctx->hnodes.p;
+    D.qnodes = (const MtsgQNode *)ctx->qnodes.p;
     D.tris = (const MtsgTri *)ctx->tris.p;
     D.prim_vtx = (const uint32_t *)ctx->prim_vtx.p;
     D.dpdu = (const float *)ctx->dpdu.p;
@@ -625,6 +627,17 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         if (nl > 1) { L.lum_dim = L.array_end; L.array_end += 2; }
         if (nb > 1) { L.bsdf_dim = L.array_end; L.array_end += 2; }
     }
+    L.trav_ovf = nullptr;
+    L.ovf_depth = 0;
+#ifdef MTSG_BVH4
+    // the BSDF-set variants traverse the 4-wide BVH (<= 3 pushes per level):
+    // MTSG_Q_LDS_STACK entries per lane in LDS, deeper ones in HBM (trav_ovf)
+    if (L.bset && !L.scene_lds) {
+        L.stack_depth = std::max<uint32_t>(L.stack_depth, MTSG_Q_LDS_STACK);
+        const uint32_t need = 3 * H.qnode_depth + 1;
+        L.ovf_depth = need > MTSG_Q_LDS_STACK ? need - MTSG_Q_LDS_STACK : 0;
+    }
+#endif
     L.waves = 3;
     if (!L.scene_lds) {
         const size_t perBlock = (160u << 10) / 4;
@@ -679,6 +692,12 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     int bpc = 0;
     mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
+    if (L.ovf_depth) {
+        const size_t lanes = (size_t)ctx->num_cus * bpc * BLOCK_THREADS;
+        if ((e = ctx->trav_ovf.ensure(lanes * L.ovf_depth * 8)) != hipSuccess)
+            return hip_fail(ctx, e, "traversal overflow stack");
+        L.trav_ovf = (uint32_t *)ctx->trav_ovf.p;
+    }
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
     if (replay) {
         // IndependentSampler's Random() = seed(5489); RenderJob clones it per worker in
@@ -869,7 +888,7 @@ const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() :
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->hnodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->hnodes, &ctx->qnodes, &ctx->trav_ovf, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,

@@ -44,6 +44,17 @@ struct MtsgHNode {
     int32_t c0, c1;
 };
 
+// The BVH2 collapsed to a 4-wide BVH (each node's children are its BVH2
+// node's grandchildren where those are inner nodes), child boxes as halves
+// rounded outward like MtsgHNode: 64 B, four 16 B loads, half the node levels.
+// box[3j .. 3j+2] = child j's {lox hix}{loy hiy}{loz hiz}; child[j]: a node
+// index (> 0), a leaf reference (< 0, mtsg_leaf_ref) or 0 (no child)
+#define MTSG_Q_LDS_STACK 24   // 4-wide BVH: traversal stack entries per lane kept in LDS
+struct MtsgQNode {
+    uint32_t box[12];
+    int32_t child[4];
+};
+
 struct MtsgTri {             // 48 B
     uint32_t k;
     float n_u, n_v, n_d;
@@ -181,6 +192,7 @@ struct MtsgEnv {
 struct MtsgDeviceScene {
     const MtsgNode *nodes;
     const MtsgHNode *hnodes;    // the same nodes, half-float boxes (large scenes)
+    const MtsgQNode *qnodes;    // the same BVH collapsed to 4-wide nodes (large scenes)
     const MtsgTri *tris;
     const uint32_t *prim_vtx;   // 4 per primitive: v0, v1, v2, shape
     const float *dpdu;          // 3 per primitive
@@ -259,6 +271,8 @@ struct MtsgLaunch {
     uint32_t lds_dims;                // dims [0, lds_dims) staged in LDS
     uint32_t nibbles;                 // 8 (index < 2^32) or MTSG_NIBBLES
     uint32_t stack_depth;             // LDS traversal stack entries per lane
+    uint32_t *trav_ovf;               // 4-wide BVH: per-lane stack entries beyond the LDS ones ({node, dist} pairs)
+    uint32_t ovf_depth;               // entries per lane in trav_ovf
     uint32_t num_nodes;               // BVH2 inner nodes
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)

@@ -52,6 +52,7 @@ typedef __attribute__((address_space(1))) const vi4 glb_i4;
 typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const vu4 glb_u4;
 typedef __attribute__((address_space(1))) const MtsgHNode glb_hnode;
+typedef __attribute__((address_space(1))) const MtsgQNode glb_qnode;
 
 // one BVH2 node's two child boxes and child references: the 64 B MtsgNode
 // (LDS or HBM) in four 16 B loads, or the 32 B MtsgHNode in two, its half
@@ -244,6 +245,50 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         // inner nodes
         while ((uint32_t)node < (uint32_t)DONE) {
             if (STATS) nodes++;
+            if constexpr (std::is_same<NodeT, glb_qnode>::value) {
+                // 4-wide node: slab-test the four child boxes, visit the nearest
+                // hit child next and push the other hit ones farthest first
+                NodeT *q = nodesArr + node;
+                const vu4 B0 = *reinterpret_cast<glb_u4 *>(&q->box[0]);
+                const vu4 B1 = *reinterpret_cast<glb_u4 *>(&q->box[4]);
+                const vu4 B2 = *reinterpret_cast<glb_u4 *>(&q->box[8]);
+                const vi4 C = *reinterpret_cast<glb_i4 *>(&q->child[0]);
+                auto slab = [&](uint32_t wx, uint32_t wy, uint32_t wz, int ch) -> float {
+                    const float t0x = __builtin_fmaf(half_lo(wx), ix, -ox), t1x = __builtin_fmaf(half_hi(wx), ix, -ox);
+                    const float t0y = __builtin_fmaf(half_lo(wy), iy, -oy), t1y = __builtin_fmaf(half_hi(wy), iy, -oy);
+                    const float t0z = __builtin_fmaf(half_lo(wz), iz, -oz), t1z = __builtin_fmaf(half_hi(wz), iz, -oz);
+                    const float nn = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
+                    const float ff = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
+                    return (ch != 0 && nn <= ff) ? nn : INFINITY;
+                };
+                float d0 = slab(B0.x, B0.y, B0.z, C.x), d1 = slab(B0.w, B1.x, B1.y, C.y);
+                float d2 = slab(B1.z, B1.w, B2.x, C.z), d3 = slab(B2.y, B2.z, B2.w, C.w);
+                int k0 = C.x, k1 = C.y, k2 = C.z, k3 = C.w;
+                auto cx = [](float &da, int &ka, float &db, int &kb) {
+                    const bool sw = db < da;
+                    const float td = sw ? db : da, tk_d = sw ? da : db;
+                    const int tk = sw ? kb : ka, tk2 = sw ? ka : kb;
+                    da = td; db = tk_d; ka = tk; kb = tk2;
+                };
+#ifdef MTSG_BVH4_NEAREST   // only the nearest hit child first; the others pushed in slot order
+                cx(d0, k0, d1, k1); cx(d0, k0, d2, k2); cx(d0, k0, d3, k3);
+#else
+                cx(d0, k0, d1, k1); cx(d2, k2, d3, k3); cx(d0, k0, d2, k2); cx(d1, k1, d3, k3); cx(d1, k1, d2, k2);
+#endif
+                auto push = [&](int ref, float t) {
+                    if (LDSK == 0 || sp < LDSK) {
+                        stkN[sp * BLOCK] = ref;
+                        stkD[sp * BLOCK] = dist_down16(t);
+                    } else {
+                        ovf[sp - LDSK] = make_uint2((uint32_t)ref, dist_down16(t));
+                    }
+                    ++sp;
+                };
+                if (d3 < INFINITY) push(k3, d3);
+                if (d2 < INFINITY) push(k2, d2);
+                if (d1 < INFINITY) push(k1, d1);
+                node = d0 < INFINITY ? k0 : pop();
+            } else {
             vf4 a, b, c;
             int ec0, ec1;
             load_node(nodesArr + node, a, b, c, ec0, ec1);
@@ -278,6 +323,7 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
             } else {
                 node = pop();
             }
+            }
             // park the first leaf reached and keep descending
             if (node < 0 && leaf == 0) {
                 leaf = node;
@@ -288,19 +334,47 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         // leaves
         while (leaf < 0) {
             const uint32_t ref = (uint32_t)(~leaf);
-            const uint32_t first = ref >> 4, count = ref & 15u;
-            for (uint32_t i = first; i < first + count; ++i) {
+            const uint32_t first = ref >> 4, count = ref & 15u, end = first + count;
+#ifdef MTSG_LEAF_PREFETCH
+            // the next record is loaded while the current one is tested
+            vf4 p0 = {}, p1 = {}, p2 = {};
+            if (count) {
+                TriT *tr = trisArr + first;
+                p0 = *reinterpret_cast<F4 *>(&tr->k);
+                p1 = *reinterpret_cast<F4 *>(&tr->a_u);
+                p2 = *reinterpret_cast<F4 *>(&tr->c_nu);
+            }
+#endif
+            for (uint32_t i = first; i < end; ++i) {
                 if (STATS) tests++;
+#ifdef MTSG_LEAF_PREFETCH
+                const vf4 q0 = p0, q1 = p1, q2 = p2;
+                {
+                    TriT *tn = trisArr + (i + 1 < end ? i + 1 : i);
+                    p0 = *reinterpret_cast<F4 *>(&tn->k);
+                    p1 = *reinterpret_cast<F4 *>(&tn->a_u);
+                    p2 = *reinterpret_cast<F4 *>(&tn->c_nu);
+                }
+#else
                 TriT *tr = trisArr + i;
                 const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
                 const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
                 const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
+#endif
                 const uint32_t k = __float_as_uint(q0.x);
                 // TriAccel::rayIntersect (triaccel.h:92-160)
                 float o_u, o_v, o_k, d_u, d_v, d_k;
+#ifdef MTSG_LEAF_SELECT
+                if (!ANA || k < 3) {   // triangle: the projection axes as selects, no branches
+                    const bool k0 = k == 0, k1 = k == 1;
+                    o_u = k0 ? o.y : k1 ? o.z : o.x; o_v = k0 ? o.z : k1 ? o.x : o.y; o_k = k0 ? o.x : k1 ? o.y : o.z;
+                    d_u = k0 ? d.y : k1 ? d.z : d.x; d_v = k0 ? d.z : k1 ? d.x : d.y; d_k = k0 ? d.x : k1 ? d.y : d.z;
+                }
+#else
                 if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
                 else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
                 else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
+#endif
                 else {
                     if constexpr (ANA) {
                         // analytic primitive (skdtree.h:280-290: Shape::rayIntersect on [mint, maxt])
@@ -1768,6 +1842,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 #else
     constexpr bool HNODES = false;
 #endif
+#ifdef MTSG_BVH4   // ... or the 4-wide BVH (layout.h MtsgQNode)
+    constexpr bool QNODES = HNODES;
+    uint2 *qovf = (uint2 *)L.trav_ovf + (size_t)(blockIdx.x * BLOCK + threadIdx.x) * L.ovf_depth;
+#else
+    constexpr bool QNODES = false;
+    uint2 *qovf = nullptr;
+#endif
     extern __shared__ uint32_t lds[];
     const MtsgDeviceScene &S = L.scene;
     const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
@@ -1879,6 +1960,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 if (SCENE_LDS)
                     occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
                                                           sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
+                else if constexpr (QNODES)
+                    occluded = traverse<true, STATS, ANA, MTSG_Q_LDS_STACK>((glb_qnode *)S.qnodes, (glb_tri *)S.tris,
+                                                                            st.P.its.p, st.sd, mint, maxt, stkN, stkD,
+                                                                            sl, a0, a1, a2, c.nodes, c.tests,
+                                                                            S.analytic, qovf);
                 else if constexpr (HNODES)
                     occluded = traverse<true, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
                                                           mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
@@ -1903,6 +1989,10 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
                 if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
                                                       hu, hv, ht, c.nodes, c.tests, S.analytic);
+                else if constexpr (QNODES)
+                    hit = traverse<false, STATS, ANA, MTSG_Q_LDS_STACK>((glb_qnode *)S.qnodes, (glb_tri *)S.tris,
+                                                                        st.ro, st.rd, mint, maxt, stkN, stkD, slot,
+                                                                        hu, hv, ht, c.nodes, c.tests, S.analytic, qovf);
                 else if constexpr (HNODES)
                     hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,

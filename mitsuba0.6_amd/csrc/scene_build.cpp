@@ -762,6 +762,53 @@ static MtsgHNode half_node(const MtsgNode &n) {
     return h;
 }
 
+// the BVH2 `n2` collapsed to 4-wide nodes (layout.h MtsgQNode), depth-first
+// with the root at 0: an inner BVH2 child is replaced by its two children
+struct QCollapse {
+    const std::vector<MtsgNode> &n2;
+    std::vector<MtsgQNode> &q;
+    uint32_t depth = 0;
+    int32_t emit(int32_t ref, uint32_t level) {
+        if (ref < 0) return ref;
+        depth = std::max(depth, level);
+        struct Kid { float lo[3], hi[3]; int32_t ref; } kids[4];
+        int nk = 0;
+        auto box = [](const MtsgNode &n, int c, Kid &k) {
+            if (c == 0) {
+                k.lo[0] = n.c0lox; k.hi[0] = n.c0hix; k.lo[1] = n.c0loy; k.hi[1] = n.c0hiy; k.lo[2] = n.c0loz; k.hi[2] = n.c0hiz;
+                k.ref = n.c0;
+            } else {
+                k.lo[0] = n.c1lox; k.hi[0] = n.c1hix; k.lo[1] = n.c1loy; k.hi[1] = n.c1hiy; k.lo[2] = n.c1loz; k.hi[2] = n.c1hiz;
+                k.ref = n.c1;
+            }
+        };
+        const MtsgNode &n = n2[ref];
+        for (int c = 0; c < 2; ++c) {
+            Kid k;
+            box(n, c, k);
+            if (k.ref >= 0) {
+                box(n2[k.ref], 0, kids[nk++]);
+                box(n2[k.ref], 1, kids[nk++]);
+            } else {
+                kids[nk++] = k;
+            }
+        }
+        const int32_t id = (int32_t)q.size();
+        q.push_back(MtsgQNode());
+        int32_t refs[4] = {0, 0, 0, 0};
+        for (int j = 0; j < nk; ++j) refs[j] = emit(kids[j].ref, level + 1);
+        MtsgQNode &out = q[id];
+        for (int j = 0; j < 4; ++j) {
+            for (int a = 0; a < 3; ++a)
+                out.box[3 * j + a] = j < nk ? (uint32_t)half_outward(kids[j].lo[a], false) |
+                                                  ((uint32_t)half_outward(kids[j].hi[a], true) << 16)
+                                            : 0u;
+            out.child[j] = refs[j];
+        }
+        return id;
+    }
+};
+
 // LanczosSincFilter::eval with lobes = 2 (rfilters/lanczos.cpp:43-55)
 float lanczos2(float x) {
     x = std::fabs(x);
@@ -1462,6 +1509,11 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     if (B.maxDepth + 1 >= 32) { err = "BVH too deep for the traversal stack"; return MTSGPU_EINVAL; }
     S.hnodes.resize(S.nodes.size());
     for (size_t i = 0; i < S.nodes.size(); ++i) S.hnodes[i] = half_node(S.nodes[i]);
+    S.qnodes.clear();
+    S.qnodes.reserve(S.nodes.size() / 2 + 2);
+    QCollapse qc{S.nodes, S.qnodes};
+    qc.emit(0, 1);
+    S.qnode_depth = qc.depth;
     // triangles in leaf order
     S.tris.resize(prims);
     for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];

@@ -27,6 +27,8 @@ int mtsg_rtrans_check(const MtsgRTrans &t, float eta, float alphaMin, float alph
 struct HostScene {
     std::vector<MtsgNode> nodes;
     std::vector<MtsgHNode> hnodes;   // the same BVH, half-float boxes
+    std::vector<MtsgQNode> qnodes;   // the same BVH collapsed to 4-wide nodes
+    uint32_t qnode_depth = 0;        // inner-node levels of qnodes
     std::vector<MtsgTri> tris;
     std::vector<uint32_t> prim_vtx;
     std::vector<float> dpdu, positions, normals;
