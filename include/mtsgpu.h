@@ -339,6 +339,16 @@ int mtsgpu_debug_kdtree(mtsgpu_ctx *ctx, uint32_t *nodes, size_t node_cap, uint3
 /* Host-only (no device needed): configure `scene` and build its kd-tree, as above. */
 int mtsgpu_kdtree_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *indices,
                        size_t index_cap, uint32_t *info8, char *msg, size_t cap);
+/* Host-only (no device needed): configure `scene` and export the BVH the
+ * kernels traverse: info4 = {BVH2 nodes, half-box nodes,
+ * 4-wide nodes, 4-wide inner-node levels}; `nodes` (MtsgNode, 16 words each),
+ * `hnodes` (MtsgHNode, 8 words: child boxes as IEEE halves rounded outward)
+ * and `qnodes` (MtsgQNode, 16 words: the BVH2 collapsed to 4-wide nodes) are
+ * copied when their capacities (in words) suffice.  Replaces no reference
+ * interface: it is the checker's view of ShapeKDTree's acceleration structure
+ * (src/librender/skdtree.cpp) as rebuilt here. */
+int mtsgpu_bvh_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *hnodes,
+                    size_t hnode_cap, uint32_t *qnodes, size_t qnode_cap, uint32_t *info4, char *msg, size_t cap);
 /* Diagnostics (tests): device arithmetic probe -- for each i, out[8i..8i+7] =
  * {a/b, sqrt|a|, sin a, cos a, acos(clamp a), atan2(a,b), exp(-|a|), a*b+a}
  * computed by the kernels' own routines; scene info = {nodes, prims, depth, CUs}. */

@@ -969,6 +969,27 @@ int mtsgpu_debug_kdtree(mtsgpu_ctx *ctx, uint32_t *nodes, size_t node_cap, uint3
     return MTSGPU_OK;
 }
 
+int mtsgpu_bvh_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *hnodes,
+                    size_t hnode_cap, uint32_t *qnodes, size_t qnode_cap, uint32_t *info4, char *msg, size_t cap) {
+    if (!scene || !info4) return MTSGPU_EINVAL;
+    HostScene H;
+    std::string err;
+    const int rc = mtsg_configure_scene(scene, H, err);
+    if (msg && cap) {
+        std::strncpy(msg, err.c_str(), cap - 1);
+        msg[cap - 1] = 0;
+    }
+    if (rc) return rc;
+    info4[0] = (uint32_t)H.nodes.size();
+    info4[1] = (uint32_t)H.hnodes.size();
+    info4[2] = (uint32_t)H.qnodes.size();
+    info4[3] = H.qnode_depth;
+    if (nodes && node_cap >= H.nodes.size() * 16) std::memcpy(nodes, H.nodes.data(), H.nodes.size() * 64);
+    if (hnodes && hnode_cap >= H.hnodes.size() * 8) std::memcpy(hnodes, H.hnodes.data(), H.hnodes.size() * 32);
+    if (qnodes && qnode_cap >= H.qnodes.size() * 16) std::memcpy(qnodes, H.qnodes.data(), H.qnodes.size() * 64);
+    return MTSGPU_OK;
+}
+
 int mtsgpu_kdtree_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node_cap, uint32_t *indices,
                        size_t index_cap, uint32_t *info8, char *msg, size_t cap) {
     if (!scene || !info8) return MTSGPU_EINVAL;

@@ -30,7 +30,8 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_debug_arith', 'mtsgpu_debug_scene_info', 'mtsgpu_debug_counters', 'mtsgpu_debug_sfmt', 'mtsgpu_develop', 'mtsgpu_develop_device', 'mtsgpu_check_scene',
            'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
-           'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm']
+           'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm',
+           'mtsgpu_bvh_host']
 
 _lib = None
 
@@ -74,6 +75,8 @@ def load_library(path=None):
     L.mtsgpu_debug_kdtree.argtypes = [C.c_void_p, P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_size_t, P(C.c_uint32)]
     L.mtsgpu_kdtree_host.argtypes = [P(abi.SceneDesc), P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_size_t,
                                      P(C.c_uint32), C.c_char_p, C.c_size_t]
+    L.mtsgpu_bvh_host.argtypes = [P(abi.SceneDesc), P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_size_t,
+                                  P(C.c_uint32), C.c_size_t, P(C.c_uint32), C.c_char_p, C.c_size_t]
     L.mtsgpu_group_create.argtypes = [P(C.c_int), C.c_int, P(C.c_void_p)]
     L.mtsgpu_group_size.argtypes = [C.c_void_p]
     L.mtsgpu_group_upload_scene.argtypes = [C.c_void_p, P(abi.SceneDesc)]
@@ -103,6 +106,28 @@ def check_scene(scene):
 
 
 KD_KEYS = ('nodes', 'indices', 'inner', 'leaves', 'nonempty_leaves', 'retracted', 'pruned', 'max_depth')
+
+
+def bvh_host(scene):
+    """The BVH the kernels traverse, built on the host without a device
+    (mtsgpu_bvh_host): (nodes (N, 16) uint32 MtsgNode words, hnodes (N, 8) MtsgHNode
+    words, qnodes (M, 16) MtsgQNode words, 4-wide inner-node levels)."""
+    L = load_library()
+    d = scene.desc()
+    info = (C.c_uint32 * 4)()
+    buf = C.create_string_buffer(512)
+    rc = L.mtsgpu_bvh_host(C.byref(d), None, 0, None, 0, None, 0, info, buf, 512)
+    if rc != 0:
+        raise MtsgpuError(rc, buf.value.decode())
+    n = np.zeros((info[0], 16), np.uint32)
+    h = np.zeros((info[1], 8), np.uint32)
+    q = np.zeros((info[2], 16), np.uint32)
+    up = C.POINTER(C.c_uint32)
+    rc = L.mtsgpu_bvh_host(C.byref(d), n.ctypes.data_as(up), n.size, h.ctypes.data_as(up), h.size,
+                           q.ctypes.data_as(up), q.size, info, buf, 512)
+    if rc != 0:
+        raise MtsgpuError(rc, buf.value.decode())
+    return n, h, q, int(info[3])
 
 
 def kdtree_host(scene):
