@@ -519,7 +519,12 @@ __device__ __forceinline__ bool cubic_weights(float p, uint32_t size, KnotW &k) 
     return true;
 }
 
-__device__ __noinline__ float cubic2d(float px, float py, glb_f32 *values, uint32_t sx, uint32_t sy) {
+#ifdef MTSG_CUBIC2D_INLINE   // A/B: the 2D spline lookup inlined into roughplastic's callers
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+float cubic2d(float px, float py, glb_f32 *values, uint32_t sx, uint32_t sy) {
     KnotW kx, ky;
     if (!cubic_weights(px, sx, kx)) return 0.0f;
     if (!cubic_weights(py, sy, ky)) return 0.0f;
