@@ -872,26 +872,39 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
 // and ShapeKDTree::intersect's TriAccel test (skdtree.h:248-338), which keeps
 // a hit at t == maxt: among exactly tied triangles the last one tested wins,
 // as in the reference.  TriAccel records are in global primitive order.
-// Correctness path (mtsgpu_trace_rays with MTSGPU_TRACE_KDTREE): the stack
-// lives in scratch.
+// The reference's stack entry holds the entry/exit point p = ray(t) with
+// p[axis] = split; here an entry keeps (node, t, split, prev | axis << 8),
+// 16 B instead of 24, and p[a] is re-formed as split (a == axis) or o[a] +
+// d[a] * t — the same rounded product and sum the reference stores, so every
+// comparison sees the same floats.  The entry and exit points the descent
+// compares against are held in registers (only a push or a pop changes them),
+// so a descent step reads no stack memory; the stack itself lives in scratch.
 template <bool ANY>
 __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
                             const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
                             float &bu, float &bv, uint32_t &bprim) {
-    struct Ent { uint32_t node; float t; uint32_t prev; float p[3]; };
-    constexpr uint32_t NONE = 0xffffffffu;
+    struct Ent { uint32_t node; float t; float split; uint32_t prev_axis; };
+    constexpr uint32_t NONE = 0xffffffffu, NOAXIS = 3u;
     Ent stack[48];
     uint32_t mbox[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) mbox[i] = 0xffffffffu;
-    const float oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
     const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
+    // p[a] of an entry (t, split, eaxis): the stored point of sahkdtree3.h:239-244
+    auto pt = [&](float t, float split, uint32_t eaxis, int a) -> float {
+        if ((uint32_t)a == eaxis) return split;
+        const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
+        const float da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
+        return oa + da * t;
+    };
     uint32_t enPt = 0, exPt = 1;
-    stack[0].t = mint;
-    for (int k = 0; k < 3; ++k) stack[0].p[k] = oa[k] + da[k] * mint;   // ray(mint)
-    stack[1].t = maxt;
-    for (int k = 0; k < 3; ++k) stack[1].p[k] = oa[k] + da[k] * maxt;
+    stack[0].t = mint;                                    // ray(mint)
+    stack[0].prev_axis = NOAXIS << 8;
+    stack[1].t = maxt;                                    // ray(maxt)
+    stack[1].prev_axis = NOAXIS << 8;
     stack[1].node = NONE;
+    float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;
+    uint32_t en_axis = NOAXIS, ex_axis = NOAXIS;
     bool found = false;
     uint32_t node = 0;
     while (node != NONE) {
@@ -900,31 +913,47 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             const float split = __uint_as_float(n.y);
             const int axis = (int)(n.x & 3u);
             const uint32_t left = node + ((n.x & ~(3u | 0x40000000u)) >> 2);
+            const float enP = pt(en_t, en_split, en_axis, axis);
+            const float exP = pt(ex_t, ex_split, ex_axis, axis);
             uint32_t farChild;
-            if (stack[enPt].p[axis] <= split) {
-                if (stack[exPt].p[axis] <= split) { node = left; n = nodes[node]; continue; }
-                if (stack[enPt].p[axis] == split) { node = left + 1; n = nodes[node]; continue; }
+            if (enP <= split) {
+                if (exP <= split) { node = left; n = nodes[node]; continue; }
+                if (enP == split) { node = left + 1; n = nodes[node]; continue; }
                 node = left;
                 farChild = left + 1;
             } else {
-                if (split < stack[exPt].p[axis]) { node = left + 1; n = nodes[node]; continue; }
+                if (split < exP) { node = left + 1; n = nodes[node]; continue; }
                 farChild = left;
                 node = left + 1;
             }
-            const float distToSplit = (split - oa[axis]) * rcp[axis];
+            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float distToSplit = (split - oa) * rcp[axis];
             const uint32_t tmp = exPt++;
             if (exPt == enPt) ++exPt;
             if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-            stack[exPt].prev = tmp;
+            stack[exPt].prev_axis = tmp | ((uint32_t)axis << 8);
             stack[exPt].t = distToSplit;
+            stack[exPt].split = split;
             stack[exPt].node = farChild;
-            for (int k = 0; k < 3; ++k) stack[exPt].p[k] = oa[k] + da[k] * distToSplit;
-            stack[exPt].p[axis] = split;
+            ex_t = distToSplit;
+            ex_split = split;
+            ex_axis = (uint32_t)axis;
             n = nodes[node];
         }
         for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
             const uint32_t prim = indices[e];
-            if (mbox[prim & 7u] == prim) continue;
+#ifndef MTSG_KD_MBOX_REGS
+            if (mbox[prim & 7u] == prim) continue;   // the hashed mailbox (sahkdtree3.h:138-152)
+#else
+            // A/B only (C3 -2%, C4 -9%): the mailbox held in registers.  A
+            // primitive is only ever stored in slot prim & 7, so "slot prim & 7
+            // holds prim" is "some slot holds prim": 8 compares and 8 selects
+            // instead of a dynamically indexed scratch load and store
+            bool seen = false;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) seen |= mbox[i] == prim;
+            if (seen) continue;
+#endif
             const MtsgTri &tr = tris[prim];
             const uint32_t k = tr.k;
             float o_u, o_v, o_k, d_u, d_v, d_k;
@@ -945,12 +974,24 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
                     bt = t; bu = u; bv = v; bprim = prim;
                 }
             }
+#ifndef MTSG_KD_MBOX_REGS
             mbox[prim & 7u] = prim;
+#else
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mbox[i] = (prim & 7u) == (uint32_t)i ? prim : mbox[i];
+#endif
         }
-        if (stack[exPt].t > maxt) break;
+        if (ex_t > maxt) break;
         enPt = exPt;
+        en_t = ex_t;
+        en_split = ex_split;
+        en_axis = ex_axis;
         node = stack[exPt].node;
-        exPt = stack[enPt].prev;
+        exPt = stack[enPt].prev_axis & 0xffu;
+        const Ent e = stack[exPt];
+        ex_t = e.t;
+        ex_split = e.split;
+        ex_axis = e.prev_axis >> 8;
     }
     return found;
 }

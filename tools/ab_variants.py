@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of libmtsgpu variants in one process (guide rule 24).
 usage: ab_variants.py <config> <rounds> <rows_stride> name=path[,ENV=VAL...] ...
-(environment overrides are applied around each variant's render calls)"""
+(environment overrides are applied around each variant's render calls;
+AB_ENGINE=wavefront|megakernel|kdtree picks the engine of every variant)"""
 import os
 import sys
 
@@ -14,6 +15,7 @@ from mitsuba_amd import scenes  # noqa: E402
 from mitsuba_amd.integrator import Context  # noqa: E402
 
 cfg, rounds, stride = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+engine = os.environ.get('AB_ENGINE') or None
 variants, envs = [], {}
 for a in sys.argv[4:]:
     name, rest = a.split('=', 1)
@@ -40,13 +42,13 @@ ctxs = {}
 for name, path in variants:
     c = Context(0, lib_path=path)
     with_env(name, lambda: c.upload(sc))
-    with_env(name, lambda: c.render(it, row=(8, stride, 0)))   # warm up
+    with_env(name, lambda: c.render(it, row=(8, stride, 0), engine=engine))   # warm up
     ctxs[name] = c
 res = {n: [] for n, _ in variants}
 films = {}
 for r in range(rounds):
     for name, _ in variants:
-        film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0)))
+        film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0), engine=engine))
         films.setdefault(name, film)
         res[name].append(st['samples'] / st['kernel_ms'] / 1e3)
 first = variants[0][0]
