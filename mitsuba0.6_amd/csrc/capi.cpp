@@ -34,13 +34,13 @@ hipError_t mtsg_launch_trace_kd(const MtsgDeviceScene &S, const uint32_t *kdNode
                                 const MtsgTri *kdTris, const float *rays, uint32_t n, float *out, bool shadow,
                                 int numCUs, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
-hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
-                                bool instr, hipStream_t s);
+hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid, int wk,
+                                bool ggx, bool instr, hipStream_t s);
 hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
                                 bool stats, hipStream_t s);
 hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters,
                                 hipStream_t s);
-int mtsg_wf_occupancy(const MtsgLaunch &L, int *shadeBpc, int *traceBpc);
+int mtsg_wf_occupancy(const MtsgLaunch &L, int wk, bool ggx, int *shadeBpc, int *traceBpc);
 hipError_t mtsg_launch_sfmt_probe(uint32_t *w, unsigned long long *out, int n, hipStream_t s);
 hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
                                hipStream_t s);
@@ -81,14 +81,14 @@ struct mtsgpu_ctx {
     MtsgDeviceScene dscene;
     DevBuf scan_tris;   // k-grouped TriAccel records of scan-sized scenes
     uint32_t scan_n[3] = {0, 0, 0};
-    DevBuf nodes, hnodes, qnodes, trav_ovf, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
+    DevBuf nodes, hnodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
     DevBuf qrays, qhits;      // mtsgpu_trace_rays staging
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
     // wavefront pipeline: path slots, ray queues and results, counters
-    DevBuf wf_state, wf_qray, wf_sray, wf_hit, wf_occl, wf_rcnt, wf_live, wf_ovf, wf_part;
+    DevBuf wf_state, wf_ray, wf_rslot, wf_cls, wf_cnt, wf_hit, wf_occl, wf_live, wf_ovf, wf_part, wf_kind;
     DevBuf rp_order, rp_start, rp_sfmt;   // SFMT replay: render order, unit starts, streams
     // the reference's SAH kd-tree (kdtree_build.cpp), built on first use
     bool kd_built = false;
@@ -96,6 +96,7 @@ struct mtsgpu_ctx {
     DevBuf kd_nodes, kd_indices, kd_tris;
     uint32_t *wf_live_host = nullptr;   // pinned: live-slot counts read back while the pipeline runs
     hipEvent_t wf_ev[8] = {};
+    std::vector<uint32_t> wf_kind_host;   // shape -> shade kind (wf_kinds)
     unsigned long long last_counters[16] = {};
 };
 
@@ -197,7 +198,6 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     HostScene &H = ctx->host;
     hipStream_t s = ctx->stream;
     if ((e = upload(ctx->nodes, H.nodes, s)) != hipSuccess || (e = upload(ctx->hnodes, H.hnodes, s)) != hipSuccess ||
-        (e = upload(ctx->qnodes, H.qnodes, s)) != hipSuccess ||
         (e = upload(ctx->tris, H.tris, s)) != hipSuccess ||
         (e = upload(ctx->prim_vtx, H.prim_vtx, s)) != hipSuccess || (e = upload(ctx->dpdu, H.dpdu, s)) != hipSuccess ||
         (e = upload(ctx->positions, H.positions, s)) != hipSuccess || (e = upload(ctx->normals, H.normals, s)) != hipSuccess ||
@@ -248,7 +248,6 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
     std::memset(&D, 0, sizeof D);
     D.nodes = (const MtsgNode *)ctx->nodes.p;
     D.hnodes = (const MtsgHNode *)ctx->hnodes.p;
-    D.qnodes = (const MtsgQNode *)ctx->qnodes.p;
     D.tris = (const MtsgTri *)ctx->tris.p;
     D.prim_vtx = (const uint32_t *)ctx->prim_vtx.p;
     D.dpdu = (const float *)ctx->dpdu.p;
@@ -293,33 +292,48 @@ int mtsgpu_film_border(int32_t rfilter, float rfilter_param) {
     return f.border;
 }
 
-// The wavefront pipeline for one chunk of samples: bounce after bounce,
-// wf_shade (consume results, shade, regenerate, append the next rays) then
-// wf_trace (both queues), until no path slot is live.  The live count of every
-// POLL-th bounce is read back asynchronously; the host stays at most LAG polls
-// ahead of the GPU, so the queue never drains and the overshoot (empty bounces)
-// stays small.
+// The wavefront engine's launch plan: the shade kinds the scene's shapes can
+// reach (the MISS kind always), each kernel's grid, the trace grid, the slots
+struct WfPlan {
+    bool kinds[MTSG_WK_KINDS] = {};
+    bool ggx[MTSG_WK_KINDS] = {};
+    int shadeGrid[MTSG_WK_KINDS] = {};
+    int traceGrid = 0;
+    uint32_t slots = 0;
+};
+
+// The wavefront engine for one chunk of samples (wf_kernel.hip): the MISS
+// kernel starts every slot's first path, then bounce after bounce the shade
+// kernel of each kind, then the trace kernel, until no path slot is live.  The
+// live count of every POLL-th bounce is read back asynchronously; the host
+// stays at most LAG polls ahead of the GPU, so the queues never drain and the
+// overshoot (empty bounces) stays small.
 static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, bool stats, hipStream_t stream,
-                           int shadeGrid, int traceGrid, uint32_t slots, const volatile int *cancel) {
+                           const WfPlan &plan, const volatile int *cancel) {
     hipError_t e;
+    const uint32_t slots = plan.slots;
+    const size_t cap = slots, R = MTSG_WF_REGIONS;
     MtsgWave W;
     std::memset(&W, 0, sizeof W);
     W.state = (float4 *)ctx->wf_state.p;
-    W.qray = (float4 *)ctx->wf_qray.p;
-    W.sray = (float4 *)ctx->wf_sray.p;
+    for (int p = 0; p < 2; ++p) {
+        W.ray[p] = (float4 *)ctx->wf_ray.p + (size_t)p * 2 * R * cap * 2;
+        W.rslot[p] = (uint32_t *)ctx->wf_rslot.p + (size_t)p * 2 * R * cap;
+        W.cls[p] = (uint32_t *)ctx->wf_cls.p + (size_t)p * MTSG_WK_KINDS * R * cap;
+    }
+    W.cnt = (uint32_t *)ctx->wf_cnt.p;
     W.hit = (float4 *)ctx->wf_hit.p;
     W.occl = (uint32_t *)ctx->wf_occl.p;
-    W.rcnt = (uint32_t *)ctx->wf_rcnt.p;
     W.live = (uint32_t *)ctx->wf_live.p;
     W.ovf = (uint2 *)ctx->wf_ovf.p;
+    W.shape_kind = (const uint32_t *)ctx->wf_kind.p;
     W.slots = slots;
-    W.regions = (uint32_t)shadeGrid;
-    W.rounds = slots / (uint32_t)(shadeGrid * BLOCK_THREADS);
-    W.split = (uint32_t)(traceGrid / shadeGrid);
+    W.cap = (uint32_t)cap;
     W.ovf_depth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
     unsigned long long *part = (unsigned long long *)ctx->wf_part.p;
-    const int partBlocks = std::max(shadeGrid, traceGrid);
-    if ((e = hipMemsetAsync((char *)ctx->wf_state.p + (size_t)7 * slots * 16, 0, (size_t)slots * 16, stream)) != hipSuccess ||
+    int partBlocks = plan.traceGrid;
+    for (int k = 0; k < MTSG_WK_KINDS; ++k) partBlocks = std::max(partBlocks, plan.shadeGrid[k]);
+    if ((e = hipMemsetAsync(ctx->wf_cnt.p, 0, (size_t)2 * MTSG_WF_QUEUES * R * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(ctx->wf_live.p, 0, 2 * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(part, 0, (size_t)partBlocks * 16 * 8, stream)) != hipSuccess)
         return hip_fail(ctx, e, "wavefront reset");
@@ -329,8 +343,13 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     for (uint64_t it = 0;; ++it) {
         if (it >= maxBounces) return fail(ctx, MTSGPU_EHIP, "wavefront: no convergence");
         W.parity = (uint32_t)(it & 1);
-        if ((e = mtsg_launch_wf_shade(L, W, part, shadeGrid, instr, stream)) != hipSuccess)
-            return hip_fail(ctx, e, "wf_shade launch");
+        W.seed = it == 0 ? 1u : 0u;
+        for (int k = 0; k < MTSG_WK_KINDS; ++k) {
+            if (!plan.kinds[k] || (it == 0 && k != MTSG_WK_MISS)) continue;
+            if ((e = mtsg_launch_wf_shade(L, W, part, plan.shadeGrid[k], k, plan.ggx[k], instr, stream)) != hipSuccess)
+                return hip_fail(ctx, e, "wf_shade launch");
+        }
+        W.seed = 0;
         if (it % POLL == 0) {
             const int r = polls % RING;
             if ((e = hipMemcpyAsync(ctx->wf_live_host + r, W.live + W.parity, 4, hipMemcpyDeviceToHost,
@@ -339,7 +358,7 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
                 return hip_fail(ctx, e, "wavefront poll");
             ++polls;
         }
-        if ((e = mtsg_launch_wf_trace(L, W, part, traceGrid, stats, stream)) != hipSuccess)
+        if ((e = mtsg_launch_wf_trace(L, W, part, plan.traceGrid, stats, stream)) != hipSuccess)
             return hip_fail(ctx, e, "wf_trace launch");
         bool finished = false;
         while (!finished && polls > checked) {
@@ -355,6 +374,32 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     if ((e = mtsg_launch_wf_flush(part, (uint32_t)partBlocks, L.counters, stream)) != hipSuccess)
         return hip_fail(ctx, e, "wf_flush launch");
     return MTSGPU_OK;
+}
+
+// shape -> shade kind (wf_kernel.hip) from the shape's BSDF type; per kind,
+// whether every BSDF of that kind uses the GGX distribution
+static void wf_kinds(const HostScene &H, std::vector<uint32_t> &shapeKind, WfPlan &plan) {
+    bool any[MTSG_WK_KINDS] = {}, nonGgx[MTSG_WK_KINDS] = {};
+    shapeKind.assign(std::max<size_t>(1, H.shapes.size()), (uint32_t)MTSG_WK_GEN);
+    for (size_t i = 0; i < H.shapes.size(); ++i) {
+        const MtsgBsdf &b = H.bsdfs[H.shapes[i].bsdf];
+        int k = MTSG_WK_GEN;
+        switch (b.type) {
+            case MTSGPU_BSDF_DIFFUSE: k = MTSG_WK_DIFF; break;
+            case MTSGPU_BSDF_ROUGHCONDUCTOR: k = MTSG_WK_RC; break;
+            case MTSGPU_BSDF_ROUGHDIELECTRIC: k = MTSG_WK_RD; break;
+            case MTSGPU_BSDF_ROUGHPLASTIC: k = MTSG_WK_RP; break;
+            default: break;
+        }
+        if (std::getenv("MTSGPU_WF_GENERIC")) k = MTSG_WK_GEN;   // A/B: every hit through the generic kernel
+        shapeKind[i] = (uint32_t)k;
+        any[k] = true;
+        if (b.distr != MTSGPU_DISTR_GGX) nonGgx[k] = true;
+    }
+    for (int k = 0; k < MTSG_WK_KINDS; ++k) {
+        plan.kinds[k] = any[k] || k == MTSG_WK_MISS;
+        plan.ggx[k] = any[k] && !nonGgx[k];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -627,17 +672,6 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         if (nl > 1) { L.lum_dim = L.array_end; L.array_end += 2; }
         if (nb > 1) { L.bsdf_dim = L.array_end; L.array_end += 2; }
     }
-    L.trav_ovf = nullptr;
-    L.ovf_depth = 0;
-#ifdef MTSG_BVH4
-    // the BSDF-set variants traverse the 4-wide BVH (<= 3 pushes per level):
-    // MTSG_Q_LDS_STACK entries per lane in LDS, deeper ones in HBM (trav_ovf)
-    if (L.bset && !L.scene_lds) {
-        L.stack_depth = std::max<uint32_t>(L.stack_depth, MTSG_Q_LDS_STACK);
-        const uint32_t need = 3 * H.qnode_depth + 1;
-        L.ovf_depth = need > MTSG_Q_LDS_STACK ? need - MTSG_Q_LDS_STACK : 0;
-    }
-#endif
     L.waves = 3;
     if (!L.scene_lds) {
         const size_t perBlock = (160u << 10) / 4;
@@ -692,12 +726,6 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     int bpc = 0;
     mtsg_path_kernel_occupancy(L, &bpc);
     if (bpc <= 0) bpc = 1;
-    if (L.ovf_depth) {
-        const size_t lanes = (size_t)ctx->num_cus * bpc * BLOCK_THREADS;
-        if ((e = ctx->trav_ovf.ensure(lanes * L.ovf_depth * 8)) != hipSuccess)
-            return hip_fail(ctx, e, "traversal overflow stack");
-        L.trav_ovf = (uint32_t *)ctx->trav_ovf.p;
-    }
     const bool stats_mode = (P->flags & MTSGPU_FLAG_TRAVERSAL_STATS) != 0;
     if (replay) {
         // IndependentSampler's Random() = seed(5489); RenderJob clones it per worker in
@@ -740,31 +768,43 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         L.kd_indices = (const uint32_t *)ctx->kd_indices.p;
         L.kd_tris = (const MtsgTri *)ctx->kd_tris.p;
     }
-    int shadeGrid = 0, traceGrid = 0;
-    uint32_t slots = 0;
+    WfPlan plan;
     if (wave) {
-        int sb = 0, tb = 0;
-        mtsg_wf_occupancy(L, &sb, &tb);
-        if (sb <= 0 || tb <= 0) return fail(ctx, MTSGPU_EHIP, "wavefront kernels do not fit the device");
-        shadeGrid = std::max(8, ctx->num_cus * sb / 8 * 8);   // a multiple of 8: XCD-aware slot lanes
-        const int split = std::max(1, (ctx->num_cus * tb + shadeGrid - 1) / shadeGrid);
-        traceGrid = shadeGrid * split;
-        const uint64_t lanes = (uint64_t)shadeGrid * BLOCK_THREADS;
+        std::vector<uint32_t> &shapeKind = ctx->wf_kind_host;   // kept alive for the async upload
+        wf_kinds(ctx->host, shapeKind, plan);
+        const size_t R = MTSG_WF_REGIONS;
+        int minBpc = 1 << 30;
+        for (int k = 0; k < MTSG_WK_KINDS; ++k) {
+            if (!plan.kinds[k]) continue;
+            int sb = 0, tb = 0;
+            mtsg_wf_occupancy(L, k, plan.ggx[k], &sb, &tb);
+            if (sb <= 0 || tb <= 0) return fail(ctx, MTSGPU_EHIP, "wavefront kernels do not fit the device");
+            plan.shadeGrid[k] = ctx->num_cus * sb;
+            plan.traceGrid = ctx->num_cus * tb;
+            minBpc = std::min(minBpc, sb);
+        }
+        // path slots: about 2M (MTSGPU_WF_SLOTS), a multiple of the smallest shade grid's lanes
+        const uint64_t lanes = (uint64_t)ctx->num_cus * minBpc * BLOCK_THREADS;
         uint64_t target = (uint64_t)1 << 21;
         if (const char *env = std::getenv("MTSGPU_WF_SLOTS")) target = std::max<uint64_t>(1, std::strtoull(env, nullptr, 10));
         const uint64_t items = (uint64_t)std::min(chunk, P->spp) * L.num_pixels;
         target = std::min(target, items);
-        slots = (uint32_t)(std::max<uint64_t>(1, (target + lanes - 1) / lanes) * lanes);
+        plan.slots = (uint32_t)(std::max<uint64_t>(1, (target + lanes - 1) / lanes) * lanes);
+        const size_t slots = plan.slots, cap = slots;
         const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
+        int partBlocks = plan.traceGrid;
+        for (int k = 0; k < MTSG_WK_KINDS; ++k) partBlocks = std::max(partBlocks, plan.shadeGrid[k]);
         if ((e = ctx->wf_state.ensure((size_t)MTSG_WF_STATE_VECS * slots * 16)) != hipSuccess ||
-            (e = ctx->wf_qray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
-            (e = ctx->wf_sray.ensure((size_t)2 * slots * 16)) != hipSuccess ||
-            (e = ctx->wf_hit.ensure((size_t)slots * 16)) != hipSuccess ||
-            (e = ctx->wf_occl.ensure((size_t)slots * 4)) != hipSuccess ||
-            (e = ctx->wf_rcnt.ensure((size_t)4 * shadeGrid * 4)) != hipSuccess ||
+            (e = ctx->wf_ray.ensure((size_t)2 * 2 * R * cap * 32)) != hipSuccess ||
+            (e = ctx->wf_rslot.ensure((size_t)2 * 2 * R * cap * 4)) != hipSuccess ||
+            (e = ctx->wf_cls.ensure((size_t)2 * MTSG_WK_KINDS * R * cap * 4)) != hipSuccess ||
+            (e = ctx->wf_cnt.ensure((size_t)2 * MTSG_WF_QUEUES * R * 4)) != hipSuccess ||
+            (e = ctx->wf_hit.ensure(slots * 16)) != hipSuccess ||
+            (e = ctx->wf_occl.ensure(slots * 4)) != hipSuccess ||
             (e = ctx->wf_live.ensure(2 * 4)) != hipSuccess ||
-            (e = ctx->wf_ovf.ensure((size_t)traceGrid * BLOCK_THREADS * ovfDepth * 8)) != hipSuccess ||
-            (e = ctx->wf_part.ensure((size_t)std::max(shadeGrid, traceGrid) * 16 * 8)) != hipSuccess)
+            (e = ctx->wf_ovf.ensure((size_t)plan.traceGrid * BLOCK_THREADS * ovfDepth * 8)) != hipSuccess ||
+            (e = ctx->wf_part.ensure((size_t)partBlocks * 16 * 8)) != hipSuccess ||
+            (e = upload(ctx->wf_kind, shapeKind, stream)) != hipSuccess)
             return hip_fail(ctx, e, "wavefront buffers");
         if (!ctx->wf_live_host) {
             if ((e = hipHostMalloc((void **)&ctx->wf_live_host, 8 * sizeof(uint32_t))) != hipSuccess)
@@ -780,8 +820,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         L.chunk_spp = std::min(chunk, P->spp - j0);
         L.num_items = (uint64_t)L.chunk_spp * L.num_pixels;
         if (wave) {
-            const int rc = wf_render_chunk(ctx, L, nsamp != 0 || stats_mode, stats_mode, stream, shadeGrid, traceGrid,
-                                           slots, P->cancel);
+            const int rc = wf_render_chunk(ctx, L, nsamp != 0 || stats_mode, stats_mode, stream, plan, P->cancel);
             if (rc != MTSGPU_OK) return rc;
         } else {
             const uint64_t blocksNeeded = replay ? (L.units + 255) / 256 : (L.num_items + 255) / 256;
@@ -888,13 +927,13 @@ const char *mtsgpu_last_error(mtsgpu_ctx *ctx) { return ctx ? ctx->err.c_str() :
 void mtsgpu_destroy(mtsgpu_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->hnodes, &ctx->qnodes, &ctx->trav_ovf, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
+    DevBuf *bufs[] = {&ctx->scan_tris, &ctx->kd_nodes, &ctx->kd_indices, &ctx->kd_tris, &ctx->nodes, &ctx->hnodes, &ctx->tris, &ctx->prim_vtx, &ctx->dpdu, &ctx->positions, &ctx->normals,
                       &ctx->shapes, &ctx->bsdfs, &ctx->emitters, &ctx->area_cdf, &ctx->em_cdf, &ctx->sobol,
                       &ctx->film_own, &ctx->film_spill, &ctx->samples, &ctx->counters, &ctx->contrib,
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
-                      &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_qray, &ctx->wf_sray, &ctx->wf_hit,
-                      &ctx->wf_occl, &ctx->wf_rcnt, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
+                      &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_ray, &ctx->wf_rslot, &ctx->wf_cls,
+                      &ctx->wf_cnt, &ctx->wf_hit, &ctx->wf_occl, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->wf_kind, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
     for (hipEvent_t &e : ctx->wf_ev)
         if (e) (void)hipEventDestroy(e);
@@ -980,6 +1019,7 @@ int mtsgpu_bvh_host(const mtsgpu_scene_desc *scene, uint32_t *nodes, size_t node
         msg[cap - 1] = 0;
     }
     if (rc) return rc;
+    mtsg_build_qnodes(H);
     info4[0] = (uint32_t)H.nodes.size();
     info4[1] = (uint32_t)H.hnodes.size();
     info4[2] = (uint32_t)H.qnodes.size();

@@ -98,9 +98,6 @@ __device__ __forceinline__ bool solve_quadratic_f(float a, float b, float c, flo
     return true;
 }
 
-#ifdef MTSG_ANYHIT_NANDEBUG   // diagnostic build: report any-hit sphere tests whose roots are NaN
-__device__ unsigned int g_nan_root_events;
-#endif
 
 // Shape::rayIntersect(ray, mint, maxt, t, temp) (closest) / rayIntersect(ray, mint, maxt)
 // (ANY); (lx, ly) = the rectangle's / disk's object-space hit (the `temp` data)
@@ -118,32 +115,9 @@ __device__ __forceinline__ bool ana_intersect(GAna &a, f3 o, f3 d, float mint, f
         double nearT, farT;
         if (!solve_quadratic_d(A, B, C, nearT, farT)) return false;
         if (ANY) {   // sphere.cpp:189-207
-#ifdef MTSG_ANYHIT_NANDEBUG
-            if (nearT != nearT || farT != farT) {
-                const unsigned int k = atomicAdd(&g_nan_root_events, 1u);
-                if (k < 8)
-                    printf("NANROOT %u o %.9g %.9g %.9g d %.9g %.9g %.9g c %.9g %.9g %.9g r %.9g A %.17g B %.17g C %.17g "
-                           "near %.17g far %.17g mint %.9g maxt %.9g\n",
-                           k, o.x, o.y, o.z, d.x, d.y, d.z, a.center[0], a.center[1], a.center[2], a.radius, A, B, C,
-                           nearT, farT, mint, maxt);
-            }
-#endif
-#ifdef MTSG_SPHERE_ANY_NANAWARE
-            // the same predicate in the closest-hit query's NaN-aware form, with
-            // the NaN roots (b == c == 0 exactly: the origin on the surface, the
-            // direction tangent) taken by the reference's comparisons explicitly
-            if (nearT != nearT || farT != farT) return !(nearT > maxt) && !(farT < mint);
-            if (!(nearT <= maxt && farT >= mint)) return false;
-            if (nearT < mint && farT > maxt) return false;
-            return true;
-#else
-#ifdef MTSG_ANYHIT_XC_SLOT   // diagnostic build: report the roots of an accepted any-hit test
-            t = (float)nearT; lx = (float)farT; ly = maxt;
-#endif
             if (nearT > maxt || farT < mint) return false;
             if (nearT < mint && farT > maxt) return false;
             return true;
-#endif
         }
         if (!(nearT <= maxt && farT >= mint)) return false;
         if (nearT < mint) {

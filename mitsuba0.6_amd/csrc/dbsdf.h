@@ -120,12 +120,13 @@ struct Distr { int type; float alphaU, alphaV; int sampleVisible; float expU, ex
 // compiles only the lobes and the distribution the scene has, and inlines the
 // microfacet helpers that the generic set calls out of line
 // (profiles/r03_ab_spec_C*.log).
-#define BSET_BITS (MTSG_FEAT_EXT | MTSG_FEAT_DIFF | MTSG_FEAT_GGX | MTSG_FEAT_NORC | MTSG_FEAT_NORD)
+#define BSET_BITS (MTSG_FEAT_EXT | MTSG_FEAT_DIFF | MTSG_FEAT_GGX | MTSG_FEAT_NORC | MTSG_FEAT_NORD | MTSG_FEAT_INL)
 template <int BS> struct BSet {
     static constexpr bool EXT = (BS & MTSG_FEAT_EXT) != 0, DIFF = (BS & MTSG_FEAT_DIFF) != 0;
     static constexpr bool GGX = (BS & MTSG_FEAT_GGX) != 0;
     static constexpr bool RC = (BS & MTSG_FEAT_NORC) == 0, RD = (BS & MTSG_FEAT_NORD) == 0;
-    static constexpr bool INL = GGX;   // helpers inline in specialised sets
+    // helpers inline in specialised sets (GGX) and in the wavefront engine's per-type kernels (INL)
+    static constexpr bool INL = GGX || (BS & MTSG_FEAT_INL) != 0;
 };
 // the distribution type as the variant knows it
 template <int BS> __device__ __forceinline__ int dtype(const Distr &d) { return BSet<BS>::GGX ? (int)DISTR_GGX : d.type; }
@@ -519,11 +520,7 @@ __device__ __forceinline__ bool cubic_weights(float p, uint32_t size, KnotW &k) 
     return true;
 }
 
-#ifdef MTSG_CUBIC2D_INLINE   // A/B: the 2D spline lookup inlined into roughplastic's callers
-__device__ __forceinline__
-#else
 __device__ __noinline__
-#endif
 float cubic2d(float px, float py, glb_f32 *values, uint32_t sx, uint32_t sy) {
     KnotW kx, ky;
     if (!cubic_weights(px, sx, kx)) return 0.0f;
@@ -738,30 +735,34 @@ __device__ __noinline__ BSample sm_sample(GBsdf &b, f3 wi, float sx, float sy, f
 }
 
 // ---- BSDF::eval / pdf / sample --------------------------------------------
+// one BSDF type's eval / pdf / sample bodies (inlined into the dispatchers
+// below, and on their own into the wavefront engine's per-type shade kernels)
 template <int BS>
-__device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+__device__ __forceinline__ f3 diff_eval_body(GBsdf &b, f3 wi, f3 wo, float u, float v) {   // diffuse.cpp:110-117
+    if (wi.z <= 0 || wo.z <= 0) return mk(0, 0, 0);
+    return mul(bsdf_refl<BS>(b, u, v), D_INV_PI * wo.z);
+}
+__device__ __forceinline__ float diff_pdf_body(f3 wi, f3 wo) {                            // diffuse.cpp:119-126
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    return D_INV_PI * wo.z;
+}
+template <int BS>
+__device__ __forceinline__ f3 rc_eval_body(GBsdf &b, f3 wi, f3 wo, float u, float v) {   // roughconductor.cpp:257-292
     const f3 zero = mk(0, 0, 0);
-    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:110-117
-        if (wi.z <= 0 || wo.z <= 0) return zero;
-        return mul(bsdf_refl<BS>(b, u, v), D_INV_PI * wo.z);
-    }
-    if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
-        if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
-    }
-    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:257-292
-        if (wi.z <= 0 || wo.z <= 0) return zero;
-        f3 H = normalize(add(wo, wi));
-        Distr d = bsdf_distr<BS>(b, u, v);
-        float D = distr_eval<BS>(d, H);
-        if (D == 0) return zero;
-        f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
-        float G = distr_smithG1<BS>(d, wi, H) * distr_smithG1<BS>(d, wo, H);
-        float model = D * G / (4.0f * wi.z);
-        return mul(F, model);
-    }
-    if (!BSet<BS>::RD) return zero;
-    if (wi.z == 0) return zero;                                            // roughdielectric.cpp:270-346
+    if (wi.z <= 0 || wo.z <= 0) return zero;
+    f3 H = normalize(add(wo, wi));
+    Distr d = bsdf_distr<BS>(b, u, v);
+    float D = distr_eval<BS>(d, H);
+    if (D == 0) return zero;
+    f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, H), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+    float G = distr_smithG1<BS>(d, wi, H) * distr_smithG1<BS>(d, wo, H);
+    float model = D * G / (4.0f * wi.z);
+    return mul(F, model);
+}
+template <int BS>
+__device__ __forceinline__ f3 rd_eval_body(GBsdf &b, f3 wi, f3 wo, float u, float v) {   // roughdielectric.cpp:270-346
+    const f3 zero = mk(0, 0, 0);
+    if (wi.z == 0) return zero;
     bool reflect = wi.z * wo.z > 0;
     f3 H;
     if (reflect) {
@@ -789,24 +790,28 @@ __device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo
 }
 
 template <int BS>
-__device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
-    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:119-126
-        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
-        return D_INV_PI * wo.z;
-    }
+__device__ __forceinline__ f3 bsdf_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if (b.type == BSDF_DIFFUSE) return diff_eval_body<BS>(b, wi, wo, u, v);
     if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
-        if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_eval<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
+        if (b.type >= BSDF_CONDUCTOR) return sm_eval(b, wi, wo, u, v);
     }
-    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:294-319
-        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
-        f3 H = normalize(add(wo, wi));
-        Distr d = bsdf_distr<BS>(b, u, v);
-        if (b.sample_visible) return distr_eval<BS>(d, H) * distr_smithG1<BS>(d, wi, H) / (4.0f * wi.z);
-        return distr_pdf<BS>(d, wi, H) / (4 * absdot(wo, H));
-    }
-    if (!BSet<BS>::RD) return 0.0f;
-    bool reflect = wi.z * wo.z > 0;                                        // roughdielectric.cpp:348-405
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) return rc_eval_body<BS>(b, wi, wo, u, v);
+    if (!BSet<BS>::RD) return mk(0, 0, 0);
+    return rd_eval_body<BS>(b, wi, wo, u, v);
+}
+
+template <int BS>
+__device__ __forceinline__ float rc_pdf_body(GBsdf &b, f3 wi, f3 wo, float u, float v) {   // roughconductor.cpp:294-319
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    f3 H = normalize(add(wo, wi));
+    Distr d = bsdf_distr<BS>(b, u, v);
+    if (b.sample_visible) return distr_eval<BS>(d, H) * distr_smithG1<BS>(d, wi, H) / (4.0f * wi.z);
+    return distr_pdf<BS>(d, wi, H) / (4 * absdot(wo, H));
+}
+template <int BS>
+__device__ __forceinline__ float rd_pdf_body(GBsdf &b, f3 wi, f3 wo, float u, float v) {   // roughdielectric.cpp:348-405
+    bool reflect = wi.z * wo.z > 0;
     f3 H;
     float dwh_dwo;
     if (reflect) {
@@ -826,6 +831,18 @@ __device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 
     float F = fresnel_dielectric_ext(dot(wi, H), ct, b.eta);
     prob *= reflect ? F : (1 - F);
     return fabsf(prob * dwh_dwo);
+}
+
+template <int BS>
+__device__ __forceinline__ float bsdf_pdf_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v) {
+    if (b.type == BSDF_DIFFUSE) return diff_pdf_body(wi, wo);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_pdf<BS>(b, rt, wi, wo, u, v, rp_pre<BS>(b, rt, wi, u, v));
+        if (b.type >= BSDF_CONDUCTOR) return sm_pdf(b, wi, wo);
+    }
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) return rc_pdf_body<BS>(b, wi, wo, u, v);
+    if (!BSet<BS>::RD) return 0.0f;
+    return rd_pdf_body<BS>(b, wi, wo, u, v);
 }
 
 template <int BS>
@@ -855,9 +872,11 @@ BSDF_CALL EvalPdf bsdf_eval_pdf(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, fl
 // for the lobe choice (roughdielectric.cpp:554); it is passed in as `u1d` by
 // the caller, which draws it from the sampler only for that BSDF.
 
-// RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458)
-template <int BS>
-BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v, RpPre pre) {
+// RoughPlastic::sample(bRec, pdf, sample) (roughplastic.cpp:395-458); INL:
+// its pdf and eval inline (the per-type shade kernels), else the calls
+template <int BS, bool INL>
+__device__ __forceinline__ BSample rp_sample_body(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v,
+                                                  RpPre pre) {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
     if (wi.z <= 0) return r;
@@ -881,51 +900,58 @@ BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, fl
         r.wo = square_to_cosine_hemisphere(sx, sy);
     }
     r.eta = 1.0f;
-    r.pdf = rp_pdf<BS>(b, rt, wi, r.wo, u, v, pre);
+    r.pdf = INL ? rp_pdf_body<BS>(b, rt, wi, r.wo, u, v, pre) : rp_pdf<BS>(b, rt, wi, r.wo, u, v, pre);
     if (r.pdf == 0) return r;
-    r.weight = divs(rp_eval<BS>(b, rt, wi, r.wo, u, v, pre), r.pdf);
+    r.weight = divs(INL ? rp_eval_body<BS>(b, rt, wi, r.wo, u, v, pre) : rp_eval<BS>(b, rt, wi, r.wo, u, v, pre),
+                    r.pdf);
     return r;
 }
-
 template <int BS>
-BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v,
-                              RpPre pre) {
+BSDF_CALL BSample rp_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u, float v, RpPre pre) {
+    return rp_sample_body<BS, false>(b, rt, wi, sx, sy, u, v, pre);
+}
+
+__device__ __forceinline__ BSample bsample_zero() {
     BSample r;
     r.weight = mk(0, 0, 0); r.pdf = 0; r.eta = 1.0f; r.sampledType = 0; r.wo = mk(0, 0, 1);
-    if (b.type == BSDF_DIFFUSE) {                                          // diffuse.cpp:139-150
-        if (wi.z <= 0) return r;
-        r.wo = square_to_cosine_hemisphere(sx, sy);
-        r.eta = 1.0f;
-        r.sampledType = MTSG_F_DIFF_REFL;
-        r.pdf = D_INV_PI * r.wo.z;
-        r.weight = bsdf_refl<BS>(b, u, v);
-        return r;
-    }
-    if constexpr (BSet<BS>::EXT) {
-        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample<BS>(b, rt, wi, sx, sy, u, v, pre);
-        if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
-    }
-    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) {   // roughconductor.cpp:357-406
-        if (wi.z < 0) return r;
-        Distr d = bsdf_distr<BS>(b, u, v);
-        float pdf;
-        f3 m = distr_sample<BS>(d, wi, sx, sy, pdf);
-        r.pdf = pdf;
-        if (pdf == 0) return r;
-        r.wo = reflect_v(wi, m);
-        r.eta = 1.0f;
-        r.sampledType = MTSG_F_GLOSSY_REFL;
-        if (r.wo.z <= 0) return r;
-        f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, m), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
-        float weight;
-        if (b.sample_visible) weight = distr_smithG1<BS>(d, r.wo, m);
-        else weight = distr_eval<BS>(d, m) * (distr_smithG1<BS>(d, wi, m) * distr_smithG1<BS>(d, r.wo, m)) * dot(wi, m) / (pdf * wi.z);
-        r.pdf = pdf / (4.0f * dot(r.wo, m));
-        r.weight = mul(F, weight);
-        return r;
-    }
-    if (!BSet<BS>::RD) return r;
-    Distr d = bsdf_distr<BS>(b, u, v);                                    // roughdielectric.cpp:525-615
+    return r;
+}
+template <int BS>
+__device__ __forceinline__ BSample diff_sample_body(GBsdf &b, f3 wi, float sx, float sy, float u, float v) {
+    BSample r = bsample_zero();                                            // diffuse.cpp:139-150
+    if (wi.z <= 0) return r;
+    r.wo = square_to_cosine_hemisphere(sx, sy);
+    r.eta = 1.0f;
+    r.sampledType = MTSG_F_DIFF_REFL;
+    r.pdf = D_INV_PI * r.wo.z;
+    r.weight = bsdf_refl<BS>(b, u, v);
+    return r;
+}
+template <int BS>
+__device__ __forceinline__ BSample rc_sample_body(GBsdf &b, f3 wi, float sx, float sy, float u, float v) {
+    BSample r = bsample_zero();                                            // roughconductor.cpp:357-406
+    if (wi.z < 0) return r;
+    Distr d = bsdf_distr<BS>(b, u, v);
+    float pdf;
+    f3 m = distr_sample<BS>(d, wi, sx, sy, pdf);
+    r.pdf = pdf;
+    if (pdf == 0) return r;
+    r.wo = reflect_v(wi, m);
+    r.eta = 1.0f;
+    r.sampledType = MTSG_F_GLOSSY_REFL;
+    if (r.wo.z <= 0) return r;
+    f3 F = mulv(fresnel_conductor_exact<BS>(dot(wi, m), ld3(b.eta3), ld3(b.k3)), ld3(b.spec_r));
+    float weight;
+    if (b.sample_visible) weight = distr_smithG1<BS>(d, r.wo, m);
+    else weight = distr_eval<BS>(d, m) * (distr_smithG1<BS>(d, wi, m) * distr_smithG1<BS>(d, r.wo, m)) * dot(wi, m) / (pdf * wi.z);
+    r.pdf = pdf / (4.0f * dot(r.wo, m));
+    r.weight = mul(F, weight);
+    return r;
+}
+template <int BS>
+__device__ __forceinline__ BSample rd_sample_body(GBsdf &b, f3 wi, float sx, float sy, float u1d, float u, float v) {
+    BSample r = bsample_zero();                                            // roughdielectric.cpp:525-615
+    Distr d = bsdf_distr<BS>(b, u, v);
     Distr sd = d;
     if (!b.sample_visible) distr_scale_alpha<BS>(sd, 1.2f - 0.2f * dsqrt(fabsf(wi.z)));
     float microfacetPDF;
@@ -962,6 +988,19 @@ BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, 
     r.pdf = pdf * fabsf(dwh_dwo);
     r.weight = weight;
     return r;
+}
+
+template <int BS>
+BSDF_CALL BSample bsdf_sample(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u, float v,
+                              RpPre pre) {
+    if (b.type == BSDF_DIFFUSE) return diff_sample_body<BS>(b, wi, sx, sy, u, v);
+    if constexpr (BSet<BS>::EXT) {
+        if (b.type == BSDF_ROUGHPLASTIC) return rp_sample<BS>(b, rt, wi, sx, sy, u, v, pre);
+        if (b.type >= BSDF_CONDUCTOR) return sm_sample(b, wi, sx, sy, u, v);
+    }
+    if (BSet<BS>::RC && (!BSet<BS>::RD || b.type == BSDF_ROUGHCONDUCTOR)) return rc_sample_body<BS>(b, wi, sx, sy, u, v);
+    if (!BSet<BS>::RD) return bsample_zero();
+    return rd_sample_body<BS>(b, wi, sx, sy, u1d, u, v);
 }
 
 // Call-site dispatch.  DIFF_ONLY (MTSG_FEAT_DIFF: every BSDF of the scene is
@@ -1015,4 +1054,37 @@ __device__ __forceinline__ BSample bsdf_sample_fast(GBsdf &b, glb_f32 *rt, f3 wi
     } else {
         return bsdf_sample<BS>(b, rt, wi, sx, sy, u1d, u, v, pre);
     }
+}
+
+// The wavefront engine's per-type shade kernels know the BSDF type of the
+// vertex at compile time (KIND = the BSDF_* type; -1: any, dispatched as
+// above): one type's body inline, no type dispatch and no calls.
+template <int BS, int KIND>
+__device__ __forceinline__ EvalPdf bsdf_eval_pdf_k(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, float u, float v, RpPre pre) {
+    EvalPdf r;
+    if constexpr (KIND == BSDF_DIFFUSE) {
+        r.val = diff_eval_body<BS>(b, wi, wo, u, v);
+        r.pdf = is_zero(r.val) ? 0.0f : diff_pdf_body(wi, wo);
+    } else if constexpr (KIND == BSDF_ROUGHCONDUCTOR) {
+        r.val = rc_eval_body<BS>(b, wi, wo, u, v);
+        r.pdf = is_zero(r.val) ? 0.0f : rc_pdf_body<BS>(b, wi, wo, u, v);
+    } else if constexpr (KIND == BSDF_ROUGHDIELECTRIC) {
+        r.val = rd_eval_body<BS>(b, wi, wo, u, v);
+        r.pdf = is_zero(r.val) ? 0.0f : rd_pdf_body<BS>(b, wi, wo, u, v);
+    } else if constexpr (KIND == BSDF_ROUGHPLASTIC) {
+        r.val = rp_eval_body<BS>(b, rt, wi, wo, u, v, pre);
+        r.pdf = is_zero(r.val) ? 0.0f : rp_pdf_body<BS>(b, rt, wi, wo, u, v, pre);
+    } else {
+        return bsdf_eval_pdf_fast<BS>(b, rt, wi, wo, u, v, pre);
+    }
+    return r;
+}
+template <int BS, int KIND>
+__device__ __forceinline__ BSample bsdf_sample_k(GBsdf &b, glb_f32 *rt, f3 wi, float sx, float sy, float u1d, float u,
+                                                 float v, RpPre pre) {
+    if constexpr (KIND == BSDF_DIFFUSE) return diff_sample_body<BS>(b, wi, sx, sy, u, v);
+    else if constexpr (KIND == BSDF_ROUGHCONDUCTOR) return rc_sample_body<BS>(b, wi, sx, sy, u, v);
+    else if constexpr (KIND == BSDF_ROUGHDIELECTRIC) return rd_sample_body<BS>(b, wi, sx, sy, u1d, u, v);
+    else if constexpr (KIND == BSDF_ROUGHPLASTIC) return rp_sample_body<BS, true>(b, rt, wi, sx, sy, u, v, pre);
+    else return bsdf_sample_fast<BS>(b, rt, wi, sx, sy, u1d, u, v, pre);
 }

@@ -51,17 +51,6 @@ __device__ __forceinline__ float smaxc(f3 s) { float r = s.x; r = smax(r, s.y); 
 
 // libm: glibc's float routines restated bit for bit (glibc_f32.h);
 // math::fastexp/fastlog are double exp/log in the reference (math.h:185-199)
-#ifdef MTSG_ABL_FAST_LIBM   // timing ablation only (not parity-exact): single-precision device libm
-__device__ __forceinline__ void d_sincos(float x, float *s, float *c) { sincosf(x, s, c); }
-__device__ __forceinline__ float d_acos(float x) { return acosf(x); }
-__device__ __forceinline__ float d_atan2(float y, float x) { return atan2f(y, x); }
-__device__ __forceinline__ float d_tan(float x) { return tanf(x); }
-__device__ __forceinline__ float d_atan(float x) { return atanf(x); }
-__device__ __forceinline__ float d_expf(float x) { return expf(x); }
-__device__ __forceinline__ float d_powf(float x, float y) { return powf(x, y); }
-__device__ __forceinline__ float d_fastexp(float x) { return expf(x); }
-__device__ __forceinline__ float d_fastlog(float x) { return logf(x); }
-#else
 __device__ __forceinline__ void d_sincos(float x, float *s, float *c) { glf_sincosf(x, s, c); }
 __device__ __forceinline__ float d_acos(float x) { return glf_acosf(x); }
 __device__ __forceinline__ float d_atan2(float y, float x) { return glf_atan2f(y, x); }
@@ -71,7 +60,6 @@ __device__ __forceinline__ float d_expf(float x) { return glf_expf(x); }
 __device__ __forceinline__ float d_powf(float x, float y) { return glf_powf(x, y); }
 __device__ __forceinline__ float d_fastexp(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float d_fastlog(float x) { return (float)log((double)x); }
-#endif
 
 struct Frame { f3 s, t, n; };
 __device__ __forceinline__ f3 to_local(const Frame &f, f3 v) { return mk(dot(v, f.s), dot(v, f.t), dot(v, f.n)); }

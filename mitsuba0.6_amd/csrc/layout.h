@@ -48,8 +48,8 @@ struct MtsgHNode {
 // node's grandchildren where those are inner nodes), child boxes as halves
 // rounded outward like MtsgHNode: 64 B, four 16 B loads, half the node levels.
 // box[3j .. 3j+2] = child j's {lox hix}{loy hiy}{loz hiz}; child[j]: a node
-// index (> 0), a leaf reference (< 0, mtsg_leaf_ref) or 0 (no child)
-#define MTSG_Q_LDS_STACK 24   // 4-wide BVH: traversal stack entries per lane kept in LDS
+// index (> 0), a leaf reference (< 0, mtsg_leaf_ref) or 0 (no child).  Host
+// export only (mtsgpu_bvh_host): the device traverses the BVH2
 struct MtsgQNode {
     uint32_t box[12];
     int32_t child[4];
@@ -104,7 +104,8 @@ enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4,
        MTSG_FEAT_DIFF = 8,     // DIFF: every BSDF is diffuse (path megakernel, FEAT 0 scenes only)
        // BSDF-set specialisation of the megakernel (dbsdf.h BSet): every rough
        // BSDF uses GGX / no roughdielectric / no roughconductor in the scene
-       MTSG_FEAT_GGX = 16, MTSG_FEAT_NORD = 32, MTSG_FEAT_NORC = 64 };
+       MTSG_FEAT_GGX = 16, MTSG_FEAT_NORD = 32, MTSG_FEAT_NORC = 64,
+       MTSG_FEAT_INL = 128 };   // microfacet / Fresnel helpers inline (the wavefront per-type kernels)
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
 enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
        MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*
@@ -192,7 +193,6 @@ struct MtsgEnv {
 struct MtsgDeviceScene {
     const MtsgNode *nodes;
     const MtsgHNode *hnodes;    // the same nodes, half-float boxes (large scenes)
-    const MtsgQNode *qnodes;    // the same BVH collapsed to 4-wide nodes (large scenes)
     const MtsgTri *tris;
     const uint32_t *prim_vtx;   // 4 per primitive: v0, v1, v2, shape
     const float *dpdu;          // 3 per primitive
@@ -222,28 +222,40 @@ struct MtsgLookup {
     uint32_t ycol[64];
 };
 
-// The wavefront pipeline (path_kernel.hip: wf_shade / wf_trace):
-// per-path state in SoA slots, the two ray queues of one bounce and their
-// results.  wf_shade block b owns queue region [b * rounds * 256, ...) and
-// appends to it densely (one LDS atomic per wave); wf_trace block t works on
-// region t / split.  No global atomics on the data path.
-#define MTSG_WF_STATE_VECS 8          // float4 state vectors per slot
-#define MTSG_WF_NONE 0xffffffffu      // no queue entry (ray skipped or outside the scene box)
+// The wavefront engine (wf_kernel.hip).  One bounce = the
+// per-type shade kernels, each over its queue of path slots (the slots whose
+// closest-hit ray hit a shape whose BSDF is of that type, or missed: kind
+// MISS), then one trace kernel over the two ray queues the shade kernels
+// appended to, which writes the hit records by slot and sorts the slots into
+// the next bounce's per-type queues.  Every queue is split into
+// MTSG_WF_REGIONS regions (appender block b uses region b % regions), each of
+// capacity `cap` = slots, so one wave's append is one atomic on one of 8
+// counters and a region can never overflow; consumers walk the concatenation.
+#define MTSG_WF_STATE_VECS 8          // float4 state vectors per slot (AoS: one slot = 128 B)
+#define MTSG_WF_NONE 0xffffffffu      // hit record prim: no hit
+#define MTSG_WF_REGIONS 8
 #ifndef MTSG_WF_LDS_STACK
-#define MTSG_WF_LDS_STACK 12          // wf_trace: traversal stack entries per lane in LDS (deeper: HBM)
+#define MTSG_WF_LDS_STACK 12          // trace kernel: traversal stack entries per lane in LDS (deeper: HBM)
 #endif
+// shade kinds: the BSDF type at the vertex (wf_kernel.hip specialises each)
+enum { MTSG_WK_MISS = 0, MTSG_WK_DIFF = 1, MTSG_WK_RC = 2, MTSG_WK_RD = 3, MTSG_WK_RP = 4, MTSG_WK_GEN = 5,
+       MTSG_WK_KINDS = 6 };
+#define MTSG_WF_QUEUES (2 + MTSG_WK_KINDS)   // closest rays, shadow rays, the kinds' slot queues
 struct MtsgWave {
-    float4 *state;                    // [MTSG_WF_STATE_VECS][slots]
-    float4 *qray;                     // [2 * slots] closest-hit rays {o, mint}, {d, maxt}
-    float4 *sray;                     // [2 * slots] shadow rays
+    float4 *state;                    // [slots][MTSG_WF_STATE_VECS]
+    float4 *ray[2];                   // [parity][2 (closest, shadow)][regions][cap][2] {o, mint}, {d, maxt}
+    uint32_t *rslot[2];               // [parity][2][regions][cap] the slot of each ray
+    uint32_t *cls[2];                 // [parity][kinds][regions][cap] slot queues
+    uint32_t *cnt;                    // [parity][MTSG_WF_QUEUES][regions] entries
     float4 *hit;                      // [slots] {t, u, v, prim (TriAccel slot with analytic shapes) | MTSG_WF_NONE}
     uint32_t *occl;                   // [slots] shadow results
-    uint32_t *rcnt;                   // [2 parities][2 queues][regions] entries per region
-    uint32_t *live;                   // [2 parities] live slots after wf_shade
-    uint2 *ovf;                       // wf_trace stack overflow: [trace lanes][ovf_depth]
-    uint32_t slots;                   // = regions * rounds * 256
+    uint32_t *live;                   // [2 parities] live slots after the bounce's shade kernels
+    uint2 *ovf;                       // trace stack overflow: [trace lanes][ovf_depth]
+    const uint32_t *shape_kind;       // [shapes] MTSG_WK_* of the shape's BSDF
+    uint32_t slots, cap;
     uint32_t parity;                  // bounce index & 1
-    uint32_t regions, rounds, split, ovf_depth;
+    uint32_t seed;                    // first bounce: the MISS kernel takes every slot (identity queue)
+    uint32_t ovf_depth;
 };
 
 struct MtsgLaunch {
@@ -271,8 +283,6 @@ struct MtsgLaunch {
     uint32_t lds_dims;                // dims [0, lds_dims) staged in LDS
     uint32_t nibbles;                 // 8 (index < 2^32) or MTSG_NIBBLES
     uint32_t stack_depth;             // LDS traversal stack entries per lane
-    uint32_t *trav_ovf;               // 4-wide BVH: per-lane stack entries beyond the LDS ones ({node, dist} pairs)
-    uint32_t ovf_depth;               // entries per lane in trav_ovf
     uint32_t num_nodes;               // BVH2 inner nodes
     uint32_t scene_lds;               // 1: nodes + TriAccel staged in LDS (small scenes)
     uint32_t waves;                   // kernel variant: waves per SIMD it is compiled for (3 or 4)

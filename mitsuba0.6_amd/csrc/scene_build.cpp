@@ -1509,13 +1509,18 @@ int mtsg_configure_scene(const mtsgpu_scene_desc *D, HostScene &S, std::string &
     if (B.maxDepth + 1 >= 32) { err = "BVH too deep for the traversal stack"; return MTSGPU_EINVAL; }
     S.hnodes.resize(S.nodes.size());
     for (size_t i = 0; i < S.nodes.size(); ++i) S.hnodes[i] = half_node(S.nodes[i]);
+    // triangles in leaf order
+    S.tris.resize(prims);
+    for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];
+    return MTSGPU_OK;
+}
+
+// the 4-wide collapse of the BVH2 for mtsgpu_bvh_host only (the device traverses
+// the BVH2: the 4-wide traversal lost 5-6%)
+void mtsg_build_qnodes(HostScene &S) {
     S.qnodes.clear();
     S.qnodes.reserve(S.nodes.size() / 2 + 2);
     QCollapse qc{S.nodes, S.qnodes};
     qc.emit(0, 1);
     S.qnode_depth = qc.depth;
-    // triangles in leaf order
-    S.tris.resize(prims);
-    for (uint32_t i = 0; i < prims; ++i) S.tris[i] = tacc[B.order[i]];
-    return MTSGPU_OK;
 }

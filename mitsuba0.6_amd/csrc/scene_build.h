@@ -27,7 +27,7 @@ int mtsg_rtrans_check(const MtsgRTrans &t, float eta, float alphaMin, float alph
 struct HostScene {
     std::vector<MtsgNode> nodes;
     std::vector<MtsgHNode> hnodes;   // the same BVH, half-float boxes
-    std::vector<MtsgQNode> qnodes;   // the same BVH collapsed to 4-wide nodes
+    std::vector<MtsgQNode> qnodes;   // the same BVH collapsed to 4-wide nodes (mtsg_build_qnodes, host export only)
     uint32_t qnode_depth = 0;        // inner-node levels of qnodes
     std::vector<MtsgTri> tris;
     std::vector<uint32_t> prim_vtx;
@@ -54,6 +54,7 @@ struct HostScene {
 
 // Returns MTSGPU_OK or an error code; `err` receives the message.
 int mtsg_configure_scene(const mtsgpu_scene_desc *desc, HostScene &out, std::string &err);
+void mtsg_build_qnodes(HostScene &S);   // host export only (mtsgpu_bvh_host)
 int mtsg_configure_filter(int32_t type, float param, MtsgFilter &f, std::string &err);
 // Sobol: 1024 x 52 matrices regenerated from the Joe-Kuo parameters, and the
 // look_up GF(2) tables for resolution 2^m.

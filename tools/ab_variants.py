@@ -2,7 +2,8 @@
 """Interleaved A/B timing of libmtsgpu variants in one process (guide rule 24).
 usage: ab_variants.py <config> <rounds> <rows_stride> name=path[,ENV=VAL...] ...
 (environment overrides are applied around each variant's render calls;
-AB_ENGINE=wavefront|megakernel|kdtree picks the engine of every variant)"""
+AB_ENGINE=wavefront|megakernel|kdtree picks the engine of every variant, ENGINE=... in a
+variant's list that variant's)"""
 import os
 import sys
 
@@ -22,6 +23,7 @@ for a in sys.argv[4:]:
     parts = rest.split(',')
     variants.append((name, parts[0]))
     envs[name] = dict(p.split('=', 1) for p in parts[1:])
+engines = {n: envs[n].pop('ENGINE', engine) for n, _ in variants}   # per-variant engine: name=path,ENGINE=wavefront
 
 
 def with_env(name, fn):
@@ -42,13 +44,13 @@ ctxs = {}
 for name, path in variants:
     c = Context(0, lib_path=path)
     with_env(name, lambda: c.upload(sc))
-    with_env(name, lambda: c.render(it, row=(8, stride, 0), engine=engine))   # warm up
+    with_env(name, lambda: c.render(it, row=(8, stride, 0), engine=engines[name]))   # warm up
     ctxs[name] = c
 res = {n: [] for n, _ in variants}
 films = {}
 for r in range(rounds):
     for name, _ in variants:
-        film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0), engine=engine))
+        film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0), engine=engines[name]))
         films.setdefault(name, film)
         res[name].append(st['samples'] / st['kernel_ms'] / 1e3)
 first = variants[0][0]

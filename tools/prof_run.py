@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Profiling driver: renders a config through libmtsgpu (no torch) for rocprofv3.
-usage: prof_run.py [config] [frames] [rows_stride]"""
+usage: prof_run.py [config] [frames] [rows_stride] [engine]"""
 import os
 import sys
 
@@ -15,10 +15,11 @@ from mitsuba_amd.integrator import Context  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else 'C2'
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 stride = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+engine = sys.argv[4] if len(sys.argv) > 4 else None
 sc, it = scenes.build(cfg, rfilter='box')
 ctx = Context(0)
 ctx.upload(sc)
 print('scene', ctx.scene_info())
 for f in range(frames):
-    _, _, st = ctx.render(it, row=(8, stride, 0))
+    _, _, st = ctx.render(it, row=(8, stride, 0), engine=engine)
     print('frame', f, 'kernel_ms %.2f' % st['kernel_ms'], 'Msamples/s %.1f' % (st['samples'] / st['kernel_ms'] / 1e3))
