@@ -379,13 +379,14 @@ int mtsgpu_debug_env_tables(const mtsgpu_scene_desc *scene, float *params, uint1
 /* ---- device groups: one render over several GPUs ------------------------
  * SURVEY.md 8(b)'s `mtsgpu_create(const int *devices, int n, ...)`: a group
  * holds one context per listed device (a device may be listed twice: two
- * contexts on one GPU).  mtsgpu_group_render shards the crop window's rows
- * over the members -- member k renders rows y with ((y - y0) / row_block) % n
- * == k (row_block = params->row_block, 8 if 0), the interleaved tiles of
- * BlockedImageProcess (src/librender/imageproc.cpp:28-80) -- one host thread
+ * contexts on one GPU).  mtsgpu_group_render shards the crop window's 8x8
+ * tiles over the members -- member k renders the tiles t with t % n == k
+ * (MTSGPU_FLAG_TILE_SHARD, the multi-GPU bench's decomposition; the
+ * interleaved blocks of BlockedImageProcess, src/librender/imageproc.cpp:28-80,
+ * params->row_block is ignored) -- one host thread
  * per member, each into its own HBM film, and merges the films on the first
  * member's device (peer copies over xGMI, then dst += src in member order:
- * renderproc.cpp:142-149's Film::put sum; disjoint rows make it exact for the
+ * renderproc.cpp:142-149's Film::put sum; disjoint tiles make it exact for the
  * box filter).  params->row_stride must be 0 or 1 (the group owns the
  * sharding).  The SFMT replay samplers render on the first member alone (their
  * streams follow one block order).  Stats are summed, kernel_ms is the
@@ -401,6 +402,11 @@ int mtsgpu_group_render(mtsgpu_group *group, const mtsgpu_render_params *params,
  * (`film_device`, (W+2b)(H+2b)x5 floats). */
 int mtsgpu_group_render_device(mtsgpu_group *group, const mtsgpu_render_params *params, float *film_device,
                                mtsgpu_stats *stats);
+/* Host-only (no device): member k's render params in an n-member group render
+ * (the tile decomposition above), and the number of window pixels a render
+ * with the given params covers (the kernels' item -> pixel rule). */
+int mtsgpu_group_member_params(const mtsgpu_render_params *params, int n, int k, mtsgpu_render_params *out);
+uint64_t mtsgpu_render_pixels(const mtsgpu_render_params *params);
 /* Member k's context (borrowed; for develop / trace_rays on one device). */
 mtsgpu_ctx *mtsgpu_group_member(mtsgpu_group *group, int k);
 const char *mtsgpu_group_last_error(mtsgpu_group *group);

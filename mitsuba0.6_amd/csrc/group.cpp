@@ -3,7 +3,7 @@
 // over 32x32 blocks handed to worker threads and sums their ImageBlocks into
 // the film (BlockedImageProcess, src/librender/imageproc.cpp:28-80;
 // BlockedRenderProcess::processResult -> Film::put, renderproc.cpp:142-149).
-// Here each GPU is a worker with a fixed share of interleaved row blocks; it
+// Here each GPU is a worker with a fixed share of interleaved 8x8 tiles; it
 // renders them into a film of its own in HBM, and the films are merged on the
 // first member's device: a peer copy over xGMI, then dst += src, in member
 // order, so the merged film does not depend on which member finished first.
@@ -88,6 +88,40 @@ void add_stats(mtsgpu_stats &a, const mtsgpu_stats &b) {
 
 extern "C" {
 
+// member k's share of an n-member render: the bench's decomposition
+// (MTSGPU_FLAG_TILE_SHARD), the window's 8x8 tiles t with t % n == k, so the
+// members' pixel counts differ by at most one tile (the reference deals its
+// 32x32 blocks to workers: BlockedImageProcess, imageproc.cpp:28-80)
+int mtsgpu_group_member_params(const mtsgpu_render_params *params, int n, int k, mtsgpu_render_params *out) {
+    if (!params || !out || n <= 0 || k < 0 || k >= n) return MTSGPU_EINVAL;
+    *out = *params;
+    out->flags |= MTSGPU_FLAG_TILE_SHARD;
+    out->row_block = 8;
+    out->row_stride = (uint32_t)n;
+    out->row_phase = (uint32_t)k;
+    return MTSGPU_OK;
+}
+
+// the pixels of the crop window a render with these params covers: the
+// kernels' item -> pixel rule (dpath.h pixel_of) counted on the host
+uint64_t mtsgpu_render_pixels(const mtsgpu_render_params *P) {
+    if (!P || P->width == 0 || P->height == 0) return 0;
+    const uint64_t stride = P->row_stride ? P->row_stride : 1, phase = P->row_phase % stride;
+    const uint64_t tx = (P->width + 7) / 8, ty = (P->height + 7) / 8;
+    uint64_t n = 0;
+    if (P->flags & MTSGPU_FLAG_TILE_SHARD) {
+        for (uint64_t t = phase; t < tx * ty; t += stride) {
+            const uint64_t x0 = (t % tx) * 8, y0 = (t / tx) * 8;
+            n += std::min<uint64_t>(8, P->width - x0) * std::min<uint64_t>(8, P->height - y0);
+        }
+        return n;
+    }
+    const uint64_t rb = P->row_block ? P->row_block : 1;
+    for (uint64_t y = 0; y < P->height; ++y)
+        if ((y / rb) % stride == phase) n += P->width;
+    return n;
+}
+
 int mtsgpu_group_create(const int *devices, int n, mtsgpu_group **out) {
     if (!out) return MTSGPU_EINVAL;
     *out = nullptr;
@@ -170,10 +204,8 @@ int mtsgpu_group_render_device(mtsgpu_group *g, const mtsgpu_render_params *para
             hipError_t e = hipSetDevice(M.device);
             if (e == hipSuccess && k > 0) e = ensure(M.film, M.film_bytes, bytes);
             if (e != hipSuccess) { M.rc = MTSGPU_EHIP; M.err = std::string("member film: ") + hipGetErrorString(e); return; }
-            mtsgpu_render_params P = *params;
-            P.row_block = params->row_block ? params->row_block : 8;
-            P.row_stride = (uint32_t)n;
-            P.row_phase = (uint32_t)k;
+            mtsgpu_render_params P;
+            mtsgpu_group_member_params(params, n, k, &P);
             M.rc = mtsgpu_render_device(M.ctx, &P, k == 0 ? film_device : M.film, nullptr, &M.stats);
             if (M.rc != MTSGPU_OK) M.err = mtsgpu_last_error(M.ctx);
         });

@@ -31,7 +31,7 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
            'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm',
-           'mtsgpu_bvh_host']
+           'mtsgpu_bvh_host', 'mtsgpu_group_member_params', 'mtsgpu_render_pixels']
 
 _lib = None
 
@@ -56,6 +56,9 @@ def load_library(path=None):
     L.mtsgpu_create.argtypes = [C.c_int, P(C.c_void_p)]
     L.mtsgpu_upload_scene.argtypes = [C.c_void_p, P(abi.SceneDesc)]
     L.mtsgpu_film_border.argtypes = [C.c_int32, C.c_float]
+    L.mtsgpu_group_member_params.argtypes = [P(abi.RenderParams), C.c_int, C.c_int, P(abi.RenderParams)]
+    L.mtsgpu_render_pixels.argtypes = [P(abi.RenderParams)]
+    L.mtsgpu_render_pixels.restype = C.c_uint64
     L.mtsgpu_render.argtypes = [C.c_void_p, P(abi.RenderParams), P(C.c_float), P(C.c_float), P(abi.Stats)]
     L.mtsgpu_render_device.argtypes = [C.c_void_p, P(abi.RenderParams), C.c_void_p, C.c_void_p, P(abi.Stats)]
     L.mtsgpu_last_error.argtypes = [C.c_void_p]
@@ -324,7 +327,7 @@ class Context:
 
 class DeviceGroup:
     """One render over several GPUs of this node (mtsgpu_group_*): the library
-    shards the rows over the devices, one host thread each, and merges the films
+    shards the 8x8 tiles over the devices, one host thread each, and merges the films
     on the first device over xGMI (include/mtsgpu.h).  A device may be listed
     twice (two contexts on one GPU)."""
 
