@@ -603,7 +603,11 @@ struct Builder {
     const int nbins = env_int("MTSGPU_SAH_BINS", 128, 4, 1024);
     const float ci = env_float("MTSGPU_SAH_CI", 1.0f);
     const uint32_t leafMax = (uint32_t)env_int("MTSGPU_LEAF_MAX", MTSG_LEAF_MAX, 1, 15);
-    explicit Builder(std::vector<BuildPrim> &p, std::vector<MtsgNode> &n) : prims(p), nodes(n) {}
+    // the binned SAH's scratch, sized once and reused by every build() call
+    std::vector<BBox> bb, lb;
+    std::vector<uint32_t> bc, lc;
+    explicit Builder(std::vector<BuildPrim> &p, std::vector<MtsgNode> &n)
+        : prims(p), nodes(n), bb(nbins), lb(nbins), bc(nbins), lc(nbins) {}
 
     void inflate(BBox &b) const {
         for (int a = 0; a < 3; ++a) {
@@ -631,8 +635,6 @@ struct Builder {
         float bestCost = FLT_MAX; int bestAxis = -1, bestSplit = -1;
         const BBox nb = bounds(first, count);
         const float leafCost = ci * (float)count;
-        std::vector<BBox> bb(NB), lb(NB);
-        std::vector<uint32_t> bc(NB), lc(NB);
         for (int axis = 0; axis < 3; ++axis) {
             const float ext = cb.hi[axis] - cb.lo[axis];
             if (!(ext > 0)) continue;
