@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""bench.py -- Msamples/s of the MI355X `path` integrator on BASELINE config C2.
+"""bench.py -- Msamples/s of the MI355X `path` integrator on BASELINE config C2,
+and on C3 (matpreview, BASELINE's second north-star scene) in the same run as
+the line's `secondary` block.
 
 Workload (BASELINE.json configs[1]): Cornell box, 1280x720, 512 spp, sobol,
 path maxDepth=-1 rrDepth=5, box filter.  One step = one full frame
@@ -58,6 +60,9 @@ def parse_args(argv=None):
     ap.add_argument('--save-film', default=None, help='rank 0 writes the reduced film (.npy) after the last step')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
+    ap.add_argument('--secondary', default='C3',
+                    help="second workload timed in the same run and emitted as the line's `secondary` block "
+                         "(BASELINE's north star names Cornell box and matpreview); 'none' to skip")
     return ap.parse_args(argv)
 
 
@@ -107,6 +112,22 @@ def algorithmic_bytes_per_sample(st, scene_prims, num_emitters):
     return b / n
 
 
+def lib_sha256(path=None):
+    """sha256 of the libmtsgpu.so this run loads: the build a profile was taken on."""
+    import hashlib
+    if path is None:
+        sys.path.insert(0, REPO)
+        from pkgimport import mitsuba_amd
+        mitsuba_amd()
+        from mitsuba_amd.integrator import LIB_PATH
+        path = LIB_PATH
+    h = hashlib.sha256()
+    with open(path, 'rb') as f:
+        for chunk in iter(lambda: f.read(1 << 20), b''):
+            h.update(chunk)
+    return h.hexdigest()
+
+
 def measured_profile(kind, cfg):
     """The newest committed summary profiles/<round>_<kind>_<cfg>.json, written
     by tools/traffic_summary.py (traffic: HBM bytes per launch and per sample from
@@ -122,7 +143,7 @@ def measured_profile(kind, cfg):
     return t
 
 
-def roofline_line(bps, launch_samples, kernel_s, cfg):
+def roofline_line(bps, launch_samples, kernel_s, cfg, lib_hash=None):
     """The dominant kernel's roofline, from the live kernel time of this run and
     per-sample work measured once per build by rocprofv3 (profiles/<round>_*):
       hbm   -- measured HBM bytes per sample (separate FETCH_SIZE / WRITE_SIZE
@@ -140,6 +161,15 @@ def roofline_line(bps, launch_samples, kernel_s, cfg):
     and so is the SURVEY.md 8(d) no-reuse byte model (`hbm_model`)."""
     traffic = measured_profile('traffic', cfg)
     valu = measured_profile('valu', cfg)
+    # a per-sample profile only describes the build it was taken on (tools/prof_round.sh
+    # stamps each with the library's sha256): another build's profile gives no `frac`
+    stale = []
+    for name, prof in (('traffic', traffic), ('valu', valu)):
+        if prof is not None and prof.get('lib_sha256') != lib_hash:
+            stale.append('%s (%s, built from %s)' % (prof['source'], name, (prof.get('lib_sha256') or 'no stamp')[:12]))
+    if stale:
+        traffic = traffic if traffic and traffic.get('lib_sha256') == lib_hash else None
+        valu = valu if valu and valu.get('lib_sha256') == lib_hash else None
     model = {'achieved': round(bps * launch_samples / kernel_s / 1e9, 2), 'peak': HBM_PEAK_GBPS, 'unit': 'GB/s',
              'frac': round(bps * launch_samples / kernel_s / 1e9 / HBM_PEAK_GBPS, 5),
              'algorithmic_bytes_per_sample': round(bps, 1),
@@ -163,14 +193,23 @@ def roofline_line(bps, launch_samples, kernel_s, cfg):
               'clock_mhz': round(valu['clock_hz'] / 1e6, 1),
               'wait_frac_per_wave': round(valu['wait_frac_per_wave'], 4), 'source': valu['source']}
     cands = [(k, v) for k, v in (('hbm', hbm), ('valu', vl)) if v]
+    reason = None
     if not cands:
-        kind, top = 'hbm', model
+        # no measured profile of this build: the model's bytes are no measurement, so no frac
+        kind, top = 'hbm', dict(model, frac=None)
+        reason = ('no rocprofv3 profile of this build (libmtsgpu.so sha256 %s): %s' % (
+            (lib_hash or '?')[:12], '; '.join(stale) if stale else 'none committed'))
     else:
         kind, top = max(cands, key=lambda kv: kv[1]['frac'])
     line = {'bound': kind, 'achieved': top['achieved'], 'peak': top['peak'], 'unit': top['unit'], 'frac': top['frac'],
             'traffic': round(traffic['hbm_bytes_per_sample'] * launch_samples) if hbm else None,
             'traffic_unit': 'B per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)',
-            'hbm': hbm, 'valu': vl, 'hbm_model': model, 'kernel_ms_avg': round(kernel_s * 1e3, 3)}
+            'hbm': hbm, 'valu': vl, 'hbm_model': model, 'kernel_ms_avg': round(kernel_s * 1e3, 3),
+            'lib_sha256': lib_hash}
+    if reason:
+        line['frac_null_reason'] = reason
+    elif stale:
+        line['stale_profiles_ignored'] = stale
     return line
 
 
@@ -246,31 +285,23 @@ def cpu_baseline(scene, integ, threads):
             'cgroup_cpu_quota': quota}
 
 
-def build_scene(args):
+def build_scene(config, size=None):
     sys.path.insert(0, REPO)
     from pkgimport import mitsuba_amd
     mitsuba_amd()
     from mitsuba_amd import scenes
     kw = {'rfilter': 'box'}
-    if args.size:
-        w, h, spp = (int(v) for v in args.size.lower().split('x'))
+    if size:
+        w, h, spp = (int(v) for v in size.lower().split('x'))
         kw.update(width=w, height=h, spp=spp)
-    return scenes.build(args.config, **kw)
+    return scenes.build(config, **kw)
 
 
-def main():
-    args = parse_args()
-    rc = launch_ranks(args)
-    if rc is not None:
-        sys.exit(rc)
-
-    import torch  # loads the HIP runtime first; libmtsgpu shares it
-    import torch.distributed as dist
-
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    scene, integ = build_scene(args)
+def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
+    """Times args.steps frames of `config` (after args.warmup untimed ones) on
+    this rank's tiles, bracketed by barrier + synchronize; returns rank 0's
+    result dict (None on other ranks)."""
+    scene, integ = build_scene(config, args.size)
     from mitsuba_amd import film_border
     from mitsuba_amd.distributed import TileSharding
     W, H, spp = scene.sensor.width, scene.sensor.height, integ.sampleCount
@@ -280,12 +311,6 @@ def main():
     gpu = args.device == 'gpu'
 
     if gpu:
-        if not torch.cuda.is_available():
-            sys.exit('bench.py: no GPU visible (the HIP path has no CPU fallback; --device cpu-oracle is the '
-                     'launcher rehearsal)')
-        torch.cuda.set_device(local)
-        if world > 1:
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
         from mitsuba_amd.integrator import Context
         ctx = Context(torch.cuda.current_device())
         t_up = time.time()
@@ -308,8 +333,6 @@ def main():
         def sync():
             torch.cuda.synchronize()
     else:
-        if world > 1:
-            dist.init_process_group('gloo')
         import oracle.binding as ob
         upload_s = 0.0
         film = torch.zeros(((H + 2 * b) * (W + 2 * b) * 5,), dtype=torch.float32)
@@ -326,9 +349,6 @@ def main():
 
         def sync():
             pass
-
-    if world > 1:
-        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
 
     for _ in range(args.warmup):
         step()
@@ -364,46 +384,91 @@ def main():
     total_samples = float(s.item())
     frame_samples = W * H * spp
     assert int(total_samples) == frame_samples * args.steps, (total_samples, frame_samples)
-
-    if rank == 0:
-        if args.save_film:
-            import numpy as np
-            np.save(args.save_film, film.cpu().numpy().reshape(H + 2 * b, W + 2 * b, 5))
-        value = total_samples / elapsed_max / 1e6
-        roofline = None
-        cpu = None
-        if gpu:
-            # roofline: traversal counters from a bounded stats pass (1/16 of the rows), always
-            # through the BVH: tiny scenes' linear TriAccel scan (an implementation choice that
-            # reads every record from the scalar cache) must not inflate the workload's bytes
-            os.environ['MTSGPU_NO_SCAN'] = '1'
-            try:
-                _, _, sst = ctx.render(integ, row=(8, 16, 0), traversal_stats=True)
-            finally:
-                os.environ.pop('MTSGPU_NO_SCAN', None)
-            bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
-            avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
-            per_launch_samples = samples_rank / max(1, len(kernel_ms))
-            roofline = roofline_line(bps, per_launch_samples, avg_kernel_s, args.config)
-            if not args.no_cpu_baseline and world == 1:
-                cpu = cpu_baseline(scene, integ, args.cpu_threads)
-        metric = BASELINE_METRIC if args.config == 'C2' and not args.size else \
-            'Msamples/s (and s/frame) at %d spp, %dx%d' % (spp, W, H)
-        out = {
-            'metric': metric, 'value': round(value, 2),
-            'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': round(elapsed_max / args.steps * 1e3, 2), 'higher_is_better': True,
-            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
-            'config': {'workload': WORKLOADS.get(args.config, args.config), 'width': W, 'height': H, 'spp': spp,
+    if rank != 0:
+        return None
+    if args.save_film and config == args.config:
+        import numpy as np
+        np.save(args.save_film, film.cpu().numpy().reshape(H + 2 * b, W + 2 * b, 5))
+    value = total_samples / elapsed_max / 1e6
+    roofline = None
+    cpu = None
+    if gpu:
+        # roofline: traversal counters from a bounded stats pass (1/16 of the rows), always
+        # through the BVH: tiny scenes' linear TriAccel scan (an implementation choice that
+        # reads every record from the scalar cache) must not inflate the workload's bytes
+        os.environ['MTSGPU_NO_SCAN'] = '1'
+        try:
+            _, _, sst = ctx.render(integ, row=(8, 16, 0), traversal_stats=True)
+        finally:
+            os.environ.pop('MTSGPU_NO_SCAN', None)
+        bps = algorithmic_bytes_per_sample(sst, scene.num_triangles, len(scene.emitters))
+        avg_kernel_s = (sum(kernel_ms) / len(kernel_ms)) / 1e3
+        per_launch_samples = samples_rank / max(1, len(kernel_ms))
+        roofline = roofline_line(bps, per_launch_samples, avg_kernel_s, config, lib_hash)
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(scene, integ, args.cpu_threads)
+    return {'value': round(value, 2), 'ms_per_step': round(elapsed_max / args.steps * 1e3, 2),
+            'config': {'workload': WORKLOADS.get(config, config), 'width': W, 'height': H, 'spp': spp,
                        'samples_per_frame': frame_samples,
                        'parallelism': '8x8 tiles dealt over %d rank(s) + %s film reduce' % (
                            world, 'RCCL' if gpu else 'gloo'),
                        'world_size_reported': dist.get_world_size() if world > 1 else 1,
                        'reduce_ms_max': round(float(r.item()) * 1e3, 3),
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},
-            'roofline': roofline,
-            'cpu_baseline': cpu,
+            'roofline': roofline, 'cpu_baseline': cpu, 'spp': spp, 'W': W, 'H': H}
+
+
+def main():
+    args = parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+
+    import torch  # loads the HIP runtime first; libmtsgpu shares it
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    gpu = args.device == 'gpu'
+    lib_hash = None
+    if gpu:
+        if not torch.cuda.is_available():
+            sys.exit('bench.py: no GPU visible (the HIP path has no CPU fallback; --device cpu-oracle is the '
+                     'launcher rehearsal)')
+        torch.cuda.set_device(local)
+        if world > 1:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        lib_hash = lib_sha256()
+    elif world > 1:
+        dist.init_process_group('gloo')
+    if world > 1:
+        assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
+
+    main_res = run_workload(args.config, args, world, rank, local, dist, torch, lib_hash)
+    second = None
+    if args.secondary and args.secondary.lower() != 'none' and args.secondary != args.config and not args.size:
+        second = run_workload(args.secondary, args, world, rank, local, dist, torch, lib_hash)
+
+    if rank == 0:
+        m = main_res
+        metric = BASELINE_METRIC if args.config == 'C2' and not args.size else \
+            'Msamples/s (and s/frame) at %d spp, %dx%d' % (m['spp'], m['W'], m['H'])
+        out = {
+            'metric': metric, 'value': m['value'],
+            'unit': 'Msamples/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': m['ms_per_step'], 'higher_is_better': True,
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': m['config'],
+            'roofline': m['roofline'],
+            'cpu_baseline': m['cpu_baseline'],
         }
+        if second is not None:
+            out['secondary'] = {
+                'metric': 'Msamples/s (and s/frame) at %d spp, %dx%d' % (second['spp'], second['W'], second['H']),
+                'value': second['value'], 'unit': 'Msamples/s', 'ms_per_step': second['ms_per_step'],
+                'steps': args.steps, 'warmup': args.warmup, 'config': second['config'],
+                'roofline': second['roofline'], 'cpu_baseline': second['cpu_baseline']}
         if not gpu:
             out['device'] = 'cpu-oracle launcher rehearsal (not a GPU measurement)'
         print(json.dumps(out), flush=True)

@@ -10,6 +10,8 @@ OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
+# the build these profiles describe (bench.py only trusts profiles of the library it times)
+sha256sum mitsuba0.6_amd/_build/libmtsgpu.so | cut -d' ' -f1 > $OUT/lib.sha256
 for cfg in ${CONFIGS:-C2 C3 C4 C5}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench_$cfg -o bench --output-format csv \
       -- python3 $ROOT/bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_$cfg.log 2>&1

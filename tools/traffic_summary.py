@@ -21,6 +21,9 @@ import sys
 src, rnd = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(REPO, 'profiles')
+# sha256 of the libmtsgpu.so the passes ran (prof_round.sh): bench.py drops profiles of other builds
+_sha = os.path.join(src, 'lib.sha256')
+LIB_SHA = open(_sha).read().split()[0] if os.path.exists(_sha) else None
 
 
 def counter(path_glob, name):
@@ -41,7 +44,7 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
     if fetch and write:
         f, w = sum(fetch) / len(fetch), sum(write) / len(write)
         samples = SAMPLES.get(cfg)
-        out = {'config': cfg, 'kernel': 'path_kernel', 'launches': len(fetch), 'FETCH_SIZE_KiB': f, 'WRITE_SIZE_KiB': w,
+        out = {'config': cfg, 'kernel': 'path_kernel', 'lib_sha256': LIB_SHA, 'launches': len(fetch), 'FETCH_SIZE_KiB': f, 'WRITE_SIZE_KiB': w,
                'hbm_bytes_per_launch': 2 * f * 1024 + w * 1024,
                'hbm_bytes_per_launch_fetch_raw': f * 1024 + w * 1024,
                'hbm_bytes_per_sample': (2 * f * 1024 + w * 1024) / samples if samples else None,
@@ -79,7 +82,7 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
             if 'path_kernel' in r['Kernel_Name']:
                 durs.append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) * 1e-9)
     pass_samples = SAMPLES[cfg] // 4          # tools/prof_run.py <cfg> 1 4: a quarter of the rows
-    out = {'config': cfg, 'kernel': 'path_kernel', 'counters': c,
+    out = {'config': cfg, 'kernel': 'path_kernel', 'lib_sha256': LIB_SHA, 'counters': c,
            'valu_busy_per_simd': 4 * c['SQ_ACTIVE_INST_VALU'] / (SIMDS * c['GRBM_GUI_ACTIVE'] / XCDS),
            'valu_issue_frac_per_wave': c['SQ_ACTIVE_INST_VALU'] / wc,
            'any_issue_frac_per_wave': c['SQ_ACTIVE_INST_ANY'] / wc,
