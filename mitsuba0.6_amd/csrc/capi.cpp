@@ -773,23 +773,23 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         std::vector<uint32_t> &shapeKind = ctx->wf_kind_host;   // kept alive for the async upload
         wf_kinds(ctx->host, shapeKind, plan);
         const size_t R = MTSG_WF_REGIONS;
-        int minBpc = 1 << 30;
         for (int k = 0; k < MTSG_WK_KINDS; ++k) {
             if (!plan.kinds[k]) continue;
             int sb = 0, tb = 0;
             mtsg_wf_occupancy(L, k, plan.ggx[k], &sb, &tb);
             if (sb <= 0 || tb <= 0) return fail(ctx, MTSGPU_EHIP, "wavefront kernels do not fit the device");
-            plan.shadeGrid[k] = ctx->num_cus * sb;
-            plan.traceGrid = ctx->num_cus * tb;
-            minBpc = std::min(minBpc, sb);
         }
-        // path slots: about 2M (MTSGPU_WF_SLOTS), a multiple of the smallest shade grid's lanes
-        const uint64_t lanes = (uint64_t)ctx->num_cus * minBpc * BLOCK_THREADS;
+        // path slots: about 2M (MTSGPU_WF_SLOTS), whole blocks; the kernels run one queue
+        // entry per thread, so each grid covers the largest its queues can be (slots;
+        // 2 x slots for the trace kernel's two ray queues) and surplus blocks exit at once
         uint64_t target = (uint64_t)1 << 21;
         if (const char *env = std::getenv("MTSGPU_WF_SLOTS")) target = std::max<uint64_t>(1, std::strtoull(env, nullptr, 10));
         const uint64_t items = (uint64_t)std::min(chunk, P->spp) * L.num_pixels;
         target = std::min(target, items);
-        plan.slots = (uint32_t)(std::max<uint64_t>(1, (target + lanes - 1) / lanes) * lanes);
+        plan.slots = (uint32_t)((std::max<uint64_t>(1, target) + BLOCK_THREADS - 1) / BLOCK_THREADS * BLOCK_THREADS);
+        for (int k = 0; k < MTSG_WK_KINDS; ++k)
+            if (plan.kinds[k]) plan.shadeGrid[k] = (int)(plan.slots / BLOCK_THREADS);
+        plan.traceGrid = (int)(2 * (uint64_t)plan.slots / BLOCK_THREADS);
         const size_t slots = plan.slots, cap = slots;
         const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
         int partBlocks = plan.traceGrid;

@@ -165,6 +165,21 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t nb, uint32_t 
 }
 __device__ __forceinline__ uint32_t xcd_block(uint32_t xcds) { return xcd_remap(blockIdx.x, gridDim.x, xcds); }
 
+// The kernel's launch record (its first argument), re-read through a pointer
+// the compiler cannot follow.  A persistent loop otherwise has LICM hoist every
+// launch field and every product of them it finds invariant (camera rows,
+// scene pointers, sampler constants) out of the loop; they then stay live
+// across the whole bounce, as SGPRs spilled into VGPR lanes or as VGPR copies,
+// and push the shading state into scratch.  Re-read per iteration they are
+// s_loads from the kernarg segment (scalar cache) at their point of use.
+// Requires MtsgLaunch to be the kernel's first argument (kernarg offset 0).
+__device__ __forceinline__ const MtsgLaunch &launch_fresh() {
+    typedef __attribute__((address_space(4))) const MtsgLaunch KernargLaunch;
+    KernargLaunch *kp = (KernargLaunch *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *(const MtsgLaunch *)kp;
+}
+
 struct SamplerState {
     uint64_t sobolIndex;
     uint32_t sampleIndex;

@@ -36,7 +36,7 @@
 // The persistent megakernel: grid = CUs x resident blocks; every lane runs
 // PathShader steps with both traversals inline
 template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
-__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
+__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   // L: the first argument (launch_fresh)
     constexpr bool STATS = INSTR;
     constexpr bool ANA = (FEAT & MTSG_FEAT_ANA) != 0;
     constexpr bool HNODES = (FEAT & (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)) != 0;
@@ -68,6 +68,12 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {
 #endif
 
     while (true) {
+#ifndef MTSG_NO_FRESH_LAUNCH
+        // the launch record re-read per bounce instead of held (dpath.h launch_fresh)
+        const MtsgLaunch &L = launch_fresh();
+        const MtsgDeviceScene &S = L.scene;
+        const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
+#endif
         // ---- A: start the next sample
         while (!st.active && !done) {
             if (L.replay) {   // SFMT replay: this lane's unit, pixel after pixel, in order

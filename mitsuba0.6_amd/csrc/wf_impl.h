@@ -162,107 +162,111 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
 template <bool INSTR, int FEAT, int KIND, int HITK, int WAVES>
 __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave W, unsigned long long *part,
                                                          uint32_t queue) {
+    // one queue entry per thread: the grid covers the largest queue possible
+    // (all slots) and blocks past the queue's end leave at once.  No persistent
+    // loop, so nothing is carried or hoisted across items (a grid-stride loop
+    // kept the launch fields and the loop state live across the whole shading
+    // and spilled 170-560 VGPRs)
+    const uint32_t p = W.parity, region = blockIdx.x % WF_R;
+    QueueView Q;
+    Q.load(wf_cnt(W, p, 2 + queue));
+    const uint32_t n = W.seed ? W.slots : Q.total();
+    if (blockIdx.x * BLOCK >= n) return;   // block-uniform
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t red[BLOCK / 64 * 16];
     const MtsgDeviceScene &S = L.scene;
     const LdsView<false> V = stage_lds<false>(L, lds);   // ends with a barrier
     PathCounters c = {};
     const PathShader<INSTR, false, FEAT, KIND, HITK> sh{L, V.hs, V.SC, V.ycolTab, c};
-    const uint32_t p = W.parity, region = blockIdx.x % WF_R;
-    QueueView Q;
-    Q.load(wf_cnt(W, p, 2 + queue));
-    const uint32_t n = W.seed ? W.slots : Q.total();
     const uint32_t *cls = W.cls[p] + (size_t)queue * WF_R * W.cap;
     float4 *qray = W.ray[p], *sray = W.ray[p] + (size_t)2 * WF_R * W.cap;
     uint32_t *qslot = W.rslot[p], *sslot = W.rslot[p] + (size_t)WF_R * W.cap;
     uint32_t *missQ = W.cls[p ^ 1u];   // MTSG_WK_MISS = 0: the first kind queue
     uint32_t *cq = wf_cnt(W, p, 0) + region, *cs = wf_cnt(W, p, 1) + region;
     uint32_t *cm = wf_cnt(W, p ^ 1u, 2 + MTSG_WK_MISS) + region;
-    uint32_t live = 0;
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
-        const uint32_t s = W.seed ? i : cls[Q.pos(i, W.cap)];
-        PathState st;
-        uint32_t flags = 0;
-        st.active = false;
-        const bool was = W.seed ? false : wf_load(L, W, s, st, flags);
-        bool occluded = false, hit = false;
-        uint32_t slot = 0, prim = 0;
-        float hu = 0, hv = 0, ht = 0;
-        if (was) {
-            occluded = (flags & WF_SQUEUED) != 0 && W.occl[s] != 0;
-            if constexpr (HITK == 1) {
-                // the hit record's 4th word: the TriAccel slot with analytic shapes (fill_hit
-                // reads the slot's record), else the primitive index itself
-                const float4 h = W.hit[s];
-                const uint32_t w = __float_as_uint(h.w);
-                hit = true;
-                ht = h.x; hu = h.y; hv = h.z;
-                if ((FEAT & MTSG_FEAT_ANA) != 0) { slot = w; prim = S.tris[slot].prim; }
-                else prim = w;
-            }
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const bool valid = i < n;
+    const uint32_t s = !valid ? 0u : W.seed ? i : cls[Q.pos(i, W.cap)];
+    PathState st;
+    uint32_t flags = 0;
+    st.active = false;
+    const bool was = valid && !W.seed && wf_load(L, W, s, st, flags);
+    bool occluded = false, hit = false;
+    uint32_t slot = 0, prim = 0;
+    float hu = 0, hv = 0, ht = 0;
+    if (was) {
+        occluded = (flags & WF_SQUEUED) != 0 && W.occl[s] != 0;
+        if constexpr (HITK == 1) {
+            // the hit record's 4th word: the TriAccel slot with analytic shapes (fill_hit
+            // reads the slot's record), else the primitive index itself
+            const float4 h = W.hit[s];
+            const uint32_t w = __float_as_uint(h.w);
+            hit = true;
+            ht = h.x; hu = h.y; hv = h.z;
+            if ((FEAT & MTSG_FEAT_ANA) != 0) { slot = w; prim = S.tris[slot].prim; }
+            else prim = w;
         }
-        // a slot in a queue is live, or (first bounce) not started yet
-        bool done = false;
-        if (was && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
-            sh.finish(st);
-            // regeneration: slot s takes items s, s + slots, s + 2 slots, ...
-            uint64_t it = (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots;
-            while (true) {
-                if (it >= L.num_items) { done = true; break; }
-                if (sh.start(st, it)) break;
-                it += W.slots;   // padding pixel of a partial tile
-            }
-        } else if (!was) {
-            uint64_t it = s;
-            while (true) {
-                if (it >= L.num_items) { done = true; break; }
-                if (sh.start(st, it)) break;
-                it += W.slots;
-            }
-        }
-        // the next bounce's rays (the megakernel's intervals and counts)
-        float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, s0 = r0, s1 = r0;
-        bool ps = false, pr = false;
-        if (st.active && st.haveShadow) {
-            c.shadow++;
-            float mint, maxt;
-            if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
-                ps = true;
-                s0 = make_float4(st.P.its.p.x, st.P.its.p.y, st.P.its.p.z, mint);
-                s1 = make_float4(st.sd.x, st.sd.y, st.sd.z, maxt);
-            }
-        }
-        if (st.active && st.haveRay) {
-            c.rays++;
-            float mint, maxt;
-            if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
-                pr = true;
-                r0 = make_float4(st.ro.x, st.ro.y, st.ro.z, mint);
-                r1 = make_float4(st.rd.x, st.rd.y, st.rd.z, maxt);
-            }
-        }
-        const uint32_t spos = wave_append(cs, ps);
-        const uint32_t qpos = wave_append(cq, pr);
-        // a live path without a closest-hit ray (none sampled, or outside the scene
-        // box): its next shade step is a miss
-        const bool pm = st.active && !pr;
-        const uint32_t mpos = wave_append(cm, pm);
-        if (ps) {
-            const size_t k = (size_t)region * W.cap + spos;
-            sray[2 * k] = s0; sray[2 * k + 1] = s1; sslot[k] = s;
-        }
-        if (pr) {
-            const size_t k = (size_t)region * W.cap + qpos;
-            qray[2 * k] = r0; qray[2 * k + 1] = r1; qslot[k] = s;
-        }
-        if (pm) missQ[(size_t)region * W.cap + mpos] = s;
-        live += st.active ? 1u : 0u;
-        wf_store(W, s, st, (done ? WF_DONE : 0u) | (ps ? WF_SQUEUED : 0u));
     }
+    // a slot in a queue is live, or (first bounce) not started yet
+    bool done = false;
+    if (was && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
+        sh.finish(st);
+        // regeneration: slot s takes items s, s + slots, s + 2 slots, ...
+        uint64_t it = (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots;
+        while (true) {
+            if (it >= L.num_items) { done = true; break; }
+            if (sh.start(st, it)) break;
+            it += W.slots;   // padding pixel of a partial tile
+        }
+    } else if (valid && W.seed) {
+        uint64_t it = s;
+        while (true) {
+            if (it >= L.num_items) { done = true; break; }
+            if (sh.start(st, it)) break;
+            it += W.slots;
+        }
+    }
+    // the next bounce's rays (the megakernel's intervals and counts)
+    float4 r0 = make_float4(0, 0, 0, 0), r1 = r0, s0 = r0, s1 = r0;
+    bool ps = false, pr = false;
+    if (st.active && st.haveShadow) {
+        c.shadow++;
+        float mint, maxt;
+        if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
+            ps = true;
+            s0 = make_float4(st.P.its.p.x, st.P.its.p.y, st.P.its.p.z, mint);
+            s1 = make_float4(st.sd.x, st.sd.y, st.sd.z, maxt);
+        }
+    }
+    if (st.active && st.haveRay) {
+        c.rays++;
+        float mint, maxt;
+        if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
+            pr = true;
+            r0 = make_float4(st.ro.x, st.ro.y, st.ro.z, mint);
+            r1 = make_float4(st.rd.x, st.rd.y, st.rd.z, maxt);
+        }
+    }
+    const uint32_t spos = wave_append(cs, ps);
+    const uint32_t qpos = wave_append(cq, pr);
+    // a live path without a closest-hit ray (none sampled, or outside the scene
+    // box): its next shade step is a miss
+    const bool pm = st.active && !pr;
+    const uint32_t mpos = wave_append(cm, pm);
+    if (ps) {
+        const size_t k = (size_t)region * W.cap + spos;
+        sray[2 * k] = s0; sray[2 * k + 1] = s1; sslot[k] = s;
+    }
+    if (pr) {
+        const size_t k = (size_t)region * W.cap + qpos;
+        qray[2 * k] = r0; qray[2 * k + 1] = r1; qslot[k] = s;
+    }
+    if (pm) missQ[(size_t)region * W.cap + mpos] = s;
+    if (valid) wf_store(W, s, st, (done ? WF_DONE : 0u) | (ps ? WF_SQUEUED : 0u));
     uint32_t v[16] = {};
     v[0] = (uint32_t)c.samples; v[1] = (uint32_t)c.rays; v[2] = (uint32_t)c.shadow; v[3] = (uint32_t)c.len;
     v[6] = (uint32_t)c.err;
-    v[8] = live;   // (slot 8 is otherwise unused) live slots: one atomic per block
+    v[8] = st.active ? 1u : 0u;   // (slot 8 is otherwise unused) live slots: one atomic per block
     if (INSTR) { v[7] = (uint32_t)c.hits; v[9] = (uint32_t)c.nee; v[10] = (uint32_t)c.sobol; }
     block_counters(part, v, red, 8, W.live + p);
 }
@@ -290,6 +294,8 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
     Qc.load(wf_cnt(W, p, 0));
     Qs.load(wf_cnt(W, p, 1));
     const uint32_t nc = Qc.total(), n = nc + Qs.total();
+    // one ray per thread: the grid covers both queues' largest size (2 x slots);
+    // blocks past the end leave at once (no persistent loop: DESIGN.md 4)
     if (blockIdx.x * BLOCK >= n) return;   // block-uniform
     uint32_t stackBase = 0;
     if (SCENE_LDS && !L.scan && !KD) {
@@ -312,17 +318,21 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
     const float4 *rays = W.ray[p];
     const uint32_t *rslot = W.rslot[p];
     uint32_t *next = W.cls[p ^ 1u];
-    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) {
+    {
+        const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+        const bool valid = i < n;
         const bool shadow = i >= nc;
-        const size_t k = shadow ? (size_t)WF_R * W.cap + Qs.pos(i - nc, W.cap) : Qc.pos(i, W.cap);
-        const float4 a = rays[2 * k], b = rays[2 * k + 1];
-        const uint32_t s = rslot[k];
+        const size_t k = !valid ? 0 : shadow ? (size_t)WF_R * W.cap + Qs.pos(i - nc, W.cap) : Qc.pos(i, W.cap);
+        float4 a = make_float4(0, 0, 0, 1), b = make_float4(0, 0, 1, 0);
+        uint32_t s = 0;
+        if (valid) { a = rays[2 * k]; b = rays[2 * k + 1]; s = rslot[k]; }
         const f3 o = mk(a.x, a.y, a.z), d = mk(b.x, b.y, b.z);
         const float mint = a.w, maxt = b.w;
         uint32_t slot = 0;
         float hu = 0, hv = 0, ht = 0;
         uint32_t kind = MTSG_WK_KINDS;   // no append
-        if (shadow) {
+        if (!valid) {
+        } else if (shadow) {
             bool occ;
             if constexpr (KD) occ = kd_traverse<true>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot);
             else if (SCENE_LDS && L.scan)
@@ -377,7 +387,22 @@ __global__ __launch_bounds__(BLOCK, MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunc
 
 
 // waves per SIMD each shade kind is compiled for
-template <int KIND, int HITK> struct WfWaves { static constexpr int W = HITK == 2 ? 6 : KIND == BSDF_DIFFUSE ? 5 : KIND < 0 ? 3 : 4; };
+#ifndef MTSG_WF_WAVES_MISS
+#define MTSG_WF_WAVES_MISS 4
+#endif
+#ifndef MTSG_WF_WAVES_DIFF
+#define MTSG_WF_WAVES_DIFF 4
+#endif
+#ifndef MTSG_WF_WAVES_ROUGH
+#define MTSG_WF_WAVES_ROUGH 4
+#endif
+#ifndef MTSG_WF_WAVES_GEN
+#define MTSG_WF_WAVES_GEN 3
+#endif
+template <int KIND, int HITK> struct WfWaves {
+    static constexpr int W = HITK == 2 ? MTSG_WF_WAVES_MISS : KIND == BSDF_DIFFUSE ? MTSG_WF_WAVES_DIFF
+                           : KIND < 0 ? MTSG_WF_WAVES_GEN : MTSG_WF_WAVES_ROUGH;
+};
 
 // shade kernel of (FEAT, kind, GGX): FEAT = the scene's ENV / EXT / ANA bits
 template <bool INSTR, int FEAT, int WK, bool GGX>
