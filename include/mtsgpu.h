@@ -364,7 +364,10 @@ int mtsgpu_debug_libm(mtsgpu_ctx *ctx, int fn, const float *a, const float *b, f
                       uint32_t first);
 /* the 16 raw device counters of the last render (samples, rays, shadow rays,
    path lengths, node visits, TriAccel tests, dimension errors, hits, -, NEE
-   samples, Sobol HBM words, diagnostic section cycles 11-15) */
+   samples, Sobol HBM words, diagnostic section cycles 11-14), and in 15 the
+   kernel that ran: the megakernel's feature set (MTSG_FEAT_* bits of
+   csrc/layout.h, BSDF-set bits included) | waves/SIMD << 8 | scene in LDS << 12,
+   or 1 << 16 for the wavefront engine */
 int mtsgpu_debug_counters(mtsgpu_ctx *ctx, uint64_t *out16);
 /* n nextULong draws of the device's SFMT19937 (the SFMT replay samplers' generator)
    from Random(seed), or from the clone-th Random(&master) clone of it */

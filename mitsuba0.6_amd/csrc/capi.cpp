@@ -34,6 +34,7 @@ hipError_t mtsg_launch_trace_kd(const MtsgDeviceScene &S, const uint32_t *kdNode
                                 const MtsgTri *kdTris, const float *rays, uint32_t n, float *out, bool shadow,
                                 int numCUs, hipStream_t stream);
 int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU);
+int mtsg_path_variant(const MtsgLaunch &L);
 hipError_t mtsg_launch_wf_shade(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid, int wk,
                                 bool ggx, bool instr, hipStream_t s);
 hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part, int grid,
@@ -313,6 +314,12 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     hipError_t e;
     const uint32_t slots = plan.slots;
     const size_t cap = slots, R = MTSG_WF_REGIONS;
+    // the shade kernels' launch record: their blocks are short-lived (one queue entry
+    // per thread), so the Sobol dimensions they stage in LDS are a per-block cost;
+    // MTSGPU_WF_SHADE_LDS_DIMS caps them (0: every dimension from HBM/L2)
+    MtsgLaunch Ls = L;
+    if (const char *env = std::getenv("MTSGPU_WF_SHADE_LDS_DIMS"))
+        Ls.lds_dims = std::min<uint32_t>(Ls.lds_dims, (uint32_t)std::strtoul(env, nullptr, 10));
     MtsgWave W;
     std::memset(&W, 0, sizeof W);
     W.state = (float4 *)ctx->wf_state.p;
@@ -346,7 +353,7 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
         W.seed = it == 0 ? 1u : 0u;
         for (int k = 0; k < MTSG_WK_KINDS; ++k) {
             if (!plan.kinds[k] || (it == 0 && k != MTSG_WK_MISS)) continue;
-            if ((e = mtsg_launch_wf_shade(L, W, part, plan.shadeGrid[k], k, plan.ggx[k], instr, stream)) != hipSuccess)
+            if ((e = mtsg_launch_wf_shade(Ls, W, part, plan.shadeGrid[k], k, plan.ggx[k], instr, stream)) != hipSuccess)
                 return hip_fail(ctx, e, "wf_shade launch");
         }
         W.seed = 0;
@@ -842,6 +849,10 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         return hip_fail(ctx, e, "sample copy");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel");
     std::memcpy(ctx->last_counters, hc, sizeof hc);
+    // counter 15: which kernel ran -- the megakernel's FEAT | waves << 8 | scene_lds << 12,
+    // or 1 << 16 for the wavefront engine (tests and A/B logs read it)
+    ctx->last_counters[15] = wave ? (1ull << 16)
+                                  : (unsigned long long)(mtsg_path_variant(L) | (int)(L.waves << 8) | (int)(L.scene_lds << 12));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     if (stats) {

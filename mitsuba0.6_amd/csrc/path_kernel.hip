@@ -1,187 +1,8 @@
-// path_kernel.hip -- the persistent megakernel of Mitsuba 0.6's `path`
-// integrator (MIPathTracer::Li, src/integrators/path/path.cpp:119-294, inside
-// SamplingIntegrator::renderBlock, src/librender/integrator.cpp:140-188), the
-// `direct` integrator, batch ray queries and the film reduction.
-//
-//  * lane g of the persistent grid takes items g, g + lanes, g + 2 lanes, ...
-//    (static striding: no queue, no tail of long per-pixel tasks);
-//  * a lane whose path ends starts its next item immediately (regeneration);
-//  * each loop iteration traces the lane's pending shadow ray and its
-//    closest-hit ray, then shades (PathShader, dpath.h);
-//  * LDS holds the Sobol tables and the lane-strided traversal stacks (and
-//    the whole scene for small ones).
-#include "dpath.h"
+// path_kernel.hip -- the `direct` integrator, batch ray queries, the film
+// reduction and the launchers of Mitsuba 0.6's `path` integrator megakernel
+// (dmega.h; its variants are compiled per scene feature set in path_f.hip).
+#include "dmega.h"
 
-
-// diagnostic build (-DMTSG_MK_STAMPS): wave cycles per megakernel section,
-// summed into counters 11-14 (start, shadow trace, closest trace, shade) by
-// lane 0 of each wave.  s_memtime without draining the memory counters: a
-// section's loads are consumed inside it (traversal, shading), so the split is
-// close; read shares, not times (tools/mk_stamps.py)
-#ifdef MTSG_MK_STAMPS
-#define MK_STAMP(acc, t0)                                                        \
-    do {                                                                         \
-        unsigned long long t1_;                                                  \
-        __builtin_amdgcn_sched_barrier(0);                                       \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_)::"memory"); \
-        __builtin_amdgcn_sched_barrier(0);                                       \
-        acc += t1_ - t0;                                                         \
-        t0 = t1_;                                                                \
-    } while (0)
-#else
-#define MK_STAMP(acc, t0) (void)0
-#endif
-
-
-// The persistent megakernel: grid = CUs x resident blocks; every lane runs
-// PathShader steps with both traversals inline
-template <bool INSTR, bool SCENE_LDS, int FEAT, int WAVES>
-__global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   // L: the first argument (launch_fresh)
-    constexpr bool STATS = INSTR;
-    constexpr bool ANA = (FEAT & MTSG_FEAT_ANA) != 0;
-    constexpr bool HNODES = (FEAT & (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)) != 0;
-    extern __shared__ uint32_t lds[];
-    const MtsgDeviceScene &S = L.scene;
-    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
-    lds_node *ldsNodes = V.nodes;
-    lds_tri *ldsTris = V.tris;
-    lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
-    lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
-    PathCounters c = {};
-    const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
-
-    const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    uint64_t item = L.replay ? 0 : (uint64_t)xcd_block(L.xcds) * BLOCK + threadIdx.x;
-    bool done = false;
-    PathState st;
-    st.active = false;
-    st.px = st.py = 0;
-    st.j = st.pix = 0;
-    st.smp.sobolIndex = 0; st.smp.sampleIndex = 0; st.smp.dim = 0; st.smp.err = false;
-    st.sx = st.sy = 0;
-    st.haveRay = st.primary = st.haveShadow = false;
-    st.ro = mk(0, 0, 0); st.rd = mk(0, 0, 1); st.sd = mk(0, 0, 1);
-    st.rmint = st.rmaxt = st.smaxt = 0;
-#ifdef MTSG_MK_STAMPS
-    unsigned long long mkT[4] = {0, 0, 0, 0}, mkT0;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(mkT0)::"memory");
-#endif
-
-    while (true) {
-#ifndef MTSG_NO_FRESH_LAUNCH
-        // the launch record re-read per bounce instead of held (dpath.h launch_fresh)
-        const MtsgLaunch &L = launch_fresh();
-        const MtsgDeviceScene &S = L.scene;
-        const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
-#endif
-        // ---- A: start the next sample
-        while (!st.active && !done) {
-            if (L.replay) {   // SFMT replay: this lane's unit, pixel after pixel, in order
-                const uint32_t unit = blockIdx.x * BLOCK + threadIdx.x;
-                if (unit >= L.units) { done = true; break; }
-                const uint32_t k0 = L.unit_start[unit], n = L.unit_start[unit + 1] - k0;
-                if (item >= (uint64_t)n * L.chunk_spp) { done = true; break; }
-                const uint32_t k = k0 + (uint32_t)(item / L.chunk_spp), jj = (uint32_t)(item % L.chunk_spp);
-                ++item;
-                sh.start_xy(st, L.order[k], jj);
-                break;
-            }
-            if (item >= L.num_items) { done = true; break; }
-            const uint64_t it = item;
-            item += lanes;
-            sh.start(st, it);
-        }
-        if (__all(done)) break;
-        MK_STAMP(mkT[0], mkT0);
-
-        // ---- B: trace the shadow ray, then the closest-hit ray ---------------
-        bool occluded = false;
-        bool hit = false;
-        uint32_t slot = 0, prim = 0;
-        float hu = 0, hv = 0, ht = 0;
-        if (SCENE_LDS && L.scan) {
-            // tiny scene: both rays of the bounce in one pass (scan_pair); when
-            // both exist they leave the same point (ro was set to its.p)
-            float minS = INFINITY, maxS = -INFINITY, minC = INFINITY, maxC = -INFINITY;
-            bool okS = false, okC = false;
-            if (st.active && st.haveShadow) {
-                c.shadow++;
-                if (!is_zero(st.P.neeC)) okS = ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, minS, maxS);
-                if (!okS) { minS = INFINITY; maxS = -INFINITY; }
-            }
-            if (st.active && st.haveRay) {
-                c.rays++;
-                okC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
-                if (!okC) { minC = INFINITY; maxC = -INFINITY; }
-            }
-            if (__any(okS || okC))
-                scan_pair<STATS>(L, okC ? st.ro : st.P.its.p, st.sd, st.rd, minS, maxS, minC, maxC, occluded, hit,
-                                 prim, hu, hv, ht, c.tests);
-            hit = hit && okC;
-            occluded = occluded && okS;
-        } else {
-        if (st.active && st.haveShadow) {
-            c.shadow++;
-            float mint, maxt;
-            // a shadow ray whose estimate is zero cannot change Li: skip its traversal
-            if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
-                uint32_t sl; float a0, a1, a2;
-                if (SCENE_LDS)
-                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
-                                                          sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
-                else if constexpr (HNODES)
-                    occluded = traverse<true, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
-                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
-                                                          S.analytic);
-                else
-                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
-                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
-                                                          S.analytic);
-            }
-        }
-        // the NEE estimate is added now (as shade() would first thing), so it
-        // is not live across the closest-hit traversal
-        if (st.active && st.haveShadow) {
-            if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
-            st.haveShadow = false;
-        }
-        MK_STAMP(mkT[1], mkT0);
-        if (st.active && st.haveRay) {
-            c.rays++;
-            float mint, maxt;
-            if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
-                if (SCENE_LDS)
-                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
-                                                      hu, hv, ht, c.nodes, c.tests, S.analytic);
-                else if constexpr (HNODES)
-                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
-                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
-                                                      S.analytic);
-                else
-                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
-                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
-                                                      S.analytic);
-            }
-            if (hit) prim = SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
-        }
-        }
-        if (st.active && st.haveShadow) {   // scan_pair case
-            if (!occluded) st.P.L = add(st.P.L, st.P.neeC);
-            st.haveShadow = false;
-        }
-
-        MK_STAMP(mkT[2], mkT0);
-
-        // ---- C: shade -------------------------------------------------------
-        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
-        MK_STAMP(mkT[3], mkT0);
-    }
-    path_counters_flush<STATS>(L, c);
-#ifdef MTSG_MK_STAMPS
-    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
-        for (int k = 0; k < 4; ++k) atomicAdd(L.counters + 11 + k, mkT[k]);
-#endif
-}
 
 // ===========================================================================
 // The `direct` integrator: MIDirectIntegrator::Li (integrators/direct/direct.cpp:
@@ -721,56 +542,27 @@ size_t mtsg_path_lds_bytes(const MtsgLaunch &L) {
     return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16 + scene + ((size_t)L.stack_depth * 3 * BLOCK + 1) / 2) * 4;
 }
 
-// variants: small scenes (BVH in LDS) run 3 waves/SIMD with 32 Sobol dims in
-// LDS; large scenes run 4 waves/SIMD (128 VGPRs) when the traversal stacks fit
-// 4 blocks per CU, else 3 (capi.cpp picks L.waves and L.lds_dims)
-template <bool SCENE_LDS, int FEAT, int WAVES>
-static void launch_path_w(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
-    const size_t lds = mtsg_path_lds_bytes(L);
-    if (instr) hipLaunchKernelGGL((path_kernel<true, SCENE_LDS, FEAT, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
-    else hipLaunchKernelGGL((path_kernel<false, SCENE_LDS, FEAT, WAVES>), dim3(grid), dim3(BLOCK), lds, stream, L);
-}
+// the megakernel variants, one object per scene feature set (path_f.hip)
+#define MTSG_PATH_F_DECL(N)                                                                                  \
+    hipError_t mtsg_launch_path_f##N(const MtsgLaunch &L, int grid, bool instr, hipStream_t s, int bits);   \
+    int mtsg_path_occupancy_f##N(const MtsgLaunch &L, int bits, int *bpc);
+MTSG_PATH_F_DECL(0) MTSG_PATH_F_DECL(1) MTSG_PATH_F_DECL(2) MTSG_PATH_F_DECL(3) MTSG_PATH_F_DECL(6)
+MTSG_PATH_F_DECL(7)
+#undef MTSG_PATH_F_DECL
 
 int mtsg_path_features(const MtsgLaunch &L) {
     return (L.scene.env_emitter >= 0 ? MTSG_FEAT_ENV : 0) | ((L.ext || L.ana) ? MTSG_FEAT_EXT : 0) |
            (L.ana ? MTSG_FEAT_ANA : 0);
 }
 
-// the specialised BSDF sets compiled for the large-scene megakernel: the
-// scene's features (ENV / EXT / ANA) must match, and the set's restrictions
-// (GGX / NORD / NORC) must hold for the scene (L.bset); dbsdf.h BSet
-#define MTSG_SPEC_BITS (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)
-#define MTSG_SPEC_SETS(X)                                                                         \
-    X(MTSG_FEAT_ENV | MTSG_FEAT_GGX | MTSG_FEAT_NORD)             /* rough conductors, envmap  */ \
-    X(MTSG_FEAT_GGX | MTSG_FEAT_NORC)                             /* rough glass, area lights  */ \
-    X(MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC) /* plastic */
-static int spec_variant(const MtsgLaunch &L) {
+// The BSDF-set specialisation (dbsdf.h BSet) of large scenes: bit 0 = every
+// rough BSDF uses GGX, bit 1 = no roughdielectric, bit 2 = no roughconductor
+// (capi.cpp L.bset).  Every feature set has all 7 sets compiled (path_f.hip);
+// small scenes staged in LDS and the direct integrator take the generic kernel.
+static int spec_bits(const MtsgLaunch &L) {
     if (L.scene_lds || L.integrator == MTSG_INTEGRATOR_DIRECT) return 0;
-    const int f = mtsg_path_features(L);
-#define MTSG_SPEC_PICK(V) \
-    if (((V) & ~MTSG_SPEC_BITS) == f && ((V) & MTSG_SPEC_BITS & ~(int)L.bset) == 0) return (V);
-    MTSG_SPEC_SETS(MTSG_SPEC_PICK)
-#undef MTSG_SPEC_PICK
-    return 0;
+    return ((L.bset & MTSG_FEAT_GGX) ? 1 : 0) | ((L.bset & MTSG_FEAT_NORD) ? 2 : 0) | ((L.bset & MTSG_FEAT_NORC) ? 4 : 0);
 }
-
-template <int FEAT>
-static void launch_path(const MtsgLaunch &L, int grid, bool instr, hipStream_t stream) {
-    if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {   // large scenes only (spec_variant)
-        if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
-        else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
-    } else {
-        if (L.scene_lds) {
-            if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {   // no calls: room for 4 waves (capi.cpp)
-                if (L.waves == 4) { launch_path_w<true, FEAT, 4>(L, grid, instr, stream); return; }
-            }
-            launch_path_w<true, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
-        }
-        else if (L.waves == 4) launch_path_w<false, FEAT, 4>(L, grid, instr, stream);
-        else launch_path_w<false, FEAT, MTSG_WAVES_PER_EU>(L, grid, instr, stream);
-    }
-}
-
 
 template <int FEAT>
 static void launch_direct(const MtsgLaunch &L, int grid, hipStream_t stream) {
@@ -792,25 +584,15 @@ hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool st
         }
         return hipGetLastError();
     }
-    switch (spec_variant(L)) {
-#define MTSG_SPEC_CASE(V) \
-        case (V): launch_path<(V)>(L, grid, instr, stream); return hipGetLastError();
-        MTSG_SPEC_SETS(MTSG_SPEC_CASE)
-#undef MTSG_SPEC_CASE
-        default: break;
-    }
+    const int bits = spec_bits(L);
     switch (mtsg_path_features(L)) {
-        case 0:
-            if (L.all_diffuse) launch_path<MTSG_FEAT_DIFF>(L, grid, instr, stream);
-            else launch_path<0>(L, grid, instr, stream);
-            break;
-        case MTSG_FEAT_ENV: launch_path<MTSG_FEAT_ENV>(L, grid, instr, stream); break;
-        case MTSG_FEAT_EXT: launch_path<MTSG_FEAT_EXT>(L, grid, instr, stream); break;
-        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, grid, instr, stream); break;
-        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: launch_path<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, instr, stream); break;
-        default: launch_path<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, grid, instr, stream); break;
+        case 0: return mtsg_launch_path_f0(L, grid, instr, stream, bits);
+        case MTSG_FEAT_ENV: return mtsg_launch_path_f1(L, grid, instr, stream, bits);
+        case MTSG_FEAT_EXT: return mtsg_launch_path_f2(L, grid, instr, stream, bits);
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: return mtsg_launch_path_f3(L, grid, instr, stream, bits);
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: return mtsg_launch_path_f6(L, grid, instr, stream, bits);
+        default: return mtsg_launch_path_f7(L, grid, instr, stream, bits);
     }
-    return hipGetLastError();
 }
 
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream) {
@@ -863,42 +645,22 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
     return hipGetLastError();
 }
 
-template <bool SCENE_LDS, int FEAT, int WAVES>
-static int occupancy_w(const MtsgLaunch &L, int *bpc) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(bpc, path_kernel<false, SCENE_LDS, FEAT, WAVES>, BLOCK,
-                                                             mtsg_path_lds_bytes(L));
-}
-template <int FEAT>
-static int occupancy_e(const MtsgLaunch &L, int *bpc) {
-    if constexpr ((FEAT & MTSG_SPEC_BITS) != 0) {
-        if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
-        return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
-    } else {
-        if (L.scene_lds) {
-            if constexpr ((FEAT & MTSG_FEAT_DIFF) != 0) {
-                if (L.waves == 4) return occupancy_w<true, FEAT, 4>(L, bpc);
-            }
-            return occupancy_w<true, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
-        }
-        if (L.waves == 4) return occupancy_w<false, FEAT, 4>(L, bpc);
-        return occupancy_w<false, FEAT, MTSG_WAVES_PER_EU>(L, bpc);
-    }
-}
-int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
-    switch (spec_variant(L)) {
-#define MTSG_SPEC_CASE(V) \
-        case (V): return occupancy_e<(V)>(L, blocksPerCU);
-        MTSG_SPEC_SETS(MTSG_SPEC_CASE)
-#undef MTSG_SPEC_CASE
-        default: break;
-    }
-    switch (mtsg_path_features(L)) {
-        case 0: return L.all_diffuse ? occupancy_e<MTSG_FEAT_DIFF>(L, blocksPerCU) : occupancy_e<0>(L, blocksPerCU);
-        case MTSG_FEAT_ENV: return occupancy_e<MTSG_FEAT_ENV>(L, blocksPerCU);
-        case MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_EXT>(L, blocksPerCU);
-        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT>(L, blocksPerCU);
-        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: return occupancy_e<MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, blocksPerCU);
-        default: return occupancy_e<MTSG_FEAT_ENV | MTSG_FEAT_EXT | MTSG_FEAT_ANA>(L, blocksPerCU);
-    }
+// the FEAT template argument of the megakernel mtsg_launch_path runs for L
+// (reported through debug counter 15 so the tests can see which one ran)
+int mtsg_path_variant(const MtsgLaunch &L) {
+    const int bits = spec_bits(L), f = mtsg_path_features(L);
+    if (bits) return f | ((bits & 1) ? MTSG_FEAT_GGX : 0) | ((bits & 2) ? MTSG_FEAT_NORD : 0) | ((bits & 4) ? MTSG_FEAT_NORC : 0);
+    return (f == 0 && L.all_diffuse) ? (int)MTSG_FEAT_DIFF : f;
 }
 
+int mtsg_path_kernel_occupancy(const MtsgLaunch &L, int *blocksPerCU) {
+    const int bits = spec_bits(L);
+    switch (mtsg_path_features(L)) {
+        case 0: return mtsg_path_occupancy_f0(L, bits, blocksPerCU);
+        case MTSG_FEAT_ENV: return mtsg_path_occupancy_f1(L, bits, blocksPerCU);
+        case MTSG_FEAT_EXT: return mtsg_path_occupancy_f2(L, bits, blocksPerCU);
+        case MTSG_FEAT_ENV | MTSG_FEAT_EXT: return mtsg_path_occupancy_f3(L, bits, blocksPerCU);
+        case MTSG_FEAT_EXT | MTSG_FEAT_ANA: return mtsg_path_occupancy_f6(L, bits, blocksPerCU);
+        default: return mtsg_path_occupancy_f7(L, bits, blocksPerCU);
+    }
+}

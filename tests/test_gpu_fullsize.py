@@ -74,7 +74,44 @@ def test_bsdf_set_variant_equals_generic(gpu_ctx, cfg, monkeypatch):
     win = (0, 200, sc.sensor.width, 2)
     gpu_ctx.upload(sc)
     _, smp_s, st_s = gpu_ctx.render(it, window=win, samples=True)
+    assert gpu_ctx.debug_counters()[15] & (FEAT_GGX | FEAT_NORD | FEAT_NORC), 'no BSDF-set kernel ran'
     monkeypatch.setenv('MTSGPU_NO_BSDF_SETS', '1')
     _, smp_g, st_g = gpu_ctx.render(it, window=win, samples=True)
     _records_equal(smp_s, smp_g)
     assert st_s['rays'] == st_g['rays'] and st_s['shadow_rays'] == st_g['shadow_rays']
+
+
+FEAT_ENV, FEAT_EXT, FEAT_GGX, FEAT_NORD, FEAT_NORC = 1, 2, 16, 32, 64   # csrc/layout.h MTSG_FEAT_*
+
+
+def _beckmann_conductor_box():
+    """The Cornell box with Beckmann rough conductors on the two blocks and area
+    light only: no GGX, no roughdielectric -- none of the three benchmark sets."""
+    from mitsuba_amd.scene import BSDF
+    sc, it = scenes.build('C1', width=96, height=72, spp=8)
+    sc.bsdfs.append(BSDF('roughconductor', distribution='beckmann', alpha=0.3, material='Al'))
+    sc.bsdfs.append(BSDF('roughconductor', distribution='beckmann', alphaU=0.1, alphaV=0.35, material='Au'))
+    sc.meshes[5].bsdf = len(sc.bsdfs) - 2
+    sc.meshes[6].bsdf = len(sc.bsdfs) - 1
+    return sc, it
+
+
+def test_bsdf_set_beckmann_conductor_scene(gpu_ctx, oracle, monkeypatch):
+    """every (feature set x BSDF set) combination has a
+    specialised megakernel (path_f.hip), so a Beckmann roughconductor scene with
+    an area light runs the NORD set (no GGX bit, roughconductors present): its
+    records equal the generic kernel's and the oracle's bit for bit, and debug
+    counter 15 shows which kernel ran."""
+    monkeypatch.setenv('MTSGPU_NO_SCENE_LDS', '1')   # the sets serve large scenes (BVH in HBM)
+    sc, it = _beckmann_conductor_box()
+    gpu_ctx.upload(sc)
+    _, smp_s, st_s = gpu_ctx.render(it, samples=True)
+    ran = gpu_ctx.debug_counters()[15]
+    assert ran & 0xff == FEAT_NORD, hex(ran)
+    monkeypatch.setenv('MTSGPU_NO_BSDF_SETS', '1')
+    _, smp_g, st_g = gpu_ctx.render(it, samples=True)
+    assert gpu_ctx.debug_counters()[15] & 0xff == 0
+    _records_equal(smp_s, smp_g)
+    _, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0, threads=THREADS)
+    _records_equal(smp_s, smp_o)
+    assert st_s['rays'] == st_g['rays'] == st_o['rays']
