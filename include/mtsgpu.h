@@ -274,6 +274,39 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene);
  * `scene` and report the first error as the reference would raise it
  * (Log(EError) message into msg[cap]).  Returns MTSGPU_OK or the error code. */
 int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap);
+
+/* ---- the BSDF subtrees of a scene file (for the plugin shim) --------------
+ * Host-only.  Inside Mitsuba, twosided's nested BSDFs and every BSDF's
+ * textures are private children (src/bsdfs/twosided.cpp:198-210): a plugin
+ * cannot reach them, but the scene's source file can
+ * (Scene::getSourceFile, include/mitsuba/render/scene.h:1107).
+ * mtsgpu_xml_bsdf parses that file and returns the tree below the <bsdf> with
+ * the given id: node 0 is that BSDF, every other node a nested <bsdf> or
+ * <texture> (a <ref> child resolved by id) with its parent's index and the
+ * parameter name it fills ('name' attribute); each node owns num_props
+ * property elements from first_prop on (tag float/integer/boolean/string/
+ * rgb/srgb/spectrum/point/vector, name, value with $params replaced by the
+ * file's <default> values).  The shim rebuilds a Properties object per node.
+ * Returns MTSGPU_OK, MTSGPU_EINVAL (unreadable file, syntax error, unknown id;
+ * message in err), or MTSGPU_ENOMEM when a capacity is too small (the counts
+ * are still returned). */
+enum { MTSGPU_XML_BSDF = 0, MTSGPU_XML_TEXTURE = 1 };
+typedef struct {
+    int32_t kind;                   /* MTSGPU_XML_BSDF / MTSGPU_XML_TEXTURE        */
+    int32_t parent;                 /* parent node index, -1 for node 0            */
+    char plugin[32];                /* the 'type' attribute                        */
+    char name[64];                  /* parameter name under the parent ('' if none)*/
+    char id[64];                    /* the element's 'id' ('' if none)             */
+    int32_t first_prop, num_props;
+} mtsgpu_xml_node;
+typedef struct {
+    char tag[16];                   /* float, integer, boolean, string, rgb, ...   */
+    char name[64];
+    char value[128];
+} mtsgpu_xml_prop;
+int mtsgpu_xml_bsdf(const char *xml_path, const char *bsdf_id, mtsgpu_xml_node *nodes, int node_cap,
+                    mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props, char *err,
+                    size_t err_cap);
 /* Border size b of the film for the given filter parameters. */
 int mtsgpu_film_border(int32_t rfilter, float rfilter_param);
 /* Render the window into `film` (host memory, layout above).  `samples` may be

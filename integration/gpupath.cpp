@@ -27,8 +27,14 @@
  * the reference's behaviour.
  *
  * Multi-GPU: the 'devices' property ("0,1,2,3"; default: the current device)
- * selects a device group; mtsgpu_group_render shards the crop's row blocks
+ * selects a device group; mtsgpu_group_render shards the crop's 8x8 tiles
  * over the GPUs and merges the films over xGMI before Film::put.
+ *
+ * Nested (twosided) and textured BSDFs: the plugins keep them as private
+ * children, so the shim reads their element trees back from the scene file
+ * (Scene::getSourceFile, scene.h:1107) by the BSDF's id through
+ * mtsgpu_xml_bsdf, rebuilds a Properties object per element and converts it
+ * like any other BSDF.  Such a BSDF needs an id in the file.
  */
 #include <mitsuba/render/scene.h>
 #include <mitsuba/render/trimesh.h>
@@ -173,6 +179,7 @@ public:
         std::vector<mtsgpu_mesh_desc> meshes;
         std::vector<const Emitter *> emitterObjs;
         m_bsdfs.clear(); m_bsdfObjs.clear(); m_keep.clear();
+        m_sceneFile = scene->getSourceFile();    /* nested / textured BSDFs are read from it by id */
         std::vector<mtsgpu_emitter_desc> emitters;
         for (size_t i = 0; i < scene->getEmitters().size(); ++i) {   /* scene order = emitter PDF order */
             const Emitter *e = scene->getEmitters()[i].get();
@@ -288,7 +295,7 @@ public:
         }
         rp.x0 = (uint32_t) film->getCropOffset().x; rp.y0 = (uint32_t) film->getCropOffset().y;
         rp.width = (uint32_t) film->getCropSize().x; rp.height = (uint32_t) film->getCropSize().y;
-        rp.row_block = 8;                                /* the group's row-block interleave */
+        rp.row_block = 8;                                /* (the group deals 8x8 tiles itself) */
         rp.cancel = &m_cancelled;
 
         if (!m_group) {
@@ -338,38 +345,153 @@ public:
 
     MTS_DECLARE_CLASS()
 private:
-    /* Raise on textured parameters: a constant BSDF gives the same diffuse
-       reflectance and roughness at every surface position. */
-    void checkConstant(const BSDF *bsdf) {
+    /* Does the BSDF give the same diffuse reflectance and roughness at every
+       surface position (no textured parameter)? */
+    static bool isConstant(const BSDF *bsdf) {
         Intersection a, b;
         a.uv = Point2(0.173f, 0.291f); b.uv = Point2(0.618f, 0.854f);
         a.p = Point(0.0f); b.p = Point(1.0f);
         bool varies = bsdf->getDiffuseReflectance(a) != bsdf->getDiffuseReflectance(b);
         for (int c = 0; c < bsdf->getComponentCount(); ++c)
             varies |= bsdf->getRoughness(a, c) != bsdf->getRoughness(b, c);
-        if (varies)
-            Log(EError, "textured BSDF parameters: load the scene with mitsuba0.6_amd/xmlscene.py "
-                "(the plugin's textures are private children)");
+        return !varies;
     }
 
     /* Append a BSDF descriptor (de-duplicated by pointer); NULL -> -1 (the
-       library applies Shape::configure's default diffuse, shape.cpp:48-70). */
+       library applies Shape::configure's default diffuse, shape.cpp:48-70).
+       The plugins keep textures and nested BSDFs as private children, out of
+       reach of a plugin shim: twosided and textured BSDFs (detected by
+       evaluating the BSDF at two surface positions) are read back from the
+       scene file by their id (mtsgpu_xml_bsdf, Scene::getSourceFile). */
     int bsdfIndex(const BSDF *bsdf) {
         if (!bsdf) return -1;
         const int have = indexOf(m_bsdfObjs, bsdf);
         if (have >= 0) return have;
         const Properties &p = bsdf->getProperties();
+        if (p.getPluginName() != "twosided" && isConstant(bsdf))
+            return appendDesc(p, bsdf, NULL);
+        return xmlBsdf(bsdf);
+    }
+
+    int xmlBsdf(const BSDF *bsdf) {
+        const std::string id = bsdf->getID();
+        if (m_sceneFile.empty())
+            Log(EError, "BSDF \"%s\" has nested BSDFs or textures, which a plugin cannot read, and the scene "
+                "has no source file to read them from", id.c_str());
+        std::vector<mtsgpu_xml_node> nodes(64);
+        std::vector<mtsgpu_xml_prop> props(1024);
+        int nn = 0, np = 0;
+        char err[512] = "";
+        int rc = mtsgpu_xml_bsdf(m_sceneFile.string().c_str(), id.c_str(), nodes.data(), (int) nodes.size(),
+                                 props.data(), (int) props.size(), &nn, &np, err, sizeof err);
+        if (rc == MTSGPU_ENOMEM) {
+            nodes.resize((size_t) nn); props.resize((size_t) np);
+            rc = mtsgpu_xml_bsdf(m_sceneFile.string().c_str(), id.c_str(), nodes.data(), nn, props.data(), np,
+                                 &nn, &np, err, sizeof err);
+        }
+        if (rc != MTSGPU_OK)
+            Log(EError, "BSDF \"%s\" (nested BSDFs / textures are read from %s by the BSDF's id): %s",
+                id.c_str(), m_sceneFile.string().c_str(), err);
+        nodes.resize((size_t) nn);
+        return xmlNode(nodes, props, 0, bsdf);
+    }
+
+    /* one node of the file's tree (and its subtree) -> descriptors */
+    int xmlNode(const std::vector<mtsgpu_xml_node> &nodes, const std::vector<mtsgpu_xml_prop> &props, int k,
+                const BSDF *obj) {
+        Properties p(nodes[k].plugin);
+        for (int i = nodes[k].first_prop; i < nodes[k].first_prop + nodes[k].num_props; ++i)
+            setProperty(p, props[i]);
+        std::vector<std::pair<std::string, mtsgpu_texture_desc> > tex;
+        std::vector<int> nested;
+        for (int c = k + 1; c < (int) nodes.size(); ++c) {
+            if (nodes[c].parent != k) continue;
+            if (nodes[c].kind == MTSGPU_XML_TEXTURE) tex.push_back(std::make_pair(std::string(nodes[c].name),
+                                                                                  textureDesc(nodes[c], props)));
+            else nested.push_back(c);
+        }
+        if (p.getPluginName() == "twosided") {                   /* twosided.cpp:63-110, 193-205 */
+            if (nested.empty()) Log(EError, "A nested one-sided material is required!");
+            if (nested.size() > 2) Log(EError, "No more than two nested BRDFs can be added!");
+            mtsgpu_bsdf_desc d;
+            std::memset(&d, 0, sizeof d);
+            d.type = MTSGPU_BSDF_TWOSIDED;
+            d.nested[0] = d.nested[1] = -1;
+            const int idx = (int) m_bsdfs.size();
+            m_bsdfs.push_back(d);
+            m_bsdfObjs.push_back(obj);
+            for (size_t j = 0; j < nested.size(); ++j) {
+                const int ni = xmlNode(nodes, props, nested[j], NULL);
+                m_bsdfs[idx].nested[j] = ni;
+            }
+            return idx;
+        }
+        if (!nested.empty()) Log(EError, "%s: nested BSDFs are only supported inside twosided", nodes[k].plugin);
+        return appendDesc(p, obj, &tex);
+    }
+
+    /* a property element of the file as the scene loader would set it (scenehandler.cpp) */
+    static void setProperty(Properties &p, const mtsgpu_xml_prop &e) {
+        const std::string tag = e.tag, name = e.name, v = e.value;
+        std::vector<Float> f;
+        {
+            std::string t = v;
+            for (size_t i = 0; i < t.size(); ++i) if (t[i] == ',') t[i] = ' ';
+            std::istringstream is(t);
+            for (Float x; is >> x;) f.push_back(x);
+        }
+        if (tag == "float") p.setFloat(name, f.empty() ? 0 : f[0]);
+        else if (tag == "integer") p.setInteger(name, atoi(v.c_str()));
+        else if (tag == "boolean") p.setBoolean(name, v == "true");
+        else if (tag == "string") p.setString(name, v);
+        else if (tag == "point" && f.size() == 3) p.setPoint(name, Point(f[0], f[1], f[2]));
+        else if (tag == "vector" && f.size() == 3) p.setVector(name, Vector(f[0], f[1], f[2]));
+        else if (tag == "rgb" || tag == "srgb") {
+            Spectrum s;
+            if (tag == "srgb" && !v.empty() && v[0] == '#') {
+                const unsigned long c = strtoul(v.c_str() + 1, NULL, 16);
+                s.fromSRGB(((c >> 16) & 0xff) / 255.0f, ((c >> 8) & 0xff) / 255.0f, (c & 0xff) / 255.0f);
+            } else if (f.size() == 1 || f.size() == 3) {
+                const Float r = f[0], g = f.size() == 3 ? f[1] : f[0], b = f.size() == 3 ? f[2] : f[0];
+                if (tag == "srgb") s.fromSRGB(r, g, b); else s.fromLinearRGB(r, g, b);
+            } else {
+                SLog(EError, "could not parse <%s name=\"%s\" value=\"%s\">", e.tag, e.name, e.value);
+            }
+            p.setSpectrum(name, s);
+        } else if (tag == "spectrum" && f.size() == 1 && v.find(':') == std::string::npos) {
+            p.setSpectrum(name, Spectrum(f[0]));
+        } else {
+            SLog(EError, "<%s name=\"%s\" value=\"%s\"> in a nested or textured BSDF is not supported",
+                 e.tag, e.name, e.value);
+        }
+    }
+
+    /* checkerboard (textures/checkerboard.cpp) with Texture2D's uv transform (texture.cpp:81-95) */
+    static mtsgpu_texture_desc textureDesc(const mtsgpu_xml_node &n, const std::vector<mtsgpu_xml_prop> &props) {
+        if (std::string(n.plugin) != "checkerboard")
+            SLog(EError, "texture \"%s\" is not supported (checkerboard)", n.plugin);
+        Properties p(n.plugin);
+        for (int i = n.first_prop; i < n.first_prop + n.num_props; ++i) setProperty(p, props[i]);
+        mtsgpu_texture_desc t;
+        std::memset(&t, 0, sizeof t);
+        t.type = MTSGPU_TEX_CHECKERBOARD;
+        toRGB(p.getSpectrum("color0", Spectrum(.4f)), t.color0);
+        toRGB(p.getSpectrum("color1", Spectrum(.2f)), t.color1);
+        t.uoffset = (float) p.getFloat("uoffset", 0.0f);
+        t.voffset = (float) p.getFloat("voffset", 0.0f);
+        const Float uvscale = p.getFloat("uvscale", 1.0f);
+        t.uscale = (float) p.getFloat("uscale", uvscale);
+        t.vscale = (float) p.getFloat("vscale", uvscale);
+        return t;
+    }
+
+    /* a descriptor from a BSDF's Properties; `tex`: its texture children (name -> texture) */
+    int appendDesc(const Properties &p, const BSDF *bsdf,
+                   const std::vector<std::pair<std::string, mtsgpu_texture_desc> > *tex) {
         const std::string name = p.getPluginName();
         mtsgpu_bsdf_desc d;
         std::memset(&d, 0, sizeof d);
         d.nested[0] = d.nested[1] = -1;
-        /* The plugins keep textures and nested BSDFs as private children, out of
-           reach of a plugin shim: textured parameters (checkerboard) and twosided
-           render through the library's own XML loader (mitsuba0.6_amd/xmlscene.py).
-           Detect them by evaluating the BSDF at two surface positions. */
-        if (name == "twosided")
-            Log(EError, "twosided: load the scene with mitsuba0.6_amd/xmlscene.py (nested BSDFs are private to the plugin)");
-        checkConstant(bsdf);
         d.type = name == "diffuse" ? MTSGPU_BSDF_DIFFUSE : name == "roughconductor" ? MTSGPU_BSDF_ROUGHCONDUCTOR
                : name == "roughdielectric" ? MTSGPU_BSDF_ROUGHDIELECTRIC : name == "roughplastic" ? MTSGPU_BSDF_ROUGHPLASTIC
                : name == "conductor" ? MTSGPU_BSDF_CONDUCTOR : name == "dielectric" ? MTSGPU_BSDF_DIELECTRIC
@@ -410,6 +532,17 @@ private:
             d.rtrans_data = b.data();
             d.rtrans_bytes = b.size();
         }
+        for (size_t i = 0; tex && i < tex->size(); ++i) {      /* BSDF::addChild of a texture */
+            const std::string &pn = (*tex)[i].first;
+            if (pn == "alpha" && (d.type == MTSGPU_BSDF_ROUGHCONDUCTOR || d.type == MTSGPU_BSDF_ROUGHDIELECTRIC
+                                  || d.type == MTSGPU_BSDF_ROUGHPLASTIC))
+                d.alpha_tex = (*tex)[i].second;
+            else if ((pn == "reflectance" && d.type == MTSGPU_BSDF_DIFFUSE) ||
+                     (pn == "diffuseReflectance" && (d.type == MTSGPU_BSDF_ROUGHPLASTIC || d.type == MTSGPU_BSDF_PLASTIC)))
+                d.reflectance_tex = (*tex)[i].second;
+            else
+                Log(EError, "%s: unsupported texture parameter \"%s\"", name.c_str(), pn.c_str());
+        }
         m_bsdfs.push_back(d);
         m_bsdfObjs.push_back(bsdf);
         return (int) m_bsdfs.size() - 1;
@@ -421,7 +554,8 @@ private:
     mtsgpu_group *m_group = NULL;
     volatile int32_t m_cancelled = 0;
     std::vector<mtsgpu_bsdf_desc> m_bsdfs;
-    std::vector<const BSDF *> m_bsdfObjs;
+    std::vector<const BSDF *> m_bsdfObjs;          /* parallel to m_bsdfs (NULL: a nested BSDF) */
+    fs::path m_sceneFile;
     ref_vector<Bitmap> m_keep;
 #if GPU_INTEGRATOR == 2
     int m_emitterSamples = 1, m_bsdfSamples = 1;

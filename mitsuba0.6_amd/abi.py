@@ -122,3 +122,17 @@ def fptr(a):
 def uptr(a):
     assert a.dtype == np.uint32 and a.flags.c_contiguous
     return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+XML_BSDF, XML_TEXTURE = 0, 1
+
+
+class XmlNode(C.Structure):
+    """mtsgpu_xml_node (include/mtsgpu.h)."""
+    _fields_ = [('kind', C.c_int32), ('parent', C.c_int32), ('plugin', C.c_char * 32), ('name', C.c_char * 64),
+                ('id', C.c_char * 64), ('first_prop', C.c_int32), ('num_props', C.c_int32)]
+
+
+class XmlProp(C.Structure):
+    """mtsgpu_xml_prop (include/mtsgpu.h)."""
+    _fields_ = [('tag', C.c_char * 16), ('name', C.c_char * 64), ('value', C.c_char * 128)]

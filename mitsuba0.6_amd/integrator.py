@@ -31,7 +31,8 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_trace_rays', 'mtsgpu_group_create', 'mtsgpu_group_size', 'mtsgpu_group_upload_scene',
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
            'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm',
-           'mtsgpu_bvh_host', 'mtsgpu_group_member_params', 'mtsgpu_render_pixels']
+           'mtsgpu_bvh_host', 'mtsgpu_group_member_params', 'mtsgpu_render_pixels',
+           'mtsgpu_xml_bsdf']
 
 _lib = None
 
@@ -59,6 +60,8 @@ def load_library(path=None):
     L.mtsgpu_group_member_params.argtypes = [P(abi.RenderParams), C.c_int, C.c_int, P(abi.RenderParams)]
     L.mtsgpu_render_pixels.argtypes = [P(abi.RenderParams)]
     L.mtsgpu_render_pixels.restype = C.c_uint64
+    L.mtsgpu_xml_bsdf.argtypes = [C.c_char_p, C.c_char_p, P(abi.XmlNode), C.c_int, P(abi.XmlProp), C.c_int,
+                                  P(C.c_int), P(C.c_int), C.c_char_p, C.c_size_t]
     L.mtsgpu_render.argtypes = [C.c_void_p, P(abi.RenderParams), P(C.c_float), P(C.c_float), P(abi.Stats)]
     L.mtsgpu_render_device.argtypes = [C.c_void_p, P(abi.RenderParams), C.c_void_p, C.c_void_p, P(abi.Stats)]
     L.mtsgpu_last_error.argtypes = [C.c_void_p]

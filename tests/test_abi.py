@@ -34,7 +34,7 @@ STRUCTS = {'mtsgpu_bsdf_desc': abi.BsdfDesc, 'mtsgpu_emitter_desc': abi.EmitterD
            'mtsgpu_mesh_desc': abi.MeshDesc, 'mtsgpu_sensor_desc': abi.SensorDesc,
            'mtsgpu_scene_desc': abi.SceneDesc, 'mtsgpu_render_params': abi.RenderParams,
            'mtsgpu_stats': abi.Stats, 'mtsgpu_develop_params': abi.DevelopParams,
-           'mtsgpu_texture_desc': abi.TextureDesc}
+           'mtsgpu_texture_desc': abi.TextureDesc, 'mtsgpu_xml_node': abi.XmlNode, 'mtsgpu_xml_prop': abi.XmlProp}
 
 
 def test_struct_layout_matches_python_mirror(tmp_path):

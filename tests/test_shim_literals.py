@@ -94,8 +94,8 @@ def test_mts_class_arguments_are_registered():
 def test_plugin_name_literals_are_reference_plugins():
     src = _shim()
     plugins = _plugins()
-    lits = _compared_literals(src, r'\bname\b')
-    assert {'diffuse', 'roughconductor', 'roughdielectric', 'roughplastic', 'twosided'} <= set(lits)
+    lits = _compared_literals(src, r'\bname\b|getPluginName\(\)|std::string\(n\.plugin\)')
+    assert {'diffuse', 'roughconductor', 'roughdielectric', 'roughplastic', 'twosided', 'checkerboard'} <= set(lits)
     cpu = re.search(r'cpuPluginName\(\)\s*\{(.*?)\}', src, flags=re.S).group(1)
     lits += re.findall(r'"(\w+)"', cpu)
     bad = [n for n in lits if n not in plugins]
