@@ -159,21 +159,16 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
 // shade kernels: KIND = BSDF_* type of the queue's vertices (-1: any, the GEN
 // queue), HITK = 1 (every closest-hit ray hit) or 2 (the MISS queue)
 // ---------------------------------------------------------------------------
-template <bool INSTR, int FEAT, int KIND, int HITK, int WAVES>
-__global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave W, unsigned long long *part,
-                                                         uint32_t queue) {
-    // one queue entry per thread: the grid covers the largest queue possible
-    // (all slots) and blocks past the queue's end leave at once.  No persistent
-    // loop, so nothing is carried or hoisted across items (a grid-stride loop
-    // kept the launch fields and the loop state live across the whole shading
-    // and spilled 170-560 VGPRs)
+// One block of a shade kind's queue: queue entries kb * BLOCK + threadIdx of
+// queue `queue` (n entries, view Q), one per thread.  No persistent loop, so
+// nothing is carried or hoisted across items (a grid-stride loop kept the
+// launch fields and the loop state live across the whole shading and spilled
+// 170-560 VGPRs)
+template <bool INSTR, int FEAT, int KIND, int HITK>
+__device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWave &W, unsigned long long *part,
+                                               uint32_t queue, const QueueView &Q, uint32_t n, uint32_t kb,
+                                               uint32_t *lds, uint32_t *red) {
     const uint32_t p = W.parity, region = blockIdx.x % WF_R;
-    QueueView Q;
-    Q.load(wf_cnt(W, p, 2 + queue));
-    const uint32_t n = W.seed ? W.slots : Q.total();
-    if (blockIdx.x * BLOCK >= n) return;   // block-uniform
-    extern __shared__ uint32_t lds[];
-    __shared__ uint32_t red[BLOCK / 64 * 16];
     const MtsgDeviceScene &S = L.scene;
     const LdsView<false> V = stage_lds<false>(L, lds);   // ends with a barrier
     PathCounters c = {};
@@ -184,7 +179,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave 
     uint32_t *missQ = W.cls[p ^ 1u];   // MTSG_WK_MISS = 0: the first kind queue
     uint32_t *cq = wf_cnt(W, p, 0) + region, *cs = wf_cnt(W, p, 1) + region;
     uint32_t *cm = wf_cnt(W, p ^ 1u, 2 + MTSG_WK_MISS) + region;
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    const uint32_t i = kb * BLOCK + threadIdx.x;
     const bool valid = i < n;
     const uint32_t s = !valid ? 0u : W.seed ? i : cls[Q.pos(i, W.cap)];
     PathState st;
@@ -269,6 +264,20 @@ __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave 
     v[8] = st.active ? 1u : 0u;   // (slot 8 is otherwise unused) live slots: one atomic per block
     if (INSTR) { v[7] = (uint32_t)c.hits; v[9] = (uint32_t)c.nee; v[10] = (uint32_t)c.sobol; }
     block_counters(part, v, red, 8, W.live + p);
+}
+
+// a shade kind's kernel: the grid covers the largest queue possible (all
+// slots) and blocks past the queue's end leave at once
+template <bool INSTR, int FEAT, int KIND, int HITK, int WAVES>
+__global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave W, unsigned long long *part,
+                                                         uint32_t queue) {
+    QueueView Q;
+    Q.load(wf_cnt(W, W.parity, 2 + queue));
+    const uint32_t n = W.seed ? W.slots : Q.total();
+    if (blockIdx.x * BLOCK >= n) return;   // block-uniform
+    extern __shared__ uint32_t lds[];
+    __shared__ uint32_t red[BLOCK / 64 * 16];
+    wf_shade_block<INSTR, FEAT, KIND, HITK>(L, W, part, queue, Q, n, blockIdx.x, lds, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -428,6 +437,7 @@ __host__ auto wf_shade_fn_g(bool instr, bool ggx) {
 typedef void (*WfShadeFn)(MtsgLaunch, MtsgWave, unsigned long long *, uint32_t);
 template <int FEAT>
 __host__ WfShadeFn wf_shade_pick_f(int wk, bool instr, bool ggx) {
+
     switch (wk) {
         case MTSG_WK_MISS: return wf_shade_fn_g<FEAT, MTSG_WK_MISS>(instr, ggx);
         case MTSG_WK_DIFF: return wf_shade_fn_g<FEAT, MTSG_WK_DIFF>(instr, ggx);

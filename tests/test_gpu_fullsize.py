@@ -90,7 +90,7 @@ def _beckmann_conductor_box():
     from mitsuba_amd.scene import BSDF
     sc, it = scenes.build('C1', width=96, height=72, spp=8)
     sc.bsdfs.append(BSDF('roughconductor', distribution='beckmann', alpha=0.3, material='Al'))
-    sc.bsdfs.append(BSDF('roughconductor', distribution='beckmann', alphaU=0.1, alphaV=0.35, material='Au'))
+    sc.bsdfs.append(BSDF('roughconductor', distribution='beckmann', alpha=0.12, material='Au'))
     sc.meshes[5].bsdf = len(sc.bsdfs) - 2
     sc.meshes[6].bsdf = len(sc.bsdfs) - 1
     return sc, it
