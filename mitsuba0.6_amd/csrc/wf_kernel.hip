@@ -3,6 +3,8 @@
 // feature set in wf_shade_f.hip, one object per set, so they build in parallel)
 #include "wf_impl.h"
 
+#include <cstdlib>
+
 int mtsg_path_features(const MtsgLaunch &L);   // path_kernel.hip
 #define MTSG_WF_PICK_DECL(N) WfShadeFn mtsg_wf_pick_##N(int wk, bool instr, bool ggx);
 MTSG_WF_PICK_DECL(0) MTSG_WF_PICK_DECL(1) MTSG_WF_PICK_DECL(2) MTSG_WF_PICK_DECL(3) MTSG_WF_PICK_DECL(6)
@@ -21,6 +23,7 @@ __global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsign
 // host-side launchers (capi.cpp)
 // ---------------------------------------------------------------------------
 size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) { return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16) * 4; }
+bool mtsg_wf_trace_dynamic(const MtsgLaunch &L);
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
     if (L.kd_nodes) return 16;
     const bool scan = L.scene_lds && L.scan;
@@ -42,7 +45,26 @@ static WfShadeFn wf_shade_pick(const MtsgLaunch &L, int wk, bool instr, bool ggx
 }
 
 typedef void (*WfTraceFn)(MtsgLaunch, MtsgWave, unsigned long long *);
+// the dynamic-fetch trace kernel (opt-in, MTSGPU_WF_DYN=1) serves BVHs in
+// HBM; it lost to the one-ray-per-thread kernel (C3 604 -> 489, C4 172 -> 149,
+// C5 607 -> 497 Msamples/s, profiles/r04_ab_wf_dyn.log).  HN: the half-float
+// node copy (valid when the scene's extent allows it, as for the BSDF-set
+// megakernels)
+bool mtsg_wf_trace_dynamic(const MtsgLaunch &L) {
+    const char *e = std::getenv("MTSGPU_WF_DYN");
+    return !L.kd_nodes && !L.scene_lds && e && e[0] == '1';
+}
+static WfTraceFn wf_trace_dyn_pick(const MtsgLaunch &L, bool stats) {
+    const bool ana = L.ana != 0, hn = L.bset != 0;
+#define MTSG_DYN(ST, A, H) wf_trace_dyn<ST, A, H>
+    if (stats) return ana ? (hn ? MTSG_DYN(true, true, true) : MTSG_DYN(true, true, false))
+                          : (hn ? MTSG_DYN(true, false, true) : MTSG_DYN(true, false, false));
+    return ana ? (hn ? MTSG_DYN(false, true, true) : MTSG_DYN(false, true, false))
+               : (hn ? MTSG_DYN(false, false, true) : MTSG_DYN(false, false, false));
+#undef MTSG_DYN
+}
 static WfTraceFn wf_trace_pick(const MtsgLaunch &L, bool stats) {
+    if (mtsg_wf_trace_dynamic(L)) return wf_trace_dyn_pick(L, stats);
     const bool ana = L.ana != 0;
     if (L.kd_nodes) return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
     if (stats) {

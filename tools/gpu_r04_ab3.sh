@@ -1,0 +1,10 @@
+#!/bin/bash
+# r04: wavefront tests, then A/B: megakernel, wavefront with the single-shot
+# trace kernel, wavefront with the dynamic-fetch trace kernel (C3-C5)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export PYTHONUNBUFFERED=1
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_wavefront.py tests/test_gpu_kdtree.py > gpurun_out/r04_ab3_tests.log 2>&1 || exit 1
+L=mitsuba0.6_amd/_build/libmtsgpu.so
+for c in C3 C4 C5; do echo "== $c" >> gpurun_out/r04_ab3.log; timeout -k 10 240 python -u tools/ab_variants.py $c 3 4 mega=$L,ENGINE=megakernel wave_ss=$L,ENGINE=wavefront,MTSGPU_WF_DYN=0 wave_dyn=$L,ENGINE=wavefront >> gpurun_out/r04_ab3.log 2>&1 || exit 1; done
+bash tools/gpu_r04_wfpmc.sh
