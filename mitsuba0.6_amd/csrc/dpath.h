@@ -505,17 +505,38 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
 // d[a] * t — the same rounded product and sum the reference stores, so every
 // comparison sees the same floats.  The entry and exit points the descent
 // compares against are held in registers (only a push or a pop changes them),
-// so a descent step reads no stack memory; the stack itself lives in scratch.
-template <bool ANY>
+// so a descent step reads no stack memory.  LDSK = 0: the stack and the
+// mailbox live in scratch; LDSK > 0 (the wavefront engine's kd trace kernel):
+// the mailbox and the first LDSK stack entries live in LDS, lane-strided
+// (lmbox[slot * BLOCK], lstk[entry * BLOCK]), deeper entries in scratch.
+struct KdEnt { uint32_t node; float t; float split; uint32_t prev_axis; };
+typedef __attribute__((address_space(3))) vu4 lds_kdent;
+typedef __attribute__((address_space(3))) uint32_t lds_w32;
+template <bool ANY, int LDSK = 0>
 __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
                             const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
-                            float &bu, float &bv, uint32_t &bprim) {
-    struct Ent { uint32_t node; float t; float split; uint32_t prev_axis; };
+                            float &bu, float &bv, uint32_t &bprim, lds_kdent *lstk = nullptr,
+                            lds_w32 *lmbox = nullptr) {
+    typedef KdEnt Ent;
     constexpr uint32_t NONE = 0xffffffffu, NOAXIS = 3u;
-    Ent stack[48];
-    uint32_t mbox[8];
+    Ent stackS[48 - LDSK];
+    uint32_t mboxS[LDSK ? 1 : 8];
+    // entry i: LDS below LDSK, scratch above
+    auto ld = [&](uint32_t i) -> Ent {
+        if (LDSK && i < (uint32_t)LDSK) {
+            const vu4 v = lstk[i * BLOCK];
+            return Ent{v.x, __uint_as_float(v.y), __uint_as_float(v.z), v.w};
+        }
+        return stackS[i - LDSK];
+    };
+    auto st = [&](uint32_t i, const Ent &e) {
+        if (LDSK && i < (uint32_t)LDSK) lstk[i * BLOCK] = vu4{e.node, __float_as_uint(e.t), __float_as_uint(e.split), e.prev_axis};
+        else stackS[i - LDSK] = e;
+    };
+    auto mb = [&](uint32_t k) -> uint32_t { if constexpr (LDSK > 0) return lmbox[k * BLOCK]; else return mboxS[k]; };
+    auto mbset = [&](uint32_t k, uint32_t v) { if constexpr (LDSK > 0) lmbox[k * BLOCK] = v; else mboxS[k] = v; };
 #pragma unroll
-    for (int i = 0; i < 8; ++i) mbox[i] = 0xffffffffu;
+    for (int i = 0; i < 8; ++i) mbset(i, 0xffffffffu);
     const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
     // p[a] of an entry (t, split, eaxis): the stored point of sahkdtree3.h:239-244
     auto pt = [&](float t, float split, uint32_t eaxis, int a) -> float {
@@ -525,11 +546,8 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         return oa + da * t;
     };
     uint32_t enPt = 0, exPt = 1;
-    stack[0].t = mint;                                    // ray(mint)
-    stack[0].prev_axis = NOAXIS << 8;
-    stack[1].t = maxt;                                    // ray(maxt)
-    stack[1].prev_axis = NOAXIS << 8;
-    stack[1].node = NONE;
+    st(0, Ent{0u, mint, 0.0f, NOAXIS << 8});              // ray(mint)
+    st(1, Ent{NONE, maxt, 0.0f, NOAXIS << 8});            // ray(maxt)
     float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;
     uint32_t en_axis = NOAXIS, ex_axis = NOAXIS;
     bool found = false;
@@ -558,10 +576,7 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             const uint32_t tmp = exPt++;
             if (exPt == enPt) ++exPt;
             if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-            stack[exPt].prev_axis = tmp | ((uint32_t)axis << 8);
-            stack[exPt].t = distToSplit;
-            stack[exPt].split = split;
-            stack[exPt].node = farChild;
+            st(exPt, Ent{farChild, distToSplit, split, tmp | ((uint32_t)axis << 8)});
             ex_t = distToSplit;
             ex_split = split;
             ex_axis = (uint32_t)axis;
@@ -569,7 +584,7 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         }
         for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
             const uint32_t prim = indices[e];
-            if (mbox[prim & 7u] == prim) continue;   // the hashed mailbox (sahkdtree3.h:138-152)
+            if (mb(prim & 7u) == prim) continue;   // the hashed mailbox (sahkdtree3.h:138-152)
             const MtsgTri &tr = tris[prim];
             const uint32_t k = tr.k;
             float o_u, o_v, o_k, d_u, d_v, d_k;
@@ -590,16 +605,16 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
                     bt = t; bu = u; bv = v; bprim = prim;
                 }
             }
-            mbox[prim & 7u] = prim;
+            mbset(prim & 7u, prim);
         }
         if (ex_t > maxt) break;
         enPt = exPt;
         en_t = ex_t;
         en_split = ex_split;
         en_axis = ex_axis;
-        node = stack[exPt].node;
-        exPt = stack[enPt].prev_axis & 0xffu;
-        const Ent e = stack[exPt];
+        node = ld(exPt).node;
+        exPt = ld(enPt).prev_axis & 0xffu;
+        const Ent e = ld(exPt);
         ex_t = e.t;
         ex_split = e.split;
         ex_axis = e.prev_axis >> 8;

@@ -24,8 +24,15 @@ __global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsign
 // ---------------------------------------------------------------------------
 size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) { return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16) * 4; }
 bool mtsg_wf_trace_dynamic(const MtsgLaunch &L);
+// the kd trace kernel's mailbox + first stack entries in LDS (MTSGPU_KD_LDS=1):
+// C4 62.2 -> 65.0, C3 356.8 -> 330.2 Msamples/s (profiles/r04_ab_kd_lds.log), so
+// opt-in; the default keeps them in scratch
+static bool kd_lds() {
+    const char *e = std::getenv("MTSGPU_KD_LDS");
+    return e && e[0] == '1';
+}
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
-    if (L.kd_nodes) return 16;
+    if (L.kd_nodes) return kd_lds() ? (size_t)MTSG_WF_KD_LDSK * BLOCK * 16 + 8 * BLOCK * 4 : 16;
     const bool scan = L.scene_lds && L.scan;
     const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
     const size_t K = std::min<size_t>(L.stack_depth, MTSG_WF_LDS_STACK);
@@ -66,7 +73,11 @@ static WfTraceFn wf_trace_dyn_pick(const MtsgLaunch &L, bool stats) {
 static WfTraceFn wf_trace_pick(const MtsgLaunch &L, bool stats) {
     if (mtsg_wf_trace_dynamic(L)) return wf_trace_dyn_pick(L, stats);
     const bool ana = L.ana != 0;
-    if (L.kd_nodes) return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
+    if (L.kd_nodes) {
+        if (kd_lds()) return stats ? wf_trace<true, false, false, true, MTSG_WF_KD_LDSK>
+                                   : wf_trace<false, false, false, true, MTSG_WF_KD_LDSK>;
+        return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
+    }
     if (stats) {
         if (L.scene_lds) return ana ? wf_trace<true, true, true, false> : wf_trace<true, true, false, false>;
         return ana ? wf_trace<true, false, true, false> : wf_trace<true, false, false, false>;
