@@ -14,7 +14,7 @@ export TMPDIR=/tmp
 sha256sum mitsuba0.6_amd/_build/libmtsgpu.so | cut -d' ' -f1 > $OUT/lib.sha256
 for cfg in ${CONFIGS:-C2 C3 C4 C5}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/bench_$cfg -o bench --output-format csv \
-      -- python3 $ROOT/bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_$cfg.log 2>&1
+      -- python3 $ROOT/bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline --secondary none > $OUT/bench_$cfg.log 2>&1
   for ctr in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace -d $OUT/pmc_${cfg}_$ctr -o pmc --output-format csv \
         -- python3 $ROOT/tools/prof_run.py $cfg 1 1 > $OUT/pmc_${cfg}_$ctr.log 2>&1
