@@ -179,13 +179,18 @@ __device__ __forceinline__ BSample bsdf_sample_2s(const MtsgDeviceScene &S, GBsd
         rp_pre_for<(EXT ? (int)MTSG_FEAT_EXT : 0)>(bsdf, (glb_f32 *)S.rtrans, h.wi, h.u, h.v));
 }
 
-// direct_kernel's shadow rays: the any-hit traversal as a separate (not
-// inlined) function.  Inlined into direct_kernel's nested divergent loops at
-// -O3, hipcc (ROCm 7.2, gfx950) produced wrong occlusion answers for 15% of the
-// samples of the analytic-shape scene; the same source is exact at -O1, as a
-// call, with the NaN-aware (closest-hit) form of the sphere predicate, and
-// inlined into path_kernel / trace_kernel (DESIGN.md 4 has the bisection)
+// direct_kernel's shadow rays: the any-hit traversal.  Inlined into
+// direct_kernel's nested divergent loops at -O3, hipcc (ROCm 7.2, gfx950)
+// produced wrong occlusion answers for 15% of the samples of the analytic-shape
+// scene; the pass bisection pinned it to GVN's scalar PRE on that kernel
+// (DESIGN.md 4).  This translation unit is therefore compiled with
+// -mllvm -enable-pre=false (Makefile), and the traversal is inlined again;
+// -DMTSG_SHADOW_ANY_NOINLINE restores the round-2 workaround (a call)
+#ifdef MTSG_SHADOW_ANY_NOINLINE
 #define SHADOW_ANY_CALL __device__ __noinline__
+#else
+#define SHADOW_ANY_CALL __device__ __forceinline__
+#endif
 template <bool ANA, typename NodeT, typename TriT>
 SHADOW_ANY_CALL bool shadow_any(NodeT *nodes, TriT *tris, f3 o, f3 d, float mint, float maxt,
                                         lds_stk_n *stkN, lds_stk_d *stkD, unsigned long long &cN,
