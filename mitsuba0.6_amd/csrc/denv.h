@@ -14,6 +14,12 @@ typedef __attribute__((address_space(1))) const float glb_f32;
 typedef unsigned int env_u2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const env_u2 glb_u2;
 
+// the envmap NEE's sampleDirect / pdfDirect: out-of-line calls (MTSG_ENV_INLINE: inlined, an A/B knob)
+#ifdef MTSG_ENV_INLINE
+#define ENV_CALL __device__ __forceinline__
+#else
+#define ENV_CALL __device__ __noinline__
+#endif
 __device__ __forceinline__ float half_bits_to_float(uint32_t h) {
     return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
 }
@@ -261,7 +267,7 @@ __device__ __forceinline__ f3 env_sample_direct_impl(glb_env *E, f3 ref, float s
 }
 
 // internalPdfDirection (envmap.cpp:606-633), solid angle
-__device__ __noinline__ float env_pdf_direction(glb_env *E, f3 dw) {
+ENV_CALL float env_pdf_direction(glb_env *E, f3 dw) {
     const f3 d = env_to_local(E, dw);
     const float uvx = d_atan2(d.x, -d.z) * D_INV_TWOPI, uvy = d_acos(smin(1.0f, smax(-1.0f, d.y))) * D_INV_PI;
     if (!isfinite(uvx) || !isfinite(uvy)) return 0.0f;
@@ -279,7 +285,7 @@ __device__ __noinline__ float env_pdf_direction(glb_env *E, f3 dw) {
 }
 
 struct EnvSample { f3 value, d; float dist, pdf; };
-__device__ __noinline__ EnvSample env_sample_direct(glb_env *E, f3 ref, float sx, float sy) {
+ENV_CALL EnvSample env_sample_direct(glb_env *E, f3 ref, float sx, float sy) {
     EnvSample r;
     r.d = mk(0, 0, 1);
     r.dist = 0.0f;

@@ -74,6 +74,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         // the launch record re-read per bounce instead of held (dpath.h launch_fresh)
         const MtsgLaunch &L = launch_fresh();
         const MtsgDeviceScene &S = L.scene;
+#ifndef MTSG_NO_FRESH_VIEW
+        // the LDS / scene pointers re-derived from it as well (dpath.h lds_view):
+        // C2 +2.0%, C4 +3.8%, C5 +0.7%, C3 0 (profiles/r04_ab_fresh_view.log)
+        const LdsView<SCENE_LDS> V = lds_view<SCENE_LDS>(L, lds);
+        lds_node *ldsNodes = V.nodes;
+        lds_tri *ldsTris = V.tris;
+        lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
+        lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
+#endif
         const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 #endif
         // ---- A: start the next sample

@@ -1120,6 +1120,9 @@ struct LdsView {
 };
 
 template <bool SCENE_LDS>
+__device__ __forceinline__ LdsView<SCENE_LDS> lds_view(const MtsgLaunch &L, uint32_t *lds);
+
+template <bool SCENE_LDS>
 __device__ __forceinline__ LdsView<SCENE_LDS> stage_lds(const MtsgLaunch &L, uint32_t *lds) {
     const MtsgDeviceScene &S = L.scene;
     const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
@@ -1156,6 +1159,22 @@ __device__ __forceinline__ LdsView<SCENE_LDS> stage_lds(const MtsgLaunch &L, uin
         }
     }
     __syncthreads();
+    return lds_view<SCENE_LDS>(L, lds);
+}
+
+// the pointers into the staged LDS (and the scene buffers it mirrors), derived
+// from the launch record alone: the persistent megakernel re-derives them per
+// bounce from launch_fresh() instead of holding them live across it
+template <bool SCENE_LDS>
+__device__ __forceinline__ LdsView<SCENE_LDS> lds_view(const MtsgLaunch &L, uint32_t *lds) {
+    const MtsgDeviceScene &S = L.scene;
+    const uint32_t tabWords = L.lds_dims * L.nibbles * 16;
+    const uint32_t base2 = tabWords + 16 * 16;
+    uint32_t sceneWords = 0;
+    if (SCENE_LDS) {
+        sceneWords = L.num_nodes * 16 + S.num_prims * 12 + 4 * S.num_prims + 3 * S.num_prims + 3 * L.num_verts +
+                     3 * L.num_verts + L.num_shapes * (uint32_t)(sizeof(MtsgShape) / 4);
+    }
     LdsView<SCENE_LDS> v;
     v.ycolTab = (lds_u32 *)(lds + tabWords);
     // base2 and the node array size are multiples of 4 words: 16-byte aligned (ds_read_b128)
