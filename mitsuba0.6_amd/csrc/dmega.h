@@ -57,8 +57,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     bool done = false;
     PathState st;
     st.active = false;
-    st.px = st.py = 0;
-    st.j = st.pix = 0;
+    st.pix = 0;
     st.smp.sobolIndex = 0; st.smp.sampleIndex = 0; st.smp.dim = 0; st.smp.err = false;
     st.sx = st.sy = 0;
     st.haveRay = st.primary = st.haveShadow = false;

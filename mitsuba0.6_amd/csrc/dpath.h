@@ -1086,10 +1086,12 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 // with both traversals inline; the wavefront pipeline (wf_shade / wf_trace)
 // runs the traversals as separate kernels over compacted ray queues.
 // ---------------------------------------------------------------------------
+// (the pixel's coordinates and the sample index are not kept: pixel_of(pix)
+// and smp.sampleIndex give them where needed, two and one fewer registers
+// live across every bounce)
 struct PathState {
     bool active;
-    int px, py;
-    uint32_t j, pix;
+    uint32_t pix;
     float sx, sy;
     SamplerState smp;
     PathVars P;
@@ -1233,31 +1235,28 @@ struct PathShader {
     __device__ __forceinline__ bool start(PathState &st, uint64_t it) const {
         const uint32_t jj = (uint32_t)(it / L.num_pixels);
         st.pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
-        if (!pixel_of(L, st.pix, st.px, st.py)) return false;
-        begin(st, jj);
+        int px, py;
+        if (!pixel_of(L, st.pix, px, py)) return false;
+        begin(st, jj, px, py);
         return true;
     }
 
     // the SFMT replay's next sample: crop pixel xy (x | y << 16), sample jj of the chunk
     __device__ __forceinline__ void start_xy(PathState &st, uint32_t xy, uint32_t jj) const {
         const uint32_t lx = xy & 0xffffu, ly = xy >> 16;   // row_stride 1: compact row = ly
-        st.px = (int)(L.x0 + lx);
-        st.py = (int)(L.y0 + ly);
         st.pix = ((ly >> 3) * L.tiles_x + (lx >> 3)) * 64u + (ly & 7u) * 8u + (lx & 7u);   // pixel_of's inverse
-        begin(st, jj);
+        begin(st, jj, (int)(L.x0 + lx), (int)(L.y0 + ly));
     }
 
-    __device__ __forceinline__ void begin(PathState &st, uint32_t jj) const {
+    __device__ __forceinline__ void begin(PathState &st, uint32_t jj, const int px, const int py) const {
         const MtsgDeviceScene &S = L.scene;
         SamplerState &smp = st.smp;
         PathVars &P = st.P;
-        const int px = st.px, py = st.py;
-        uint32_t &j = st.j;
+        const uint32_t j = L.j0 + jj;
         float &sx = st.sx, &sy = st.sy;
         bool &haveRay = st.haveRay, &primary = st.primary, &haveShadow = st.haveShadow;
         f3 &ro = st.ro, &rd = st.rd;
         float &rmint = st.rmint, &rmaxt = st.rmaxt;
-        j = L.j0 + jj;
         smp.dim = 0;
         smp.sampleIndex = j;
         smp.err = false;
@@ -1303,7 +1302,8 @@ struct PathShader {
         const MtsgDeviceScene &S = L.scene;
         PathVars &P = st.P;
         SamplerState &smp = st.smp;
-        const int px = st.px, py = st.py;
+        // next2d reads the pixel only for dimensions 0-1 (begin() has drawn them)
+        const int px = 0, py = 0;
         const float sx = st.sx, sy = st.sy;
         if constexpr (HITK == 1) hit = true;
         if constexpr (HITK == 2) hit = false;
@@ -1591,8 +1591,9 @@ struct PathShader {
     __device__ __forceinline__ void finish(PathState &st) const {
         PathVars &P = st.P;
         SamplerState &smp = st.smp;
-        const int px = st.px, py = st.py;
-        const uint32_t j = st.j, pix = st.pix;
+        const uint32_t j = smp.sampleIndex, pix = st.pix;
+        int px = 0, py = 0;
+        pixel_of(L, pix, px, py);
         const float sx = st.sx, sy = st.sy;
         bool &haveRay = st.haveRay, &haveShadow = st.haveShadow;
         // block->put(samplePos, spec, alpha) (integrator.cpp:184): the own-pixel

@@ -111,7 +111,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     flags = f.x;
     st.active = (f.x & WF_ACTIVE) != 0;
     if (!st.active) {
-        st.j = h.y; st.pix = h.x;   // the last item's (sample, pixel): regeneration continues after it
+        st.smp.sampleIndex = h.y; st.pix = h.x;   // the last item's (sample, pixel): regeneration continues after it
         return false;
     }
     st.P.L = mk(a.x, a.y, a.z); st.P.eta = a.w;
@@ -120,7 +120,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     st.P.refN = mk(d.x, d.y, d.z); st.sx = d.w;
     st.ro = mk(e.x, e.y, e.z); st.sy = e.w;
     st.rd = mk(g.x, g.y, g.z); st.P.depth = __float_as_int(g.w);
-    st.pix = h.x; st.j = h.y;
+    st.pix = h.x;
     st.smp.sobolIndex = (uint64_t)h.z | ((uint64_t)h.w << 32);
     st.smp.sampleIndex = h.y;
     st.smp.dim = f.x >> 16;
@@ -131,7 +131,6 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     st.haveShadow = (f.x & WF_SHADOW) != 0;
     st.P.scattered = (f.x & WF_SCATTERED) != 0;
     st.P.emitted = (f.x & WF_EMITTED) != 0;
-    pixel_of(L, st.pix, st.px, st.py);
     return true;
 }
 
@@ -145,7 +144,7 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
     f.z = f.w = 0;
     reinterpret_cast<uint4 *>(v)[7] = f;
     reinterpret_cast<uint4 *>(v)[6] =
-        make_uint4(st.pix, st.j, (uint32_t)st.smp.sobolIndex, (uint32_t)(st.smp.sobolIndex >> 32));
+        make_uint4(st.pix, st.smp.sampleIndex, (uint32_t)st.smp.sobolIndex, (uint32_t)(st.smp.sobolIndex >> 32));
     if (!st.active) return;
     v[0] = make_float4(st.P.L.x, st.P.L.y, st.P.L.z, st.P.eta);
     v[1] = make_float4(st.P.thr.x, st.P.thr.y, st.P.thr.z, st.P.bsdfPdf);
@@ -207,7 +206,7 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
     if (was && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
         sh.finish(st);
         // regeneration: slot s takes items s, s + slots, s + 2 slots, ...
-        uint64_t it = (uint64_t)(st.j - L.j0) * L.num_pixels + st.pix + W.slots;
+        uint64_t it = (uint64_t)(st.smp.sampleIndex - L.j0) * L.num_pixels + st.pix + W.slots;
         while (true) {
             if (it >= L.num_items) { done = true; break; }
             if (sh.start(st, it)) break;
