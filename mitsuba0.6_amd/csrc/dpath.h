@@ -219,11 +219,24 @@ __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float(
 // LDSK > 0: the first LDSK stack entries live in LDS, deeper ones in a per-lane
 // global array `ovf` ({node, distance} pairs): a short LDS stack keeps the
 // traversal kernel's LDS per lane small (wf_trace occupancy); 0: all in LDS
+// RTOP (MTSG_REG_TOP=1, opt-in): the stack's top entry is cached in two
+// registers, so the pop that follows a push (depth-first: the far child after
+// the near subtree) reads no LDS; deeper entries live in LDS as before.
+// Bit-identical, but lost C2 -0.9%, C3 -4.2%, C4 -5.2%, C5 -3.9%
+// (profiles/r04_ab_reg_top.log): the node loop's extra selects cost more than
+// the LDS reads it saves.
+#ifndef MTSG_REG_TOP
+#define MTSG_REG_TOP 0
+#endif
 template <bool ANY, bool STATS, bool ANA = false, int LDSK = 0, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
                                          float &bt, unsigned long long &nodes, unsigned long long &tests,
                                          const MtsgAnalytic *anaArr = nullptr, uint2 *ovf = nullptr) {
+    constexpr bool RTOP = MTSG_REG_TOP && LDSK == 0;
+    bool cached = false;
+    int topN = 0;
+    uint16_t topD = 0;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
     const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
@@ -238,7 +251,10 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     auto pop = [&]() -> int {
         while (sp > 0) {
             --sp;
-            if (LDSK == 0 || sp < LDSK) {
+            if (RTOP && cached) {
+                cached = false;
+                if (ANY || dist_up16(topD) <= bt) return topN;
+            } else if (LDSK == 0 || sp < LDSK) {
                 if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
             } else {
                 const uint2 e = ovf[sp - LDSK];
@@ -270,7 +286,15 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 int nearC = ec0, farC = ec1;
                 float farT = n1;
                 if (n1 < n0) { nearC = ec1; farC = ec0; farT = n0; }
-                if (LDSK == 0 || sp < LDSK) {
+                if (RTOP) {
+                    if (cached) {   // the cached top moves down to LDS
+                        stkN[(sp - 1) * BLOCK] = topN;
+                        stkD[(sp - 1) * BLOCK] = topD;
+                    }
+                    topN = farC;
+                    topD = dist_down16(farT);
+                    cached = true;
+                } else if (LDSK == 0 || sp < LDSK) {
                     stkN[sp * BLOCK] = farC;
                     stkD[sp * BLOCK] = dist_down16(farT);
                 } else {
