@@ -43,6 +43,12 @@ hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks,
                                 hipStream_t s);
 int mtsg_wf_occupancy(const MtsgLaunch &L, int wk, bool ggx, int *shadeBpc, int *traceBpc);
 bool mtsg_wf_trace_dynamic(const MtsgLaunch &L);
+int mtsg_path_features(const MtsgLaunch &L);
+// the wavefront's trace kernel forms the whole hit record (MTSGPU_WF_HITREC=1; A/B in DESIGN.md 4)
+static bool wf_hitrec_on() {
+    const char *e = std::getenv("MTSGPU_WF_HITREC");
+    return e && e[0] == '1';
+}
 hipError_t mtsg_launch_sfmt_probe(uint32_t *w, unsigned long long *out, int n, hipStream_t s);
 hipError_t mtsg_launch_develop(const mtsgpu_develop_params &P, const float *film, void *out, int num_cus,
                                hipStream_t s);
@@ -90,7 +96,7 @@ struct mtsgpu_ctx {
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
     // wavefront pipeline: path slots, ray queues and results, counters
-    DevBuf wf_state, wf_ray, wf_rslot, wf_cls, wf_cnt, wf_hit, wf_occl, wf_live, wf_fetch, wf_ovf, wf_part, wf_kind;
+    DevBuf wf_state, wf_ray, wf_rslot, wf_cls, wf_cnt, wf_hit, wf_hitrec, wf_occl, wf_live, wf_fetch, wf_ovf, wf_part, wf_kind;
     DevBuf rp_order, rp_start, rp_sfmt;   // SFMT replay: render order, unit starts, streams
     // the reference's SAH kd-tree (kdtree_build.cpp), built on first use
     bool kd_built = false;
@@ -302,6 +308,7 @@ struct WfPlan {
     int shadeGrid[MTSG_WK_KINDS] = {};
     int traceGrid = 0;
     uint32_t slots = 0;
+    bool hitrec = false;   // wf_trace forms the hit records (MtsgWave::hitrec)
 };
 
 // The wavefront engine for one chunk of samples (wf_kernel.hip): the MISS
@@ -339,6 +346,10 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     W.slots = slots;
     W.cap = (uint32_t)cap;
     W.ovf_depth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
+    if (plan.hitrec) {
+        W.hitrec = (float4 *)ctx->wf_hitrec.p;
+        W.hitrec_uv = (mtsg_path_features(L) & MTSG_FEAT_EXT) ? 1u : 0u;
+    }
     unsigned long long *part = (unsigned long long *)ctx->wf_part.p;
     int partBlocks = plan.traceGrid;
     for (int k = 0; k < MTSG_WK_KINDS; ++k) partBlocks = std::max(partBlocks, plan.shadeGrid[k]);
@@ -805,6 +816,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             mtsg_wf_occupancy(L, -1, false, &sb, &tb);
             plan.traceGrid = std::max(1, ctx->num_cus * tb);
         }
+        plan.hitrec = wf_hitrec_on() && !mtsg_wf_trace_dynamic(L);
         const size_t slots = plan.slots, cap = slots;
         const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
         int partBlocks = plan.traceGrid;
@@ -815,6 +827,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             (e = ctx->wf_cls.ensure((size_t)2 * MTSG_WK_KINDS * R * cap * 4)) != hipSuccess ||
             (e = ctx->wf_cnt.ensure((size_t)2 * MTSG_WF_QUEUES * R * 4)) != hipSuccess ||
             (e = ctx->wf_hit.ensure(slots * 16)) != hipSuccess ||
+            (plan.hitrec && (e = ctx->wf_hitrec.ensure(slots * MTSG_WF_HIT_VECS * 16)) != hipSuccess) ||
             (e = ctx->wf_occl.ensure(slots * 4)) != hipSuccess ||
             (e = ctx->wf_live.ensure(2 * 4)) != hipSuccess ||
             (e = ctx->wf_fetch.ensure(2 * 4)) != hipSuccess ||
@@ -953,7 +966,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_ray, &ctx->wf_rslot, &ctx->wf_cls,
-                      &ctx->wf_cnt, &ctx->wf_hit, &ctx->wf_occl, &ctx->wf_live, &ctx->wf_fetch, &ctx->wf_ovf, &ctx->wf_part, &ctx->wf_kind, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
+                      &ctx->wf_cnt, &ctx->wf_hit, &ctx->wf_hitrec, &ctx->wf_occl, &ctx->wf_live, &ctx->wf_fetch, &ctx->wf_ovf, &ctx->wf_part, &ctx->wf_kind, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
     for (hipEvent_t &e : ctx->wf_ev)
         if (e) (void)hipEventDestroy(e);

@@ -892,6 +892,32 @@ __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, const HS &hs,
     }
 }
 
+// The wavefront engine's hit record formed by the trace kernel (MtsgWave::hitrec,
+// MTSG_WF_HIT_VECS float4 per slot): fill_hit's result, bit for bit, so a shade
+// kernel starts from one contiguous record instead of the slot -> prim -> vertex
+// chain of dependent loads.  The 6th vector (UVs) is written for textured scenes only.
+__device__ __forceinline__ void hit_store(float4 *r, const Hit &h, bool uv) {
+    r[0] = make_float4(h.t, h.p.x, h.p.y, h.p.z);
+    r[1] = make_float4(h.geoN.x, h.geoN.y, h.geoN.z, h.wi.x);
+    r[2] = make_float4(h.wi.y, h.wi.z, h.sh.s.x, h.sh.s.y);
+    r[3] = make_float4(h.sh.s.z, h.sh.t.x, h.sh.t.y, h.sh.t.z);
+    r[4] = make_float4(h.sh.n.x, h.sh.n.y, h.sh.n.z, __int_as_float(h.shape));
+    if (uv) r[5] = make_float4(h.u, h.v, 0.0f, 0.0f);
+}
+template <bool UV> __device__ __forceinline__ void hit_load(const float4 *r, Hit &h) {
+    const float4 a = r[0], b = r[1], c = r[2], d = r[3], e = r[4];
+    h.valid = 1;
+    h.t = a.x;
+    h.p = mk(a.y, a.z, a.w);
+    h.geoN = mk(b.x, b.y, b.z);
+    h.wi = mk(b.w, c.x, c.y);
+    h.sh.s = mk(c.z, c.w, d.x);
+    h.sh.t = mk(d.y, d.z, d.w);
+    h.sh.n = mk(e.x, e.y, e.z);
+    h.shape = __float_as_int(e.w);
+    if constexpr (UV) { const float4 f = r[5]; h.u = f.x; h.v = f.y; }
+}
+
 // DiscreteDistribution::sample/sampleReuse (core/pmf.h:124-169)
 __device__ __forceinline__ uint32_t dd_sample_reuse(const float *__restrict__ cdf, uint32_t n, float &value,
                                                    float *pdf) {
@@ -1320,9 +1346,10 @@ struct PathShader {
     }
 
     // the rest of one bounce, given the step's trace results: returns true
-    // when the path ends (path.cpp:135-292)
+    // when the path ends (path.cpp:135-292).  usePre: the hit record `pre` is already
+    // formed (the wavefront's trace kernel), else fill_hit forms it from (slot, prim, u, v, t)
     __device__ __forceinline__ bool shade(PathState &st, bool occluded, bool hit, uint32_t slot, uint32_t prim,
-                                          float hu, float hv, float ht) const {
+                                          float hu, float hv, float ht, bool usePre = false, const Hit &pre = Hit{}) const {
         const MtsgDeviceScene &S = L.scene;
         PathVars &P = st.P;
         SamplerState &smp = st.smp;
@@ -1346,7 +1373,8 @@ struct PathShader {
             // a miss overwrites the whole record: no field of the previous vertex stays
             // live across the next traversal except through an explicit use
             if (hit) {
-                fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, ro, rd, P.its);
+                if (usePre) P.its = pre;
+                else fill_hit<EXT, ANA>(S, hs, slot, prim, hu, hv, ht, ro, rd, P.its);
             } else {
                 P.its = Hit{};
             }

@@ -232,6 +232,7 @@ struct MtsgLookup {
 // capacity `cap` = slots, so one wave's append is one atomic on one of 8
 // counters and a region can never overflow; consumers walk the concatenation.
 #define MTSG_WF_STATE_VECS 8          // float4 state vectors per slot (AoS: one slot = 128 B)
+#define MTSG_WF_HIT_VECS 6            // float4 per precomputed hit record (dpath.h hit_store)
 #define MTSG_WF_NONE 0xffffffffu      // hit record prim: no hit
 #define MTSG_WF_REGIONS 8
 #ifndef MTSG_WF_LDS_STACK
@@ -257,6 +258,8 @@ struct MtsgWave {
     uint32_t parity;                  // bounce index & 1
     uint32_t seed;                    // first bounce: the MISS kernel takes every slot (identity queue)
     uint32_t ovf_depth;
+    float4 *hitrec;                   // [slots][MTSG_WF_HIT_VECS] hit records formed by wf_trace, or null
+    uint32_t hitrec_uv;               // textured scene: the records carry UVs
 };
 
 struct MtsgLaunch {

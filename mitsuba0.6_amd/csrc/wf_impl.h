@@ -188,22 +188,28 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
     bool occluded = false, hit = false;
     uint32_t slot = 0, prim = 0;
     float hu = 0, hv = 0, ht = 0;
+    Hit pre;
+    const bool usePre = HITK == 1 && W.hitrec != nullptr;   // launch-uniform
     if (was) {
         occluded = (flags & WF_SQUEUED) != 0 && W.occl[s] != 0;
         if constexpr (HITK == 1) {
-            // the hit record's 4th word: the TriAccel slot with analytic shapes (fill_hit
-            // reads the slot's record), else the primitive index itself
-            const float4 h = W.hit[s];
-            const uint32_t w = __float_as_uint(h.w);
             hit = true;
-            ht = h.x; hu = h.y; hv = h.z;
-            if ((FEAT & MTSG_FEAT_ANA) != 0) { slot = w; prim = S.tris[slot].prim; }
-            else prim = w;
+            if (usePre) {
+                hit_load<(FEAT & MTSG_FEAT_EXT) != 0>(W.hitrec + (size_t)s * MTSG_WF_HIT_VECS, pre);
+            } else {
+                // the hit record's 4th word: the TriAccel slot with analytic shapes (fill_hit
+                // reads the slot's record), else the primitive index itself
+                const float4 h = W.hit[s];
+                const uint32_t w = __float_as_uint(h.w);
+                ht = h.x; hu = h.y; hv = h.z;
+                if ((FEAT & MTSG_FEAT_ANA) != 0) { slot = w; prim = S.tris[slot].prim; }
+                else prim = w;
+            }
         }
     }
     // a slot in a queue is live, or (first bounce) not started yet
     bool done = false;
-    if (was && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
+    if (was && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht, usePre, pre)) {
         sh.finish(st);
         // regeneration: slot s takes items s, s + slots, s + 2 slots, ...
         uint64_t it = (uint64_t)(st.smp.sampleIndex - L.j0) * L.num_pixels + st.pix + W.slots;
@@ -363,13 +369,13 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
             W.occl[s] = occ ? 1u : 0u;
         } else {
             bool hit;
-            uint32_t w = MTSG_WF_NONE, shape = 0;
+            uint32_t w = MTSG_WF_NONE, shape = 0, prim = slot;
             if constexpr (KD) {
                 hit = kd_traverse<false, KDK>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot, kstk, kmb);
-                if (hit) { w = slot; shape = S.prim_vtx[4 * (size_t)slot + 3]; }
+                if (hit) { w = prim = slot; shape = S.prim_vtx[4 * (size_t)slot + 3]; }
             } else if (SCENE_LDS && L.scan) {
                 hit = scan_tris<false, STATS>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);
-                if (hit) { w = slot; shape = S.prim_vtx[4 * (size_t)slot + 3]; }
+                if (hit) { w = prim = slot; shape = S.prim_vtx[4 * (size_t)slot + 3]; }
             } else {
                 if (SCENE_LDS)
                     hit = traverse<false, STATS, ANA, MTSG_WF_LDS_STACK>(ldsNodes, ldsTris, o, d, mint, maxt, stkN,
@@ -381,10 +387,23 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
                 if (hit) {
                     const uint2 ps = *reinterpret_cast<const uint2 *>(&S.tris[slot].prim);   // prim, shape
                     w = ANA ? slot : ps.x;
+                    prim = ps.x;
                     shape = ps.y;
                 }
             }
-            W.hit[s] = make_float4(ht, hu, hv, __uint_as_float(w));
+            if (W.hitrec) {   // the shade kernels read the whole record (hit_store)
+                if (hit) {
+                    constexpr bool A = ANA && !KD;
+                    const HitSrc<false> hs{(glb_u32 *)S.prim_vtx, (glb_f32 *)S.positions, (glb_f32 *)S.normals,
+                                           (glb_f32 *)S.dpdu, (glb_shape *)S.shapes};
+                    Hit h;
+                    if (W.hitrec_uv) fill_hit<true, A>(S, hs, slot, prim, hu, hv, ht, o, d, h);
+                    else fill_hit<false, A>(S, hs, slot, prim, hu, hv, ht, o, d, h);
+                    hit_store(W.hitrec + (size_t)s * MTSG_WF_HIT_VECS, h, W.hitrec_uv != 0);
+                }
+            } else {
+                W.hit[s] = make_float4(ht, hu, hv, __uint_as_float(w));
+            }
             kind = hit ? W.shape_kind[shape] : (uint32_t)MTSG_WK_MISS;
         }
 #pragma unroll

@@ -117,3 +117,28 @@ def test_wavefront_row_shards_sum(gpu_ctx):
     for k in range(3):
         acc += gpu_ctx.render(it, row=(8, 3, k), engine='wavefront')[0]
     np.testing.assert_allclose(acc, full, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('case', ['shapes', 'C4', 'C5', 'kdtree'])
+def test_wavefront_hit_records(gpu_ctx, oracle, monkeypatch, case):
+    """MTSGPU_WF_HITREC=1: the trace kernel forms each closest hit's whole record
+    (fill_hit: position, normals, shading frame, wi, UVs) and the shade kernels
+    load it instead of re-deriving it from the primitive.  Analytic shapes, a
+    large HBM-BVH scene, textures (UVs in the record) and the kd-tree trace."""
+    monkeypatch.setenv('MTSGPU_WF_HITREC', '1')
+    if case == 'shapes':
+        sc, it = scenes.build('C1', width=48, height=40, spp=8, materials='shapes')
+    elif case == 'C4':
+        sc, it = scenes.build('C4', width=48, height=27, spp=4)
+    elif case == 'C5':
+        sc, it = scenes.build('C5', width=48, height=27, spp=8, env_size=(128, 64), blob=(60, 38))
+    else:
+        sc, it = scenes.build('C1', width=40, height=32, spp=8, materials='rough')
+        gpu_ctx.upload(sc)
+        _, smp_k, st_k = gpu_ctx.render(it, samples=True, engine='kdtree')
+        monkeypatch.delenv('MTSGPU_WF_HITREC')
+        _, smp_r, st_r = gpu_ctx.render(it, samples=True, engine='kdtree')
+        _records_equal(smp_k, smp_r, 'kd-tree hit records vs kd-tree')
+        assert st_k['rays'] == st_r['rays']
+        return
+    _check(gpu_ctx, oracle, sc, it, case + ' hit records')
