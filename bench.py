@@ -58,6 +58,9 @@ def parse_args(argv=None):
     ap.add_argument('--size', default=None, help='WxHxSPP override (launcher rehearsals and tests only)')
     ap.add_argument('--device', default='gpu', choices=['gpu', 'cpu-oracle'])
     ap.add_argument('--save-film', default=None, help='rank 0 writes the reduced film (.npy) after the last step')
+    ap.add_argument('--share-device', action='store_true',
+                    help='every rank on GPU 0, films reduced over gloo through host memory: a one-GPU rehearsal '
+                         'of the N-rank path (tests only; never a measurement)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
     ap.add_argument('--secondary', default='C3',
@@ -321,11 +324,19 @@ def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(max(args.steps, 1))]
 
+        def reduce():
+            if args.share_device and world > 1:   # gloo: through host memory
+                host = film.cpu()
+                shard.reduce(host, dist)
+                film.copy_(host)
+            else:
+                shard.reduce(film, dist)
+
         def step(k=None):   # mtsgpu_render_device clears the film on the stream
             st = ctx.render_device(integ, film.data_ptr(), stream, row=row, tile_shard=shard.tile_shard)
             if k is not None:
                 ev[k][0].record()
-            shard.reduce(film, dist)
+            reduce()
             if k is not None:
                 ev[k][1].record()
             return st
@@ -372,7 +383,7 @@ def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
     elapsed = time.perf_counter() - t0
     if gpu:
         reduce_s = [ev[k][0].elapsed_time(ev[k][1]) / 1e3 for k in range(args.steps)]
-    dev = 'cuda' if gpu else 'cpu'
+    dev = 'cuda' if gpu and not args.share_device else 'cpu'
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     s = torch.tensor([samples_rank], dtype=torch.float64, device=dev)
     r = torch.tensor([max(reduce_s) if reduce_s else 0.0], dtype=torch.float64, device=dev)
@@ -411,7 +422,7 @@ def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
             'config': {'workload': WORKLOADS.get(config, config), 'width': W, 'height': H, 'spp': spp,
                        'samples_per_frame': frame_samples,
                        'parallelism': '8x8 tiles dealt over %d rank(s) + %s film reduce' % (
-                           world, 'RCCL' if gpu else 'gloo'),
+                           world, 'RCCL' if gpu and not args.share_device else 'gloo'),
                        'world_size_reported': dist.get_world_size() if world > 1 else 1,
                        'reduce_ms_max': round(float(r.item()) * 1e3, 3),
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},
@@ -436,9 +447,12 @@ def main():
         if not torch.cuda.is_available():
             sys.exit('bench.py: no GPU visible (the HIP path has no CPU fallback; --device cpu-oracle is the '
                      'launcher rehearsal)')
-        torch.cuda.set_device(local)
-        if world > 1:
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        dev = 0 if args.share_device else local
+        torch.cuda.set_device(dev)
+        if world > 1 and args.share_device:
+            dist.init_process_group('gloo')   # RCCL refuses two ranks on one device
+        elif world > 1:
+            dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         lib_hash = lib_sha256()
     elif world > 1:
         dist.init_process_group('gloo')
@@ -471,6 +485,8 @@ def main():
                 'roofline': second['roofline'], 'cpu_baseline': second['cpu_baseline']}
         if not gpu:
             out['device'] = 'cpu-oracle launcher rehearsal (not a GPU measurement)'
+        elif args.share_device:
+            out['device'] = 'shared-GPU rehearsal: %d ranks on GPU 0, gloo reduce (not a scaling measurement)' % world
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
