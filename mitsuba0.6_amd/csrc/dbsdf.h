@@ -538,22 +538,26 @@ float cubic2d(float px, float py, glb_f32 *values, uint32_t sx, uint32_t sy) {
     return result;
 }
 
-// external table: eval(cosTheta, alpha) with m_etaFixed (rtrans.h:184-208)
-__device__ __forceinline__ float rt_eval(GBsdf &b, glb_f32 *rt, float cosTheta, float alpha) {
+// warpedAlpha of eval() and evalDiffuse() (rtrans.h:197, 241): a function of the
+// vertex's roughness only, so one powf serves every lookup at the vertex (RpPre)
+__device__ __forceinline__ float rt_warp_alpha(GBsdf &b, float alpha) {
+    return d_powf((alpha - b.rt_alpha_min) / (b.rt_alpha_max - b.rt_alpha_min), 0.25f);
+}
+// external table: eval(cosTheta, alpha) with m_etaFixed (rtrans.h:184-208), given
+// warpedAlpha (unused when the table is reduced to a fixed alpha)
+__device__ __forceinline__ float rt_eval_w(GBsdf &b, glb_f32 *rt, float cosTheta, float warpedAlpha) {
     const float warpedCosTheta = d_powf(fabsf(cosTheta), 0.25f);
     if (!(cosTheta >= 0)) return 0.f;
     float result;
     if (b.rt_alpha_fixed) {
         result = cubic1d(warpedCosTheta, rt + b.rt_ext, (uint32_t)b.rt_theta);
     } else {
-        const float warpedAlpha = d_powf((alpha - b.rt_alpha_min) / (b.rt_alpha_max - b.rt_alpha_min), 0.25f);
         result = cubic2d(warpedCosTheta, warpedAlpha, rt + b.rt_ext, (uint32_t)b.rt_theta, (uint32_t)b.rt_alpha);
     }
     return smin(1.0f, smax(0.0f, result));
 }
-// internal table: evalDiffuse(alpha) with m_etaFixed (rtrans.h:236-247)
-__device__ __forceinline__ float rt_eval_diffuse(GBsdf &b, glb_f32 *rt, float alpha) {
-    const float warpedAlpha = d_powf((alpha - b.rt_alpha_min) / (b.rt_alpha_max - b.rt_alpha_min), 0.25f);
+// internal table: evalDiffuse(alpha) with m_etaFixed (rtrans.h:236-247), given warpedAlpha
+__device__ __forceinline__ float rt_eval_diffuse_w(GBsdf &b, glb_f32 *rt, float warpedAlpha) {
     const float result = cubic1d(warpedAlpha, rt + b.rt_int, (uint32_t)b.rt_alpha);
     return smin(1.0f, smax(0.0f, result));
 }
@@ -565,20 +569,22 @@ __device__ __forceinline__ float rt_eval_diffuse(GBsdf &b, glb_f32 *rt, float al
 // 236-247): they depend only on the vertex (wi and the roughness at the hit),
 // so the kernel forms them once per vertex and hands them to every query there
 // -- the same values, from 2 instead of 7 table lookups per bounce
-struct RpPre { float twi, fdr; };
+// walpha: rt_warp_alpha of the vertex's roughness, for eval()'s T21 lookups too
+struct RpPre { float twi, fdr, walpha; };
 template <int BS>
 __device__ __forceinline__ RpPre rp_pre(GBsdf &b, glb_f32 *rt, f3 wi, float u, float v) {
     const Distr d = bsdf_distr<BS>(b, u, v);
     RpPre p;
-    p.twi = rt_eval(b, rt, wi.z, d.alphaU);
-    p.fdr = 1 - rt_eval_diffuse(b, rt, d.alphaU);
+    p.walpha = rt_warp_alpha(b, d.alphaU);
+    p.twi = rt_eval_w(b, rt, wi.z, p.walpha);
+    p.fdr = 1 - rt_eval_diffuse_w(b, rt, p.walpha);
     return p;
 }
 
 // the terms for the BSDF `b` queried with `wi` (zero for any other BSDF)
 template <int BS>
 __device__ __forceinline__ RpPre rp_pre_for(GBsdf &b, glb_f32 *rt, f3 wi, float u, float v) {
-    RpPre p = {0.0f, 0.0f};
+    RpPre p = {0.0f, 0.0f, 0.0f};
     if constexpr (BSet<BS>::EXT) {
         if (b.type == BSDF_ROUGHPLASTIC) p = rp_pre<BS>(b, rt, wi, u, v);
     }
@@ -610,7 +616,7 @@ __device__ __forceinline__ f3 rp_eval_body(GBsdf &b, glb_f32 *rt, f3 wi, f3 wo, 
     }
     f3 diff = bsdf_refl<BS>(b, u, v);
     const float T12 = pre.twi;
-    const float T21 = rt_eval(b, rt, wo.z, d.alphaU);
+    const float T21 = rt_eval_w(b, rt, wo.z, pre.walpha);
     const float Fdr = pre.fdr;
     if (b.nonlinear) diff = divv(diff, sub(mk(1.0f, 1.0f, 1.0f), mul(diff, Fdr)));
     else diff = divs(diff, 1 - Fdr);

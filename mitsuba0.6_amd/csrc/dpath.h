@@ -1468,7 +1468,7 @@ struct PathShader {
                 GBsdf &bsdf = ((GBsdf *)S.bsdfs)[sh.bsdf];
                 // roughplastic's per-vertex transmittance terms (dbsdf.h rp_pre), formed
                 // at the first query of this vertex and reused for the same BSDF and wi
-                RpPre rpc = {0.0f, 0.0f};
+                RpPre rpc = {0.0f, 0.0f, 0.0f};
                 GBsdf *rpB = nullptr;
                 float rpZ = 0.0f;
                 auto rpPre = [&](GBsdf *qb, f3 qwi) -> RpPre {
