@@ -165,12 +165,21 @@ __device__ __forceinline__ f3 env_to_world(glb_env *E, f3 v) {
               E->to_world[6] * v.x + E->to_world[7] * v.y + E->to_world[8] * v.z);
 }
 
-// EnvironmentMap::evalEnvironment without differentials (envmap.cpp:380-393)
-__device__ __forceinline__ f3 env_eval(glb_env *E, f3 d) {
+// A world direction's spherical coordinates in the map (envmap.cpp:384-386, 612-614):
+// evalEnvironment and internalPdfDirection form the same (u, v) from the same
+// local direction, so a miss that needs both forms them once
+struct EnvUV { float u, v, ly; };   // ly: the local direction's y (pdf's sinTheta)
+__device__ __forceinline__ EnvUV env_uv(glb_env *E, f3 d) {
     const f3 v = env_to_local(E, d);
-    const float u = d_atan2(v.x, -v.z) * D_INV_TWOPI, w = d_acos(smin(1.0f, smax(-1.0f, v.y))) * D_INV_PI;
-    return mul(env_eval_bilinear(E, 0, u, w), E->scale);
+    EnvUV r;
+    r.u = d_atan2(v.x, -v.z) * D_INV_TWOPI;
+    r.v = d_acos(smin(1.0f, smax(-1.0f, v.y))) * D_INV_PI;
+    r.ly = v.y;
+    return r;
 }
+// EnvironmentMap::evalEnvironment without differentials (envmap.cpp:380-393)
+__device__ __forceinline__ f3 env_eval_at(glb_env *E, EnvUV c) { return mul(env_eval_bilinear(E, 0, c.u, c.v), E->scale); }
+__device__ __forceinline__ f3 env_eval(glb_env *E, f3 d) { return env_eval_at(E, env_uv(E, d)); }
 
 // EnvironmentMap::evalEnvironment with ray differentials (envmap.cpp:380-410)
 __device__ __forceinline__ f3 env_eval_diff(glb_env *E, f3 d, f3 rxd, f3 ryd) {
@@ -266,10 +275,9 @@ __device__ __forceinline__ f3 env_sample_direct_impl(glb_env *E, f3 ref, float s
     return divs(value, pdf);
 }
 
-// internalPdfDirection (envmap.cpp:606-633), solid angle
-ENV_CALL float env_pdf_direction(glb_env *E, f3 dw) {
-    const f3 d = env_to_local(E, dw);
-    const float uvx = d_atan2(d.x, -d.z) * D_INV_TWOPI, uvy = d_acos(smin(1.0f, smax(-1.0f, d.y))) * D_INV_PI;
+// internalPdfDirection (envmap.cpp:606-633), solid angle, at the direction's env_uv
+ENV_CALL float env_pdf_at(glb_env *E, EnvUV c) {
+    const float uvx = c.u, uvy = c.v;
     if (!isfinite(uvx) || !isfinite(uvy)) return 0.0f;
     const int W = E->w0, H = E->h0;
     const float u = uvx * (float)W - 0.5f, v = uvy * (float)H - 0.5f;
@@ -277,11 +285,44 @@ ENV_CALL float env_pdf_direction(glb_env *E, f3 dw) {
     const float dx1 = u - (float)xPos, dx2 = 1.0f - dx1, dy1 = v - (float)yPos, dy2 = 1.0f - dy1;
     const f3 value1 = add(mul(mul(env_texel(E, 0, xPos, yPos), dx2), dy2), mul(mul(env_texel(E, 0, xPos + 1, yPos), dx1), dy2));
     const f3 value2 = add(mul(mul(env_texel(E, 0, xPos, yPos + 1), dx2), dy1), mul(mul(env_texel(E, 0, xPos + 1, yPos + 1), dx1), dy1));
-    const float sinTheta = safe_sqrt(1 - d.y * d.y);
+    const float sinTheta = safe_sqrt(1 - c.ly * c.ly);
     const int y0c = yPos < 0 ? 0 : (yPos > H - 1 ? H - 1 : yPos);
     const int y1c = yPos + 1 < 0 ? 0 : (yPos + 1 > H - 1 ? H - 1 : yPos + 1);
     return (env_lum(value1) * ((glb_f32 *)(uintptr_t)E->row_weights)[y0c] + env_lum(value2) * ((glb_f32 *)(uintptr_t)E->row_weights)[y1c]) * E->normalization /
            smax(fabsf(sinTheta), D_EPSILON);
+}
+__device__ __forceinline__ float env_pdf_direction(glb_env *E, f3 d) { return env_pdf_at(E, env_uv(E, d)); }
+
+// A miss's evalEnvironment value (evalBilinear at level 0, mipmap.h:500-522) and
+// its internalPdfDirection (envmap.cpp:606-633) at the same (u, v), in one call:
+// both read the same four texels (level 0 is w0 x h0, scene_build.cpp), and each
+// result keeps its own summation order
+struct EnvValPdf { f3 value; float pdf; };
+ENV_CALL EnvValPdf env_eval_pdf_at(glb_env *E, EnvUV c) {
+    EnvValPdf r;
+    r.value = mk(0, 0, 0);
+    r.pdf = 0.0f;
+    if (!isfinite(c.u) || !isfinite(c.v)) return r;
+    const int W = E->w0, H = E->h0;
+    const float u = c.u * (float)W - 0.5f, v = c.v * (float)H - 0.5f;
+    const int xPos = (int)floorf(u), yPos = (int)floorf(v);
+    const float dx1 = u - (float)xPos, dx2 = 1.0f - dx1, dy1 = v - (float)yPos, dy2 = 1.0f - dy1;
+    const f3 t00 = env_texel(E, 0, xPos, yPos), t01 = env_texel(E, 0, xPos, yPos + 1);
+    const f3 t10 = env_texel(E, 0, xPos + 1, yPos), t11 = env_texel(E, 0, xPos + 1, yPos + 1);
+    f3 e = mul(mul(t00, dx2), dy2);   // evalBilinear's order
+    e = add(e, mul(mul(t01, dx2), dy1));
+    e = add(e, mul(mul(t10, dx1), dy2));
+    e = add(e, mul(mul(t11, dx1), dy1));
+    r.value = mul(e, E->scale);
+    const f3 value1 = add(mul(mul(t00, dx2), dy2), mul(mul(t10, dx1), dy2));   // internalPdfDirection's
+    const f3 value2 = add(mul(mul(t01, dx2), dy1), mul(mul(t11, dx1), dy1));
+    const float sinTheta = safe_sqrt(1 - c.ly * c.ly);
+    const int y0c = yPos < 0 ? 0 : (yPos > H - 1 ? H - 1 : yPos);
+    const int y1c = yPos + 1 < 0 ? 0 : (yPos + 1 > H - 1 ? H - 1 : yPos + 1);
+    r.pdf = (env_lum(value1) * ((glb_f32 *)(uintptr_t)E->row_weights)[y0c] +
+             env_lum(value2) * ((glb_f32 *)(uintptr_t)E->row_weights)[y1c]) * E->normalization /
+            smax(fabsf(sinTheta), D_EPSILON);
+    return r;
 }
 
 struct EnvSample { f3 value, d; float dist, pdf; };

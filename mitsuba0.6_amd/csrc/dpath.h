@@ -1386,13 +1386,15 @@ struct PathShader {
                 // missed: the environment emitter, if any (path.cpp:233-247)
                 if (ENV && !(L.hide_emitters && !P.scattered)) {
                     glb_env *E = (glb_env *)S.env;
-                    const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : env_eval(E, rd);
+                    EnvValPdf vp = {mk(0, 0, 0), 0.0f};
+                    if (!E->constant) vp = env_eval_pdf_at(E, env_uv(E, rd));   // one (u, v) and texel set for both
+                    const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : vp.value;
                     float nT, fT;
                     // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
                     if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
                         float lumPdf = 0;
                         if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
-                            lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : env_pdf_direction(E, rd)) *
+                            lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : vp.pdf) *
                                      (S.emitters[S.env_emitter].weight * S.em_norm);
                         const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
                         P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
