@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MTSGPU_ABI_VERSION 7
+#define MTSGPU_ABI_VERSION 8
 
 /* ---- status codes ------------------------------------------------------ */
 enum {
@@ -45,7 +45,8 @@ enum {
     MTSGPU_ESTATE = -4,   /* call out of order (e.g. render before upload)           */
     MTSGPU_EDIM = -5,     /* Sobol dimension table exhausted (sobol.cpp:224,238)     */
     MTSGPU_ECANCEL = -6,  /* *cancel flag was set (Integrator::cancel)               */
-    MTSGPU_ENODEV = -7    /* no usable gfx950 device                                 */
+    MTSGPU_ENODEV = -7,   /* no usable gfx950 device                                 */
+    MTSGPU_ENOENT = -8    /* mtsgpu_xml_bsdf_ex: the id is not in the scene file     */
 };
 
 /* ---- scene description (POD) ------------------------------------------- */
@@ -280,21 +281,36 @@ int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap);
  * textures are private children (src/bsdfs/twosided.cpp:198-210): a plugin
  * cannot reach them, but the scene's source file can
  * (Scene::getSourceFile, include/mitsuba/render/scene.h:1107).
- * mtsgpu_xml_bsdf parses that file and returns the tree below the <bsdf> with
- * the given id: node 0 is that BSDF, every other node a nested <bsdf> or
- * <texture> (a <ref> child resolved by id) with its parent's index and the
- * parameter name it fills ('name' attribute); each node owns num_props
- * property elements from first_prop on (tag float/integer/boolean/string/
- * rgb/srgb/spectrum/point/vector, name, value with $params replaced by the
- * file's <default> values).  The shim rebuilds a Properties object per node.
- * Returns MTSGPU_OK, MTSGPU_EINVAL (unreadable file, syntax error, unknown id;
- * message in err), or MTSGPU_ENOMEM when a capacity is too small (the counts
- * are still returned). */
+ * mtsgpu_xml_bsdf_ex reads that file as SceneHandler does
+ * (src/librender/scenehandler.cpp: $parameter substitution in every
+ * attribute, <default>, <alias>, <include>, duplicate ids rejected) and
+ * returns the tree below one <bsdf>:
+ *   lookup MTSGPU_XML_BY_ID:    the <bsdf> with id `id`;
+ *   lookup MTSGPU_XML_BY_SHAPE: the <bsdf> child (inline or <ref>) of the
+ *                               <shape> with id `id` (a BSDF declared inline
+ *                               has no id of its own).
+ * Node 0 is that BSDF, every other node a nested <bsdf> or <texture> (a <ref>
+ * child resolved by id) with its parent's index and the parameter name it
+ * fills ('name' attribute); each node owns num_props property elements from
+ * first_prop on (tag float/integer/boolean/string/rgb/srgb/spectrum/point/
+ * vector, name, value after substitution, flags).  param_names/values are the
+ * loader's parameters (`mitsuba -D name=value`, src/mitsuba/mitsuba.cpp:
+ * 168-173); as in the loader they take precedence over the file's <default>s
+ * (scenehandler.cpp:684-687).  A property's flags say whether its value went
+ * through a substitution (MTSGPU_XML_PROP_PARAM) and whether a <default>
+ * supplied it (MTSGPU_XML_PROP_DEFAULT).  The shim rebuilds a Properties
+ * object per node.  Returns MTSGPU_OK, MTSGPU_ENOENT (the id is not in the
+ * file), MTSGPU_EINVAL (unreadable file, syntax error, undefined parameter,
+ * duplicate id, wrong element kind; message in err), or MTSGPU_ENOMEM when a
+ * capacity is too small (the counts are still returned).
+ * mtsgpu_xml_bsdf is the BY_ID lookup without loader parameters. */
 enum { MTSGPU_XML_BSDF = 0, MTSGPU_XML_TEXTURE = 1 };
+enum { MTSGPU_XML_BY_ID = 0, MTSGPU_XML_BY_SHAPE = 1 };
+enum { MTSGPU_XML_PROP_PARAM = 1, MTSGPU_XML_PROP_DEFAULT = 2 };
 typedef struct {
     int32_t kind;                   /* MTSGPU_XML_BSDF / MTSGPU_XML_TEXTURE        */
     int32_t parent;                 /* parent node index, -1 for node 0            */
-    char plugin[32];                /* the 'type' attribute                        */
+    char plugin[32];                /* the 'type' attribute (lower case)           */
     char name[64];                  /* parameter name under the parent ('' if none)*/
     char id[64];                    /* the element's 'id' ('' if none)             */
     int32_t first_prop, num_props;
@@ -303,7 +319,12 @@ typedef struct {
     char tag[16];                   /* float, integer, boolean, string, rgb, ...   */
     char name[64];
     char value[128];
+    int32_t flags;                  /* MTSGPU_XML_PROP_*                           */
 } mtsgpu_xml_prop;
+int mtsgpu_xml_bsdf_ex(const char *xml_path, const char *id, int32_t lookup, const char *const *param_names,
+                       const char *const *param_values, int32_t num_params, mtsgpu_xml_node *nodes, int node_cap,
+                       mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props, char *err,
+                       size_t err_cap);
 int mtsgpu_xml_bsdf(const char *xml_path, const char *bsdf_id, mtsgpu_xml_node *nodes, int node_cap,
                     mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props, char *err,
                     size_t err_cap);

@@ -30,11 +30,14 @@
  * selects a device group; mtsgpu_group_render shards the crop's 8x8 tiles
  * over the GPUs and merges the films over xGMI before Film::put.
  *
- * Nested (twosided) and textured BSDFs: the plugins keep them as private
- * children, so the shim reads their element trees back from the scene file
- * (Scene::getSourceFile, scene.h:1107) by the BSDF's id through
- * mtsgpu_xml_bsdf, rebuilds a Properties object per element and converts it
- * like any other BSDF.  Such a BSDF needs an id in the file.
+ * BSDFs: the plugins keep nested BSDFs (twosided) and textures as private
+ * children, so the scene file is the authority.  Every BSDF the file holds --
+ * by its own id, or inline in a <shape> with an id -- is read back from it
+ * (Scene::getSourceFile, scene.h:1107) through mtsgpu_xml_bsdf_ex with the
+ * loader's parameters, rebuilt as one Properties object per element and
+ * converted like any other BSDF.  A BSDF the file does not hold is converted
+ * from its Properties only when it is not twosided and shows no textured
+ * parameter; otherwise the render stops with an error naming the shape.
  */
 #include <mitsuba/render/scene.h>
 #include <mitsuba/render/trimesh.h>
@@ -51,6 +54,7 @@
 
 #include "../bsdfs/ior.h"      /* lookupIOR: the BSDF plugins' IOR presets */
 #include "mtsgpu.h"
+#include "gpupath_util.h"
 
 #ifndef GPU_INTEGRATOR
 #define GPU_INTEGRATOR 0     /* 0: path, 1: volpath, 2: direct */
@@ -220,7 +224,7 @@ public:
             const std::string cls = shape->getClass()->getName();
             mtsgpu_mesh_desc md;
             std::memset(&md, 0, sizeof md);
-            md.bsdf = bsdfIndex(shape->getBSDF());
+            md.bsdf = bsdfIndex(shape->getBSDF(), shape);
             md.emitter = shape->isEmitter() ? indexOf(emitterObjs, (const Emitter *) shape->getEmitter()) : -1;
             if (shape->hasMedium() || shape->isMediumTransition())
                 Log(EError, "participating media are not supported");
@@ -346,53 +350,116 @@ public:
     MTS_DECLARE_CLASS()
 private:
     /* Does the BSDF give the same diffuse reflectance and roughness at every
-       surface position (no textured parameter)? */
+       probed surface position (gpupath_probe_uv)?  Only for BSDFs the scene
+       file does not hold (see bsdfIndex): a probe cannot prove a parameter
+       constant, it can only catch a textured one. */
     static bool isConstant(const BSDF *bsdf) {
-        Intersection a, b;
-        a.uv = Point2(0.173f, 0.291f); b.uv = Point2(0.618f, 0.854f);
-        a.p = Point(0.0f); b.p = Point(1.0f);
-        bool varies = bsdf->getDiffuseReflectance(a) != bsdf->getDiffuseReflectance(b);
-        for (int c = 0; c < bsdf->getComponentCount(); ++c)
-            varies |= bsdf->getRoughness(a, c) != bsdf->getRoughness(b, c);
-        return !varies;
+        std::vector<Intersection> its;
+        const std::vector<std::pair<float, float> > uv = gpupath_probe_uv();
+        for (size_t k = 0; k < uv.size(); ++k) {
+            Intersection a;
+            a.uv = Point2(uv[k].first, uv[k].second);
+            a.p = Point(a.uv.x, a.uv.y, (Float) (k & 1));
+            its.push_back(a);
+        }
+        const Spectrum r0 = bsdf->getDiffuseReflectance(its[0]);
+        for (size_t k = 1; k < its.size(); ++k) {
+            if (bsdf->getDiffuseReflectance(its[k]) != r0) return false;
+            for (int c = 0; c < bsdf->getComponentCount(); ++c)
+                if (bsdf->getRoughness(its[k], c) != bsdf->getRoughness(its[0], c)) return false;
+        }
+        return true;
     }
 
     /* Append a BSDF descriptor (de-duplicated by pointer); NULL -> -1 (the
        library applies Shape::configure's default diffuse, shape.cpp:48-70).
        The plugins keep textures and nested BSDFs as private children, out of
-       reach of a plugin shim: twosided and textured BSDFs (detected by
-       evaluating the BSDF at two surface positions) are read back from the
-       scene file by their id (mtsgpu_xml_bsdf, Scene::getSourceFile). */
-    int bsdfIndex(const BSDF *bsdf) {
+       reach of a plugin shim, so the scene file is the authority: every BSDF
+       the file holds -- by its own id, or inline in a shape with an id -- is
+       read back from it (mtsgpu_xml_bsdf_ex, Scene::getSourceFile) and
+       converted from the rebuilt element tree.  Only a BSDF the file does not
+       hold (a scene built in code, an inline BSDF of a shape without id) is
+       converted from its Properties, and only when it is not twosided and the
+       probe finds no varying parameter. */
+    int bsdfIndex(const BSDF *bsdf, const Shape *shape) {
         if (!bsdf) return -1;
         const int have = indexOf(m_bsdfObjs, bsdf);
         if (have >= 0) return have;
+        const std::string where = formatString("(the BSDF of shape \"%s\", id \"%s\")",
+                                               shape->getName().c_str(), shape->getID().c_str());
+        if (!m_sceneFile.empty()) {
+            int idx = xmlBsdf(bsdf, bsdf->getID(), MTSGPU_XML_BY_ID, where);
+            if (idx == -2) idx = xmlBsdf(bsdf, shape->getID(), MTSGPU_XML_BY_SHAPE, where);
+            if (idx >= 0) return idx;
+        }
         const Properties &p = bsdf->getProperties();
-        if (p.getPluginName() != "twosided" && isConstant(bsdf))
-            return appendDesc(p, bsdf, NULL);
-        return xmlBsdf(bsdf);
+        if (p.getPluginName() == "twosided")
+            Log(EError, "twosided BSDF \"%s\" %s: its nested BSDFs are read from the scene file, which does not "
+                "hold it; give the BSDF (or its shape) an id in %s", bsdf->getID().c_str(), where.c_str(),
+                m_sceneFile.empty() ? "a scene file" : m_sceneFile.string().c_str());
+        if (!isConstant(bsdf))
+            Log(EError, "BSDF \"%s\" %s has a textured parameter, and textures are read from the scene file, which "
+                "does not hold it; give the BSDF (or its shape) an id in %s", bsdf->getID().c_str(), where.c_str(),
+                m_sceneFile.empty() ? "a scene file" : m_sceneFile.string().c_str());
+        return appendDesc(p, bsdf, NULL);
     }
 
-    int xmlBsdf(const BSDF *bsdf) {
-        const std::string id = bsdf->getID();
-        if (m_sceneFile.empty())
-            Log(EError, "BSDF \"%s\" has nested BSDFs or textures, which a plugin cannot read, and the scene "
-                "has no source file to read them from", id.c_str());
+    /* The loader's parameters ($name substitutions): the integrator's
+       'parameters' property ("name=value;name=value") if set, else the
+       `mitsuba -D name=value` arguments of this process (mitsuba.cpp:168-173).
+       They take precedence over the file's <default>s, as in the loader. */
+    void loaderParameters(std::vector<std::string> &names, std::vector<std::string> &values) const {
+        std::string cmdline, bad;
+        if (!m_props.hasProperty("parameters")) {
+            std::ifstream is("/proc/self/cmdline", std::ios::binary);
+            cmdline.assign(std::istreambuf_iterator<char>(is), std::istreambuf_iterator<char>());
+        }
+        if (!gpupath_loader_params(m_props.hasProperty("parameters"), m_props.getString("parameters", ""), cmdline,
+                                   names, values, bad))
+            Log(EError, "Invalid parameter specification \"%s\"", bad.c_str());
+    }
+
+    /* The file's tree for `id` -> descriptors; -2 when the file does not hold it */
+    int xmlBsdf(const BSDF *bsdf, const std::string &id, int lookup, const std::string &where) {
+        std::vector<std::string> pn, pv;
+        loaderParameters(pn, pv);
+        std::vector<const char *> pnc, pvc;
+        for (size_t i = 0; i < pn.size(); ++i) { pnc.push_back(pn[i].c_str()); pvc.push_back(pv[i].c_str()); }
         std::vector<mtsgpu_xml_node> nodes(64);
         std::vector<mtsgpu_xml_prop> props(1024);
         int nn = 0, np = 0;
         char err[512] = "";
-        int rc = mtsgpu_xml_bsdf(m_sceneFile.string().c_str(), id.c_str(), nodes.data(), (int) nodes.size(),
-                                 props.data(), (int) props.size(), &nn, &np, err, sizeof err);
+        const std::string file = m_sceneFile.string();
+        int rc = mtsgpu_xml_bsdf_ex(file.c_str(), id.c_str(), lookup, pnc.data(), pvc.data(), (int32_t) pn.size(),
+                                    nodes.data(), (int) nodes.size(), props.data(), (int) props.size(), &nn, &np,
+                                    err, sizeof err);
         if (rc == MTSGPU_ENOMEM) {
             nodes.resize((size_t) nn); props.resize((size_t) np);
-            rc = mtsgpu_xml_bsdf(m_sceneFile.string().c_str(), id.c_str(), nodes.data(), nn, props.data(), np,
-                                 &nn, &np, err, sizeof err);
+            rc = mtsgpu_xml_bsdf_ex(file.c_str(), id.c_str(), lookup, pnc.data(), pvc.data(), (int32_t) pn.size(),
+                                    nodes.data(), nn, props.data(), np, &nn, &np, err, sizeof err);
         }
+        if (rc == MTSGPU_ENOENT) return -2;
         if (rc != MTSGPU_OK)
-            Log(EError, "BSDF \"%s\" (nested BSDFs / textures are read from %s by the BSDF's id): %s",
-                id.c_str(), m_sceneFile.string().c_str(), err);
+            Log(EError, "BSDF \"%s\" %s, read from %s: %s", bsdf->getID().c_str(), where.c_str(), file.c_str(), err);
         nodes.resize((size_t) nn);
+        /* The top BSDF's own properties are visible: a value the file's <default>
+           supplied must be the one the loader used, or the loader had a parameter
+           this shim was not given (nested elements could differ the same way). */
+        const Properties &have = bsdf->getProperties();
+        if (std::string(nodes[0].plugin) != have.getPluginName())
+            Log(EError, "BSDF \"%s\" %s is a \"%s\" in the scene but a \"%s\" in %s", bsdf->getID().c_str(),
+                where.c_str(), have.getPluginName().c_str(), nodes[0].plugin, file.c_str());
+        Properties fromFile(nodes[0].plugin);
+        for (int i = nodes[0].first_prop; i < nodes[0].first_prop + nodes[0].num_props; ++i) {
+            setProperty(fromFile, props[i]);
+            const std::string name = props[i].name;
+            if ((props[i].flags & MTSGPU_XML_PROP_DEFAULT) && have.hasProperty(name) &&
+                have.getAsString(name) != fromFile.getAsString(name))
+                Log(EError, "BSDF \"%s\" %s: property \"%s\" is %s in the scene but %s by the file's <default>: "
+                    "the loader had parameters this integrator was not given (set its 'parameters' property to "
+                    "the loader's name=value list)", bsdf->getID().c_str(), where.c_str(), name.c_str(),
+                    have.getAsString(name).c_str(), fromFile.getAsString(name).c_str());
+        }
         return xmlNode(nodes, props, 0, bsdf);
     }
 

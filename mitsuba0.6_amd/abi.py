@@ -7,14 +7,14 @@ import ctypes as C
 
 import numpy as np
 
-OK, EINVAL, EHIP, ENOMEM, ESTATE, EDIM, ECANCEL, ENODEV = 0, -1, -2, -3, -4, -5, -6, -7
+OK, EINVAL, EHIP, ENOMEM, ESTATE, EDIM, ECANCEL, ENODEV, ENOENT = 0, -1, -2, -3, -4, -5, -6, -7, -8
 STATUS_NAMES = {OK: 'OK', EINVAL: 'EINVAL', EHIP: 'EHIP', ENOMEM: 'ENOMEM', ESTATE: 'ESTATE',
-                EDIM: 'EDIM', ECANCEL: 'ECANCEL', ENODEV: 'ENODEV'}
+                EDIM: 'EDIM', ECANCEL: 'ECANCEL', ENODEV: 'ENODEV', ENOENT: 'ENOENT'}
 
 BSDF_DIFFUSE, BSDF_ROUGHCONDUCTOR, BSDF_ROUGHDIELECTRIC, BSDF_ROUGHPLASTIC = 0, 1, 2, 3
 BSDF_CONDUCTOR, BSDF_DIELECTRIC, BSDF_PLASTIC, BSDF_TWOSIDED = 4, 5, 6, 7
 TEX_NONE, TEX_CHECKERBOARD = 0, 1
-ABI_VERSION = 7
+ABI_VERSION = 8
 TRACE_SHADOW, TRACE_KDTREE = 1, 2           # mtsgpu_trace_rays_ex flags
 DISTR_BECKMANN, DISTR_GGX, DISTR_PHONG = 0, 1, 2
 EMITTER_AREA, EMITTER_ENVMAP, EMITTER_CONSTANT = 0, 1, 2
@@ -125,6 +125,8 @@ def uptr(a):
 
 
 XML_BSDF, XML_TEXTURE = 0, 1
+XML_BY_ID, XML_BY_SHAPE = 0, 1                # mtsgpu_xml_bsdf_ex lookup
+XML_PROP_PARAM, XML_PROP_DEFAULT = 1, 2      # mtsgpu_xml_prop.flags
 
 
 class XmlNode(C.Structure):
@@ -135,4 +137,4 @@ class XmlNode(C.Structure):
 
 class XmlProp(C.Structure):
     """mtsgpu_xml_prop (include/mtsgpu.h)."""
-    _fields_ = [('tag', C.c_char * 16), ('name', C.c_char * 64), ('value', C.c_char * 128)]
+    _fields_ = [('tag', C.c_char * 16), ('name', C.c_char * 64), ('value', C.c_char * 128), ('flags', C.c_int32)]

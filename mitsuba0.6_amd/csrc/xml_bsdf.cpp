@@ -5,22 +5,41 @@
 // textures as private children (src/bsdfs/twosided.cpp:198-210, the
 // Texture-valued members of diffuse/rough*.cpp): a plugin cannot reach them.
 // The scene's source file can (Scene::getSourceFile,
-// include/mitsuba/render/scene.h:1107).  mtsgpu_xml_bsdf reads that file and
-// returns the element tree below the BSDF with the requested id -- nested
-// <bsdf> and <texture> elements, <ref> children resolved by id, and the
-// property elements of each with `$name` defaults substituted -- as flat
-// arrays.  The shim turns each node back into a Properties object and converts
-// it with the code it uses for the BSDFs it can see.
+// include/mitsuba/render/scene.h:1107).  mtsgpu_xml_bsdf_ex reads that file
+// and returns the element tree below a BSDF -- nested <bsdf> and <texture>
+// elements, <ref> children resolved by id, and the property elements of each
+// -- as flat arrays.  The shim turns each node back into a Properties object
+// and converts it with the code it uses for the BSDFs it can see.
 //
-// The XML subset is the scene format's own (SceneHandler, src/librender/
-// scenehandler.cpp): elements, attributes in single or double quotes,
-// self-closing tags, comments, the XML declaration, the five predefined
-// entities.  <include> is not followed.
+// The file is read as SceneHandler reads it (src/librender/scenehandler.cpp):
+//   - every attribute of every element has its $parameters replaced when the
+//     element starts (:208-220): the loader's parameters (the caller's list, e.g.
+//     the `mitsuba -D name=value` map, src/mitsuba/mitsuba.cpp:168-173) in
+//     reverse name order, by plain substring replacement; a '$' left over
+//     without a '[' is an error;
+//   - <default name value> adds a parameter when the element ends, unless the
+//     loader already has it (:684-687), so the caller's values win;
+//   - ids are registered when their element ends; a second element with the
+//     same id is an error (:784-786), and so is an <alias> onto a taken id
+//     (:646-656);
+//   - <include filename> parses the named file with the same parameters and
+//     ids (:658-680), relative to the including file's directory (the
+//     FileResolver has the scene's directory first);
+//   - the `type` attribute is lower-cased (:275).
+// Each returned property carries flags saying whether its value went through a
+// substitution and whether a <default> supplied it, so a caller that cannot
+// see the loader's parameters can check those values against the plugin's own.
+//
+// The XML subset is the scene format's own: elements, attributes in single or
+// double quotes, self-closing tags, comments, the XML declaration, the five
+// predefined entities.
+#include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <map>
 #include <memory>
+#include <set>
 #include <sstream>
 #include <string>
 #include <vector>
@@ -32,11 +51,18 @@ namespace {
 struct XElem {
     std::string tag;
     std::vector<std::pair<std::string, std::string>> attrs;
+    std::vector<int> flags;   // per attribute: MTSGPU_XML_PROP_* after expansion
     std::vector<std::unique_ptr<XElem>> kids;
+    int line = 0;
     const std::string *attr(const char *k) const {
         for (auto &a : attrs)
             if (a.first == k) return &a.second;
         return nullptr;
+    }
+    int attr_flags(const char *k) const {
+        for (size_t j = 0; j < attrs.size(); ++j)
+            if (attrs[j].first == k) return j < flags.size() ? flags[j] : 0;
+        return 0;
     }
 };
 
@@ -46,12 +72,13 @@ struct XParser {
     std::string err;
     explicit XParser(const std::string &src) : s(src) {}
 
+    int line_at(size_t pos) const {
+        int line = 1;
+        for (size_t k = 0; k < pos && k < s.size(); ++k) line += s[k] == '\n';
+        return line;
+    }
     bool fail(const std::string &m) {
-        if (err.empty()) {
-            size_t line = 1;
-            for (size_t k = 0; k < i && k < s.size(); ++k) line += s[k] == '\n';
-            err = m + " (line " + std::to_string(line) + ")";
-        }
+        if (err.empty()) err = m + " (line " + std::to_string(line_at(i)) + ")";
         return false;
     }
     void ws() {
@@ -99,6 +126,7 @@ struct XParser {
     }
     // an element starting at '<' (not a closing tag)
     bool element(XElem &e) {
+        e.line = line_at(i);
         ++i;   // '<'
         e.tag = name();
         if (e.tag.empty()) return fail("expected an element name");
@@ -142,39 +170,110 @@ struct XParser {
     }
 };
 
-struct TreeBuilder {
-    const XElem &root;
+bool read_file(const std::string &path, std::string &out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::stringstream ss;
+    ss << f.rdbuf();
+    out = ss.str();
+    return true;
+}
+
+std::string dir_of(const std::string &path) {
+    const size_t k = path.find_last_of('/');
+    return k == std::string::npos ? std::string() : path.substr(0, k + 1);
+}
+
+// The document-order pass of SceneHandler over a file and its includes:
+// parameter substitution, <default>, ids, <alias>, <include>.
+struct Loader {
+    std::map<std::string, std::string> params;   // name -> value (the loader's and then <default>'s)
+    std::set<std::string> from_default;          // names a <default> supplied
     std::map<std::string, const XElem *> ids;
-    std::map<std::string, std::string> defaults;
+    std::vector<std::unique_ptr<XElem>> roots;   // the main file and every included file
+    std::vector<std::string> files;
+    std::string err;
+
+    bool fail(const std::string &file, const XElem &e, const std::string &m) {
+        if (err.empty()) err = file + " (line " + std::to_string(e.line) + "): " + m;
+        return false;
+    }
+    // scenehandler.cpp:208-220, with a record of where the replacements came from
+    bool subst(std::string &v, int &flags) {
+        flags = 0;
+        if (v.empty() || v.find('$') == std::string::npos) return true;
+        for (auto it = params.rbegin(); it != params.rend(); ++it) {
+            const std::string search = "$" + it->first;
+            size_t pos = 0;
+            while ((pos = v.find(search, pos)) != std::string::npos) {
+                v.replace(pos, search.size(), it->second);
+                flags |= MTSGPU_XML_PROP_PARAM | (from_default.count(it->first) ? MTSGPU_XML_PROP_DEFAULT : 0);
+                ++pos;
+            }
+        }
+        return v.find('$') == std::string::npos || v.find('[') != std::string::npos;
+    }
+    bool load(const std::string &path, int depth) {
+        if (depth > 16) { err = path + ": <include> nests too deeply"; return false; }
+        std::string src;
+        if (!read_file(path, src)) { err = "cannot read " + path; return false; }
+        std::unique_ptr<XElem> root(new XElem());
+        XParser P(src);
+        if (!P.document(*root)) { err = path + ": " + P.err; return false; }
+        XElem *r = root.get();
+        roots.push_back(std::move(root));
+        files.push_back(path);
+        return walk(*r, path, depth);
+    }
+    bool walk(XElem &e, const std::string &file, int depth) {
+        e.flags.assign(e.attrs.size(), 0);
+        for (size_t j = 0; j < e.attrs.size(); ++j)      // startElement
+            if (!subst(e.attrs[j].second, e.flags[j]))
+                return fail(file, e, "The scene referenced an undefined parameter: \"" + e.attrs[j].second + "\"");
+        for (auto &a : e.attrs)
+            if (a.first == "type")
+                for (auto &c : a.second) c = (char)std::tolower((unsigned char)c);
+        for (auto &k : e.kids)
+            if (!walk(*k, file, depth)) return false;
+        // endElement
+        if (e.tag == "default") {
+            const std::string *n = e.attr("name"), *v = e.attr("value");
+            if (n && v && !params.count(*n)) {
+                params[*n] = *v;
+                from_default.insert(*n);
+            }
+            return true;
+        }
+        if (e.tag == "alias") {
+            const std::string *id = e.attr("id"), *as = e.attr("as");
+            auto it = id ? ids.find(*id) : ids.end();
+            if (it == ids.end()) return fail(file, e, "Referenced object '" + (id ? *id : std::string()) + "' not found!");
+            if (!as || ids.count(*as)) return fail(file, e, "Duplicate ID '" + *id + "' used in scene description!");
+            ids[*as] = it->second;
+            return true;
+        }
+        if (e.tag == "include") {
+            const std::string *fn = e.attr("filename");
+            if (!fn) return fail(file, e, "<include> without a filename");
+            const std::string p = (!fn->empty() && (*fn)[0] == '/') ? *fn : dir_of(file) + *fn;
+            return load(p, depth + 1);
+        }
+        const std::string *id = e.attr("id");
+        if (id && !id->empty() && e.tag != "ref" && e.tag != "scene") {
+            if (ids.count(*id)) return fail(file, e, "Duplicate ID '" + *id + "' used in scene description!");
+            ids[*id] = &e;
+        }
+        return true;
+    }
+};
+
+struct TreeBuilder {
+    const Loader &L;
     std::vector<mtsgpu_xml_node> nodes;
     std::vector<mtsgpu_xml_prop> props;
     std::string err;
 
-    explicit TreeBuilder(const XElem &r) : root(r) {
-        index(root);
-        for (auto &k : root.kids)
-            if (k->tag == "default" && k->attr("name") && k->attr("value")) defaults[*k->attr("name")] = *k->attr("value");
-    }
-    void index(const XElem &e) {
-        if (const std::string *id = e.attr("id"))
-            if (e.tag != "scene" && !ids.count(*id)) ids[*id] = &e;
-        for (auto &k : e.kids) index(*k);
-    }
-    // $name -> its <default> value (the loader's -D parameters are not known here)
-    bool subst(const std::string &v, std::string &out) {
-        out.clear();
-        for (size_t k = 0; k < v.size(); ++k) {
-            if (v[k] != '$') { out += v[k]; continue; }
-            size_t e = k + 1;
-            while (e < v.size() && (isalnum((unsigned char)v[e]) || v[e] == '_')) ++e;
-            const std::string n = v.substr(k + 1, e - k - 1);
-            auto it = defaults.find(n);
-            if (n.empty() || it == defaults.end()) { err = "unresolved parameter $" + n + " (no <default>)"; return false; }
-            out += it->second;
-            k = e - 1;
-        }
-        return true;
-    }
+    explicit TreeBuilder(const Loader &l) : L(l) {}
     static bool copy(char *dst, size_t cap, const std::string &v) {
         if (v.size() + 1 > cap) return false;
         std::memcpy(dst, v.c_str(), v.size() + 1);
@@ -206,14 +305,14 @@ struct TreeBuilder {
             const std::string *nm = k->attr("name");
             std::string val;
             const std::string *v = k->attr("value");
-            if (v && !subst(*v, val)) return false;
-            if (!v && (t == "point" || t == "vector")) {   // x/y/z form
-                std::string x, y, z;
-                if (!subst(k->attr("x") ? *k->attr("x") : "0", x) || !subst(k->attr("y") ? *k->attr("y") : "0", y) ||
-                    !subst(k->attr("z") ? *k->attr("z") : "0", z))
-                    return false;
-                val = x + ", " + y + ", " + z;
-            } else if (!v) {
+            if (v) {
+                val = *v;
+                p.flags = k->attr_flags("value");
+            } else if (t == "point" || t == "vector") {   // x/y/z form
+                auto xyz = [&](const char *a) { return k->attr(a) ? *k->attr(a) : std::string("0"); };
+                val = xyz("x") + ", " + xyz("y") + ", " + xyz("z");
+                p.flags = k->attr_flags("x") | k->attr_flags("y") | k->attr_flags("z");
+            } else {
                 err = "<" + t + "> in <" + e.tag + " type=\"" + *type + "\"> has no value (not supported here)";
                 return false;
             }
@@ -232,47 +331,76 @@ struct TreeBuilder {
             if (t == "bsdf" || t == "texture") {
                 if (!node(*k, self, cname, depth + 1)) return false;
             } else if (t == "ref") {
-                const std::string *rid = k->attr("id");
-                auto it = rid ? ids.find(*rid) : ids.end();
-                if (it == ids.end()) { err = "Unable to find object with id \"" + (rid ? *rid : std::string()) + "\""; return false; }
-                if (it->second->tag != "bsdf" && it->second->tag != "texture") {
-                    err = "<ref id=\"" + *rid + "\"> in a BSDF names a <" + it->second->tag + ">";
+                const XElem *r = resolve(*k);
+                if (!r) return false;
+                if (r->tag != "bsdf" && r->tag != "texture") {
+                    err = "<ref id=\"" + *k->attr("id") + "\"> in a BSDF names a <" + r->tag + ">";
                     return false;
                 }
-                if (!node(*it->second, self, cname, depth + 1)) return false;
+                if (!node(*r, self, cname, depth + 1)) return false;
             }
         }
         return true;
+    }
+    const XElem *resolve(const XElem &ref) {
+        const std::string *rid = ref.attr("id");
+        auto it = rid ? L.ids.find(*rid) : L.ids.end();
+        if (it == L.ids.end()) {
+            err = "Referenced object '" + (rid ? *rid : std::string()) + "' not found!";
+            return nullptr;
+        }
+        return it->second;
     }
 };
 
 }  // namespace
 
-extern "C" int mtsgpu_xml_bsdf(const char *xml_path, const char *bsdf_id, mtsgpu_xml_node *nodes, int node_cap,
-                               mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props, char *err,
-                               size_t err_cap) {
+extern "C" int mtsgpu_xml_bsdf_ex(const char *xml_path, const char *id, int32_t lookup, const char *const *param_names,
+                                  const char *const *param_values, int32_t num_params, mtsgpu_xml_node *nodes,
+                                  int node_cap, mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props,
+                                  char *err, size_t err_cap) {
     auto fail = [&](int code, const std::string &m) {
-        if (err && err_cap) {
-            std::snprintf(err, err_cap, "%s", m.c_str());
-        }
+        if (err && err_cap) std::snprintf(err, err_cap, "%s", m.c_str());
         return code;
     };
-    if (!xml_path || !bsdf_id || !num_nodes || !num_props || node_cap < 0 || prop_cap < 0)
-        return fail(MTSGPU_EINVAL, "null argument");
+    if (!xml_path || !id || !num_nodes || !num_props || node_cap < 0 || prop_cap < 0 || num_params < 0 ||
+        (num_params > 0 && (!param_names || !param_values)) ||
+        (lookup != MTSGPU_XML_BY_ID && lookup != MTSGPU_XML_BY_SHAPE))
+        return fail(MTSGPU_EINVAL, "null or invalid argument");
     *num_nodes = *num_props = 0;
-    std::ifstream f(xml_path, std::ios::binary);
-    if (!f) return fail(MTSGPU_EINVAL, std::string("cannot read ") + xml_path);
-    std::stringstream ss;
-    ss << f.rdbuf();
-    const std::string src = ss.str();
-    XElem root;
-    XParser P(src);
-    if (!P.document(root)) return fail(MTSGPU_EINVAL, std::string(xml_path) + ": " + P.err);
-    TreeBuilder E(root);
-    auto it = E.ids.find(bsdf_id);
-    if (it == E.ids.end() || it->second->tag != "bsdf")
-        return fail(MTSGPU_EINVAL, std::string("no <bsdf id=\"") + bsdf_id + "\"> in " + xml_path);
-    if (!E.node(*it->second, -1, std::string(), 0)) return fail(MTSGPU_EINVAL, E.err);
+    Loader L;
+    for (int k = 0; k < num_params; ++k) {
+        if (!param_names[k] || !param_values[k]) return fail(MTSGPU_EINVAL, "null parameter name or value");
+        L.params[param_names[k]] = param_values[k];
+    }
+    if (!L.load(xml_path, 0)) return fail(MTSGPU_EINVAL, L.err);
+    TreeBuilder E(L);
+    auto it = L.ids.find(id);
+    const XElem *bsdf = nullptr;
+    if (lookup == MTSGPU_XML_BY_ID) {
+        if (it == L.ids.end()) return fail(MTSGPU_ENOENT, std::string("no element with id \"") + id + "\" in " + xml_path);
+        if (it->second->tag != "bsdf")
+            return fail(MTSGPU_EINVAL, std::string("id \"") + id + "\" names a <" + it->second->tag + ">, not a <bsdf>");
+        bsdf = it->second;
+    } else {
+        // the BSDF given inline (or by <ref>) inside the <shape> with this id
+        if (it == L.ids.end()) return fail(MTSGPU_ENOENT, std::string("no element with id \"") + id + "\" in " + xml_path);
+        if (it->second->tag != "shape")
+            return fail(MTSGPU_EINVAL, std::string("id \"") + id + "\" names a <" + it->second->tag + ">, not a <shape>");
+        for (auto &k : it->second->kids) {
+            const XElem *c = k.get();
+            if (c->tag == "ref") {
+                c = E.resolve(*c);
+                if (!c) return fail(MTSGPU_EINVAL, E.err);
+            }
+            if (c->tag == "bsdf") {
+                if (bsdf) return fail(MTSGPU_EINVAL, std::string("shape \"") + id + "\" has more than one BSDF");
+                bsdf = c;
+            }
+        }
+        if (!bsdf) return fail(MTSGPU_ENOENT, std::string("shape \"") + id + "\" has no <bsdf> in " + xml_path);
+    }
+    if (!E.node(*bsdf, -1, std::string(), 0)) return fail(MTSGPU_EINVAL, E.err);
     *num_nodes = (int)E.nodes.size();
     *num_props = (int)E.props.size();
     if ((int)E.nodes.size() > node_cap || (int)E.props.size() > prop_cap)
@@ -280,4 +408,11 @@ extern "C" int mtsgpu_xml_bsdf(const char *xml_path, const char *bsdf_id, mtsgpu
     if (nodes) std::memcpy(nodes, E.nodes.data(), E.nodes.size() * sizeof(mtsgpu_xml_node));
     if (props) std::memcpy(props, E.props.data(), E.props.size() * sizeof(mtsgpu_xml_prop));
     return MTSGPU_OK;
+}
+
+extern "C" int mtsgpu_xml_bsdf(const char *xml_path, const char *bsdf_id, mtsgpu_xml_node *nodes, int node_cap,
+                               mtsgpu_xml_prop *props, int prop_cap, int *num_nodes, int *num_props, char *err,
+                               size_t err_cap) {
+    return mtsgpu_xml_bsdf_ex(xml_path, bsdf_id, MTSGPU_XML_BY_ID, nullptr, nullptr, 0, nodes, node_cap, props,
+                              prop_cap, num_nodes, num_props, err, err_cap);
 }

@@ -32,7 +32,7 @@ EXPORTS = ['mtsgpu_create', 'mtsgpu_upload_scene', 'mtsgpu_film_border', 'mtsgpu
            'mtsgpu_group_render', 'mtsgpu_group_render_device', 'mtsgpu_group_member', 'mtsgpu_group_last_error',
            'mtsgpu_group_destroy', 'mtsgpu_trace_rays_ex', 'mtsgpu_debug_kdtree', 'mtsgpu_kdtree_host', 'mtsgpu_debug_libm',
            'mtsgpu_bvh_host', 'mtsgpu_group_member_params', 'mtsgpu_render_pixels',
-           'mtsgpu_xml_bsdf']
+           'mtsgpu_xml_bsdf', 'mtsgpu_xml_bsdf_ex']
 
 _lib = None
 
@@ -62,6 +62,9 @@ def load_library(path=None):
     L.mtsgpu_render_pixels.restype = C.c_uint64
     L.mtsgpu_xml_bsdf.argtypes = [C.c_char_p, C.c_char_p, P(abi.XmlNode), C.c_int, P(abi.XmlProp), C.c_int,
                                   P(C.c_int), P(C.c_int), C.c_char_p, C.c_size_t]
+    L.mtsgpu_xml_bsdf_ex.argtypes = [C.c_char_p, C.c_char_p, C.c_int32, P(C.c_char_p), P(C.c_char_p), C.c_int32,
+                                     P(abi.XmlNode), C.c_int, P(abi.XmlProp), C.c_int, P(C.c_int), P(C.c_int),
+                                     C.c_char_p, C.c_size_t]
     L.mtsgpu_render.argtypes = [C.c_void_p, P(abi.RenderParams), P(C.c_float), P(C.c_float), P(abi.Stats)]
     L.mtsgpu_render_device.argtypes = [C.c_void_p, P(abi.RenderParams), C.c_void_p, C.c_void_p, P(abi.Stats)]
     L.mtsgpu_last_error.argtypes = [C.c_void_p]

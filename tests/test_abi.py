@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(integrator.EXPORTS) <= set(names)
-    assert L.mtsgpu_abi_version() == abi.ABI_VERSION == 7
+    assert L.mtsgpu_abi_version() == abi.ABI_VERSION == 8
 
 
 STRUCTS = {'mtsgpu_bsdf_desc': abi.BsdfDesc, 'mtsgpu_emitter_desc': abi.EmitterDesc,
