@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """bench.py -- Msamples/s of the MI355X `path` integrator on BASELINE config C2,
-and on C3 (matpreview, BASELINE's second north-star scene) in the same run as
-the line's `secondary` block.
+and on C3 (matpreview, BASELINE's second north-star scene), C4 (the 200k-triangle
+atrium BASELINE names for tile sharding) and C5 (roughplastic with the
+rough-transmittance lookup) in the same run, as the line's `secondary` blocks
+(one per config, each with its own value, ms_per_step, roofline and CPU
+baseline).
 
 Workload (BASELINE.json configs[1]): Cornell box, 1280x720, 512 spp, sobol,
 path maxDepth=-1 rrDepth=5, box filter.  One step = one full frame
@@ -63,9 +66,9 @@ def parse_args(argv=None):
                          'of the N-rank path (tests only; never a measurement)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
-    ap.add_argument('--secondary', default='C3',
-                    help="second workload timed in the same run and emitted as the line's `secondary` block "
-                         "(BASELINE's north star names Cornell box and matpreview); 'none' to skip")
+    ap.add_argument('--secondary', default='C3,C4,C5',
+                    help="further workloads timed in the same run (comma-separated), each emitted as a block of "
+                         "the line's `secondary` object; 'none' to skip")
     return ap.parse_args(argv)
 
 
@@ -460,9 +463,11 @@ def main():
         assert dist.get_world_size() == world == args.gpus, (dist.get_world_size(), world, args.gpus)
 
     main_res = run_workload(args.config, args, world, rank, local, dist, torch, lib_hash)
-    second = None
-    if args.secondary and args.secondary.lower() != 'none' and args.secondary != args.config and not args.size:
-        second = run_workload(args.secondary, args, world, rank, local, dist, torch, lib_hash)
+    second = {}
+    if args.secondary and args.secondary.lower() != 'none' and not args.size:
+        for cfg in [c.strip() for c in args.secondary.split(',') if c.strip()]:
+            if cfg != args.config and cfg not in second:
+                second[cfg] = run_workload(cfg, args, world, rank, local, dist, torch, lib_hash)
 
     if rank == 0:
         m = main_res
@@ -477,12 +482,12 @@ def main():
             'roofline': m['roofline'],
             'cpu_baseline': m['cpu_baseline'],
         }
-        if second is not None:
-            out['secondary'] = {
-                'metric': 'Msamples/s (and s/frame) at %d spp, %dx%d' % (second['spp'], second['W'], second['H']),
-                'value': second['value'], 'unit': 'Msamples/s', 'ms_per_step': second['ms_per_step'],
-                'steps': args.steps, 'warmup': args.warmup, 'config': second['config'],
-                'roofline': second['roofline'], 'cpu_baseline': second['cpu_baseline']}
+        if second:
+            out['secondary'] = {cfg: {
+                'metric': 'Msamples/s (and s/frame) at %d spp, %dx%d' % (r['spp'], r['W'], r['H']),
+                'value': r['value'], 'unit': 'Msamples/s', 'ms_per_step': r['ms_per_step'],
+                'steps': args.steps, 'warmup': args.warmup, 'config': r['config'],
+                'roofline': r['roofline'], 'cpu_baseline': r['cpu_baseline']} for cfg, r in second.items()}
         if not gpu:
             out['device'] = 'cpu-oracle launcher rehearsal (not a GPU measurement)'
         elif args.share_device:
