@@ -42,7 +42,6 @@ hipError_t mtsg_launch_wf_trace(const MtsgLaunch &L, const MtsgWave &W, unsigned
 hipError_t mtsg_launch_wf_flush(const unsigned long long *part, uint32_t blocks, unsigned long long *counters,
                                 hipStream_t s);
 int mtsg_wf_occupancy(const MtsgLaunch &L, int wk, bool ggx, int *shadeBpc, int *traceBpc);
-bool mtsg_wf_trace_dynamic(const MtsgLaunch &L);
 int mtsg_path_features(const MtsgLaunch &L);
 // the wavefront's trace kernel forms the whole hit record (MTSGPU_WF_HITREC=1; A/B in DESIGN.md 4)
 static bool wf_hitrec_on() {
@@ -96,7 +95,7 @@ struct mtsgpu_ctx {
     DevBuf film_own, film_spill, samples, counters, contrib;
     DevBuf dev_in, dev_out;   // staging of mtsgpu_develop (host film -> developed image)
     // wavefront pipeline: path slots, ray queues and results, counters
-    DevBuf wf_state, wf_ray, wf_rslot, wf_cls, wf_cnt, wf_hit, wf_hitrec, wf_occl, wf_live, wf_fetch, wf_ovf, wf_part, wf_kind;
+    DevBuf wf_state, wf_ray, wf_rslot, wf_cls, wf_cnt, wf_hit, wf_hitrec, wf_occl, wf_live, wf_ovf, wf_part, wf_kind;
     DevBuf rp_order, rp_start, rp_sfmt;   // SFMT replay: render order, unit starts, streams
     // the reference's SAH kd-tree (kdtree_build.cpp), built on first use
     bool kd_built = false;
@@ -340,7 +339,6 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     W.hit = (float4 *)ctx->wf_hit.p;
     W.occl = (uint32_t *)ctx->wf_occl.p;
     W.live = (uint32_t *)ctx->wf_live.p;
-    W.fetch = (uint32_t *)ctx->wf_fetch.p;
     W.ovf = (uint2 *)ctx->wf_ovf.p;
     W.shape_kind = (const uint32_t *)ctx->wf_kind.p;
     W.slots = slots;
@@ -355,7 +353,6 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     for (int k = 0; k < MTSG_WK_KINDS; ++k) partBlocks = std::max(partBlocks, plan.shadeGrid[k]);
     if ((e = hipMemsetAsync(ctx->wf_cnt.p, 0, (size_t)2 * MTSG_WF_QUEUES * R * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(ctx->wf_live.p, 0, 2 * 4, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(ctx->wf_fetch.p, 0, 2 * 4, stream)) != hipSuccess ||
         (e = hipMemsetAsync(part, 0, (size_t)partBlocks * 16 * 8, stream)) != hipSuccess)
         return hip_fail(ctx, e, "wavefront reset");
     constexpr int POLL = 4, LAG = 2, RING = 8;
@@ -811,12 +808,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         for (int k = 0; k < MTSG_WK_KINDS; ++k)
             if (plan.kinds[k]) plan.shadeGrid[k] = (int)(plan.slots / BLOCK_THREADS);
         plan.traceGrid = (int)(2 * (uint64_t)plan.slots / BLOCK_THREADS);
-        if (mtsg_wf_trace_dynamic(L)) {   // persistent: every resident block, no more
-            int sb = 0, tb = 0;
-            mtsg_wf_occupancy(L, -1, false, &sb, &tb);
-            plan.traceGrid = std::max(1, ctx->num_cus * tb);
-        }
-        plan.hitrec = wf_hitrec_on() && !mtsg_wf_trace_dynamic(L);
+        plan.hitrec = wf_hitrec_on();
         const size_t slots = plan.slots, cap = slots;
         const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
         int partBlocks = plan.traceGrid;
@@ -830,7 +822,6 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             (plan.hitrec && (e = ctx->wf_hitrec.ensure(slots * MTSG_WF_HIT_VECS * 16)) != hipSuccess) ||
             (e = ctx->wf_occl.ensure(slots * 4)) != hipSuccess ||
             (e = ctx->wf_live.ensure(2 * 4)) != hipSuccess ||
-            (e = ctx->wf_fetch.ensure(2 * 4)) != hipSuccess ||
             (e = ctx->wf_ovf.ensure((size_t)plan.traceGrid * BLOCK_THREADS * ovfDepth * 8)) != hipSuccess ||
             (e = ctx->wf_part.ensure((size_t)partBlocks * 16 * 8)) != hipSuccess ||
             (e = upload(ctx->wf_kind, shapeKind, stream)) != hipSuccess)
@@ -966,7 +957,7 @@ void mtsgpu_destroy(mtsgpu_ctx *ctx) {
                       &ctx->env, &ctx->env_texels, &ctx->env_rows, &ctx->env_cols, &ctx->env_weights, &ctx->env_grows, &ctx->env_gcols,
                       &ctx->rtrans, &ctx->texcoords, &ctx->qrays, &ctx->qhits,
                       &ctx->dev_in, &ctx->dev_out, &ctx->wf_state, &ctx->wf_ray, &ctx->wf_rslot, &ctx->wf_cls,
-                      &ctx->wf_cnt, &ctx->wf_hit, &ctx->wf_hitrec, &ctx->wf_occl, &ctx->wf_live, &ctx->wf_fetch, &ctx->wf_ovf, &ctx->wf_part, &ctx->wf_kind, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
+                      &ctx->wf_cnt, &ctx->wf_hit, &ctx->wf_hitrec, &ctx->wf_occl, &ctx->wf_live, &ctx->wf_ovf, &ctx->wf_part, &ctx->wf_kind, &ctx->rp_order, &ctx->rp_start, &ctx->rp_sfmt, &ctx->env_grows, &ctx->env_gcols};
     for (DevBuf *b : bufs) b->release();
     for (hipEvent_t &e : ctx->wf_ev)
         if (e) (void)hipEventDestroy(e);

@@ -130,34 +130,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             hit = hit && okC;
             occluded = occluded && okS;
         } else {
-#ifdef MTSG_SEQ_TRAVERSAL
-        // (opt-in) large scenes: both rays of the bounce through one per-lane loop
-        // (dpath.h traverse_seq): bit-identical, but lost C3 -5.5%, C4 -10%, C5 -1.7%
-        // (profiles/r04_ab_seq_traversal.log; C4's kernel spills 35 VGPRs instead of 6)
-        if constexpr (!SCENE_LDS) {
-        bool doS = false, doC = false;
-        float minS = 0, maxS = 0, minC = 0, maxC = 0;
-        if (st.active && st.haveShadow) {
-            c.shadow++;
-            // a shadow ray whose estimate is zero cannot change Li: skip its traversal
-            doS = !is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, minS, maxS);
-        }
-        if (st.active && st.haveRay) {
-            c.rays++;
-            doC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
-        }
-        if constexpr (HNODES)
-            traverse_seq<STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, doS, st.P.its.p, st.sd, minS, maxS, doC,
-                                     st.ro, st.rd, minC, maxC, stkN, stkD, occluded, hit, slot, hu, hv, ht, c.nodes,
-                                     c.tests, S.analytic);
-        else
-            traverse_seq<STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, doS, st.P.its.p, st.sd, minS, maxS, doC,
-                                     st.ro, st.rd, minC, maxC, stkN, stkD, occluded, hit, slot, hu, hv, ht, c.nodes,
-                                     c.tests, S.analytic);
-        if (hit) prim = S.tris[slot].prim;
-        MK_STAMP(mkT[1], mkT0);
-        } else {
-#endif
+        // (round 4 measured both rays of a bounce through one per-lane loop, traverse_seq:
+        // bit-identical, but C3 -5.5%, C4 -10%, C5 -1.7%, profiles/r04_ab_seq_traversal.log; removed)
         if (st.active && st.haveShadow) {
             c.shadow++;
             float mint, maxt;
@@ -202,9 +176,6 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             }
             if (hit) prim = SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
         }
-#ifdef MTSG_SEQ_TRAVERSAL
-        }
-#endif
         }
         if (st.active && st.haveShadow) {   // scan_pair case
             if (!occluded) st.P.L = add(st.P.L, st.P.neeC);

@@ -219,24 +219,13 @@ __device__ __forceinline__ float dist_up16(uint16_t h) { return __uint_as_float(
 // LDSK > 0: the first LDSK stack entries live in LDS, deeper ones in a per-lane
 // global array `ovf` ({node, distance} pairs): a short LDS stack keeps the
 // traversal kernel's LDS per lane small (wf_trace occupancy); 0: all in LDS
-// RTOP (MTSG_REG_TOP=1, opt-in): the stack's top entry is cached in two
-// registers, so the pop that follows a push (depth-first: the far child after
-// the near subtree) reads no LDS; deeper entries live in LDS as before.
-// Bit-identical, but lost C2 -0.9%, C3 -4.2%, C4 -5.2%, C5 -3.9%
-// (profiles/r04_ab_reg_top.log): the node loop's extra selects cost more than
-// the LDS reads it saves.
-#ifndef MTSG_REG_TOP
-#define MTSG_REG_TOP 0
-#endif
+// (Round 4 measured the stack's top entry cached in two registers: bit-identical,
+// but C2 -0.9%, C3 -4.2%, C4 -5.2%, C5 -3.9%, profiles/r04_ab_reg_top.log; removed.)
 template <bool ANY, bool STATS, bool ANA = false, int LDSK = 0, typename NodeT, typename TriT>
 __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f3 d, float mint, float maxt,
                                          lds_stk_n *stkN, lds_stk_d *stkD, uint32_t &bestSlot, float &bu, float &bv,
                                          float &bt, unsigned long long &nodes, unsigned long long &tests,
                                          const MtsgAnalytic *anaArr = nullptr, uint2 *ovf = nullptr) {
-    constexpr bool RTOP = MTSG_REG_TOP && LDSK == 0;
-    bool cached = false;
-    int topN = 0;
-    uint16_t topD = 0;
     typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
     const float ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
     const float iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
@@ -251,10 +240,7 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
     auto pop = [&]() -> int {
         while (sp > 0) {
             --sp;
-            if (RTOP && cached) {
-                cached = false;
-                if (ANY || dist_up16(topD) <= bt) return topN;
-            } else if (LDSK == 0 || sp < LDSK) {
+            if (LDSK == 0 || sp < LDSK) {
                 if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
             } else {
                 const uint2 e = ovf[sp - LDSK];
@@ -286,15 +272,7 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
                 int nearC = ec0, farC = ec1;
                 float farT = n1;
                 if (n1 < n0) { nearC = ec1; farC = ec0; farT = n0; }
-                if (RTOP) {
-                    if (cached) {   // the cached top moves down to LDS
-                        stkN[(sp - 1) * BLOCK] = topN;
-                        stkD[(sp - 1) * BLOCK] = topD;
-                    }
-                    topN = farC;
-                    topD = dist_down16(farT);
-                    cached = true;
-                } else if (LDSK == 0 || sp < LDSK) {
+                if (LDSK == 0 || sp < LDSK) {
                     stkN[sp * BLOCK] = farC;
                     stkD[sp * BLOCK] = dist_down16(farT);
                 } else {
@@ -373,162 +351,6 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         }
     }
     return found;
-}
-
-// A bounce's two rays -- the pending shadow ray (any hit) and the next
-// closest-hit ray -- through one per-lane traversal loop: a lane whose shadow
-// ray is resolved starts its closest-hit ray in the same loop instead of
-// waiting at the end of the shadow traversal for the slowest lane of its wave
-// (the wave then runs max(shadow + closest) traversal steps instead of
-// max(shadow) + max(closest)).  Each ray is traversed exactly as by
-// traverse() (same node order, speculative leaf parking, culling, tie rule),
-// so occlusion and the hit record are the same.
-template <bool STATS, bool ANA, typename NodeT, typename TriT>
-__device__ __forceinline__ void traverse_seq(NodeT *nodesArr, TriT *trisArr, bool doS, f3 os, f3 dS, float sMin,
-                                             float sMax, bool doC, f3 oc, f3 dC, float cMin, float cMax,
-                                             lds_stk_n *stkN, lds_stk_d *stkD, bool &occluded, bool &hitC,
-                                             uint32_t &bestSlot, float &bu, float &bv, float &bt,
-                                             unsigned long long &nodes, unsigned long long &tests,
-                                             const MtsgAnalytic *anaArr) {
-    typedef typename std::conditional<std::is_same<NodeT, lds_node>::value, lds_f4, glb_f4>::type F4;
-    constexpr int DONE = 0x7fffffff;
-    int phase = doS ? 0 : doC ? 1 : 2;   // 0: shadow ray, 1: closest-hit ray, 2: done
-    f3 o = phase == 0 ? os : oc, d = phase == 0 ? dS : dC;
-    float mint = phase == 0 ? sMin : cMin;
-    bt = phase == 0 ? sMax : cMax;
-    float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0;
-    auto setup = [&]() {
-        ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
-        iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
-        iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
-        ox = o.x * ix; oy = o.y * iy; oz = o.z * iz;
-    };
-    setup();
-    bool found = false;
-    uint32_t bestPrim = 0;
-    int sp = 0;
-    int node = phase < 2 ? 0 : DONE, leaf = 0;
-    occluded = false;
-    hitC = false;
-    auto pop = [&]() -> int {
-        while (sp > 0) {
-            --sp;
-            if (dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
-        }
-        return DONE;
-    };
-    while (phase < 2) {
-        // inner nodes (traverse())
-        while ((uint32_t)node < (uint32_t)DONE) {
-            if (STATS) nodes++;
-            vf4 a, b, c;
-            int ec0, ec1;
-            load_node(nodesArr + node, a, b, c, ec0, ec1);
-            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
-            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
-            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
-            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
-            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
-            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
-            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
-            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
-            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
-            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
-            const bool h0 = n0 <= f0, h1 = n1 <= f1;
-            if (h0 && h1) {
-                int nearC = ec0, farC = ec1;
-                float farT = n1;
-                if (n1 < n0) { nearC = ec1; farC = ec0; farT = n0; }
-                stkN[sp * BLOCK] = farC;
-                stkD[sp * BLOCK] = dist_down16(farT);
-                ++sp;
-                node = nearC;
-            } else if (h0) {
-                node = ec0;
-            } else if (h1) {
-                node = ec1;
-            } else {
-                node = pop();
-            }
-            if (node < 0 && leaf == 0) {   // park the first leaf reached and keep descending
-                leaf = node;
-                node = pop();
-            }
-            if (!__any(leaf == 0)) break;
-        }
-        // leaves
-        bool occl = false;
-        while (leaf < 0) {
-            const uint32_t ref = (uint32_t)(~leaf);
-            const uint32_t first = ref >> 4, end = first + (ref & 15u);
-            for (uint32_t i = first; i < end; ++i) {
-                if (STATS) tests++;
-                TriT *tr = trisArr + i;
-                const vf4 q0 = *reinterpret_cast<F4 *>(&tr->k);
-                const vf4 q1 = *reinterpret_cast<F4 *>(&tr->a_u);
-                const vf4 q2 = *reinterpret_cast<F4 *>(&tr->c_nu);
-                const uint32_t k = __float_as_uint(q0.x);
-                float o_u, o_v, o_k, d_u, d_v, d_k;
-                if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
-                else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
-                else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-                else {
-                    if constexpr (ANA) {
-                        float at, alx, aly;
-                        if (k == MTSG_K_ANALYTIC) {
-                            const GAna &an = ((GAna *)anaArr)[__float_as_uint(q0.y)];
-                            const bool h = phase == 0 ? ana_intersect<true>(an, o, d, mint, bt, at, alx, aly)
-                                                      : ana_intersect<false>(an, o, d, mint, bt, at, alx, aly);
-                            if (h) {
-                                if (phase == 0) { occl = true; break; }
-                                const uint32_t prim = __float_as_uint(q2.z);
-                                if (!found || at < bt || prim > bestPrim) {
-                                    found = true; bestPrim = prim; bestSlot = i; bt = at; bu = alx; bv = aly;
-                                }
-                            }
-                        }
-                    }
-                    continue;
-                }
-                const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
-                const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
-                const float c_nu = q2.x, c_nv = q2.y;
-                const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
-                if (t < mint || t > bt) continue;
-                const float hu = o_u + t * d_u - a_u;
-                const float hv = o_v + t * d_v - a_v;
-                const float u = hv * b_nu + hu * b_nv;
-                const float v = hu * c_nu + hv * c_nv;
-                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
-                    if (phase == 0) { occl = true; break; }
-                    const uint32_t prim = __float_as_uint(q2.z);
-                    if (!found || t < bt || prim > bestPrim) {   // ties: the larger primitive index
-                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
-                    }
-                }
-            }
-            if (occl) { node = DONE; leaf = 0; break; }
-            leaf = 0;
-            if (node < 0) {   // the next stack entry is a leaf too: take it now
-                leaf = node;
-                node = pop();
-            }
-        }
-        if (node == DONE && leaf == 0) {   // this ray is resolved: the shadow ray hands over to the closest-hit ray
-            if (phase == 0) {
-                occluded = occl;
-                phase = doC ? 1 : 2;
-                if (phase == 1) {
-                    o = oc; d = dC; mint = cMin; bt = cMax;
-                    setup();
-                    found = false; bestPrim = 0; sp = 0; node = 0;
-                }
-            } else {
-                hitC = found;
-                phase = 2;
-            }
-        }
-    }
 }
 
 typedef __attribute__((address_space(4))) const MtsgTri cst_tri;

@@ -251,7 +251,6 @@ struct MtsgWave {
     float4 *hit;                      // [slots] {t, u, v, prim (TriAccel slot with analytic shapes) | MTSG_WF_NONE}
     uint32_t *occl;                   // [slots] shadow results
     uint32_t *live;                   // [2 parities] live slots after the bounce's shade kernels
-    uint32_t *fetch;                  // [2 parities] queue entries taken by wf_trace_dyn
     uint2 *ovf;                       // trace stack overflow: [trace lanes][ovf_depth]
     const uint32_t *shape_kind;       // [shapes] MTSG_WK_* of the shape's BSDF
     uint32_t slots, cap;

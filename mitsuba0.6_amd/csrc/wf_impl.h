@@ -421,245 +421,9 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
 }
 
 
-// ---------------------------------------------------------------------------
-// the trace kernel with dynamic ray fetch (Aila & Laine 2009: persistent
-// while-while, terminated rays replaced).  A persistent grid; each lane holds
-// one ray of the bounce's queues at a time and, once a quarter of its wave is
-// idle (MTSG_WF_FETCH_MIN lanes), the idle lanes take the next queue entries
-// with one atomic per wave.  The lanes of a wave then stay busy although the
-// rays' traversal lengths differ several-fold (incoherent bounces), where the
-// one-ray-per-thread kernel idles a lane from its ray's end to the wave's last.
-// Each ray is traversed in the same depth-first order as traverse(), so every
-// hit record (tie rule included) equals wf_trace's.  BVH in HBM (HN: the
-// half-float node copy), LDS stack of MTSG_WF_LDS_STACK entries per lane.
-// ---------------------------------------------------------------------------
-#ifndef MTSG_WF_FETCH_MIN
-#define MTSG_WF_FETCH_MIN 16
-#endif
-#ifndef MTSG_WF_DYN_WAVES
-#define MTSG_WF_DYN_WAVES 6           // 80 VGPRs: the lane's ray state stays in registers (8: 64, 45 spilled)
-#endif
-template <bool STATS, bool ANA, bool HN>
-__global__ __launch_bounds__(BLOCK, MTSG_WF_DYN_WAVES) void wf_trace_dyn(MtsgLaunch L, MtsgWave W,
-                                                                           unsigned long long *part) {
-    typedef typename std::conditional<HN, glb_hnode, glb_node>::type NodeT;
-    extern __shared__ uint32_t lds[];
-    __shared__ uint32_t red[BLOCK / 64 * 16];
-    const MtsgDeviceScene &S = L.scene;
-    const uint32_t p = W.parity, region = blockIdx.x % WF_R, lane = lane_id();
-    if (blockIdx.x == 0) {
-        // as wf_trace, and the other parity's fetch counter (its trace is over)
-        if (threadIdx.x < MTSG_WK_KINDS * WF_R) wf_cnt(W, p, 2)[threadIdx.x] = 0;
-        else if (threadIdx.x < MTSG_WK_KINDS * WF_R + 2 * WF_R) wf_cnt(W, p ^ 1u, 0)[threadIdx.x - MTSG_WK_KINDS * WF_R] = 0;
-        else if (threadIdx.x == MTSG_WK_KINDS * WF_R + 2 * WF_R) W.live[p ^ 1u] = 0;
-        else if (threadIdx.x == MTSG_WK_KINDS * WF_R + 2 * WF_R + 1) W.fetch[p ^ 1u] = 0;
-    }
-    QueueView Qc, Qs;
-    Qc.load(wf_cnt(W, p, 0));
-    Qs.load(wf_cnt(W, p, 1));
-    const uint32_t nc = Qc.total(), n = nc + Qs.total();
-    const uint32_t K = L.stack_depth < MTSG_WF_LDS_STACK ? L.stack_depth : MTSG_WF_LDS_STACK;
-    lds_stk_n *stkN = (lds_stk_n *)lds + threadIdx.x;
-    lds_stk_d *stkD = (lds_stk_d *)(lds + K * BLOCK) + threadIdx.x;
-    uint2 *ovf = W.ovf + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * W.ovf_depth;
-    NodeT *nodesArr = HN ? (NodeT *)S.hnodes : (NodeT *)S.nodes;
-    glb_tri *trisArr = (glb_tri *)S.tris;
-    const float4 *rays = W.ray[p];
-    const uint32_t *rslot = W.rslot[p];
-    uint32_t *next = W.cls[p ^ 1u];
-    unsigned long long cN = 0, cT = 0;
-    constexpr int DONE = 0x7fffffff;
-    // the lane's ray
-    bool alive = false, shadow = false, found = false, drained = false;
-    uint32_t s = 0, bestPrim = 0, bestSlot = 0;
-    f3 o = mk(0, 0, 0), d = mk(0, 0, 1);
-    float ix = 0, iy = 0, iz = 0, ox = 0, oy = 0, oz = 0, mint = 0, bt = 0, bu = 0, bv = 0;
-    int node = DONE, leaf = 0, sp = 0;
-    auto pop = [&]() -> int {
-        while (sp > 0) {
-            --sp;
-            if (sp < MTSG_WF_LDS_STACK) {
-                if (dist_up16(stkD[sp * BLOCK]) <= bt) return stkN[sp * BLOCK];
-            } else {
-                const uint2 e = ovf[sp - MTSG_WF_LDS_STACK];
-                if (dist_up16((uint16_t)e.y) <= bt) return (int)e.x;
-            }
-        }
-        return DONE;
-    };
-    while (true) {
-        // ---- refill the idle lanes once enough of them are idle
-        if (!drained) {
-            const unsigned long long idle = __ballot(!alive);
-            const uint32_t cnt = (uint32_t)__popcll(idle);
-            if (cnt >= MTSG_WF_FETCH_MIN || cnt == 64u) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                const int leader = __builtin_ctzll(idle);
-                uint32_t base = 0;
-                if ((int)lane == leader) base = atomicAdd(W.fetch + p, cnt);
-                base = __shfl(base, leader);
-                drained = base + cnt >= n;
-                const uint32_t i = base + rank;
-                if (!alive && i < n) {
-                    shadow = i >= nc;
-                    const size_t k = shadow ? (size_t)WF_R * W.cap + Qs.pos(i - nc, W.cap) : Qc.pos(i, W.cap);
-                    const float4 a = rays[2 * k], b = rays[2 * k + 1];
-                    s = rslot[k];
-                    o = mk(a.x, a.y, a.z);
-                    d = mk(b.x, b.y, b.z);
-                    mint = a.w;
-                    bt = b.w;
-                    ix = (d.x == 0.0f) ? copysignf(1e30f, d.x) : 1.0f / d.x;
-                    iy = (d.y == 0.0f) ? copysignf(1e30f, d.y) : 1.0f / d.y;
-                    iz = (d.z == 0.0f) ? copysignf(1e30f, d.z) : 1.0f / d.z;
-                    ox = o.x * ix; oy = o.y * iy; oz = o.z * iz;
-                    found = false;
-                    bestPrim = 0;
-                    node = 0;
-                    leaf = 0;
-                    sp = 0;
-                    alive = true;
-                }
-            }
-        }
-        if (!__any(alive)) {
-            if (drained) break;
-            continue;
-        }
-        // ---- inner nodes: descend until every busy lane holds a leaf (traverse())
-        while (alive && (uint32_t)node < (uint32_t)DONE) {
-            if (STATS) cN++;
-            vf4 a, b, c;
-            int ec0, ec1;
-            load_node(nodesArr + node, a, b, c, ec0, ec1);
-            const float t0x = __builtin_fmaf(a.x, ix, -ox), t1x = __builtin_fmaf(a.y, ix, -ox);
-            const float t0y = __builtin_fmaf(a.z, iy, -oy), t1y = __builtin_fmaf(a.w, iy, -oy);
-            const float t0z = __builtin_fmaf(c.x, iz, -oz), t1z = __builtin_fmaf(c.y, iz, -oz);
-            const float n0 = fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fmaxf(fminf(t0z, t1z), mint));
-            const float f0 = fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fminf(fmaxf(t0z, t1z), bt));
-            const float u0x = __builtin_fmaf(b.x, ix, -ox), u1x = __builtin_fmaf(b.y, ix, -ox);
-            const float u0y = __builtin_fmaf(b.z, iy, -oy), u1y = __builtin_fmaf(b.w, iy, -oy);
-            const float u0z = __builtin_fmaf(c.z, iz, -oz), u1z = __builtin_fmaf(c.w, iz, -oz);
-            const float n1 = fmaxf(fmaxf(fminf(u0x, u1x), fminf(u0y, u1y)), fmaxf(fminf(u0z, u1z), mint));
-            const float f1 = fminf(fminf(fmaxf(u0x, u1x), fmaxf(u0y, u1y)), fminf(fmaxf(u0z, u1z), bt));
-            const bool h0 = n0 <= f0, h1 = n1 <= f1;
-            if (h0 && h1) {
-                int nearC = ec0, farC = ec1;
-                float farT = n1;
-                if (n1 < n0) { nearC = ec1; farC = ec0; farT = n0; }
-                if (sp < MTSG_WF_LDS_STACK) {
-                    stkN[sp * BLOCK] = farC;
-                    stkD[sp * BLOCK] = dist_down16(farT);
-                } else {
-                    ovf[sp - MTSG_WF_LDS_STACK] = make_uint2((uint32_t)farC, dist_down16(farT));
-                }
-                ++sp;
-                node = nearC;
-            } else if (h0) {
-                node = ec0;
-            } else if (h1) {
-                node = ec1;
-            } else {
-                node = pop();
-            }
-            if (node < 0 && leaf == 0) {   // park the first leaf reached and keep descending
-                leaf = node;
-                node = pop();
-            }
-            if (!__any(leaf == 0)) break;
-        }
-        // ---- leaves (traverse()'s TriAccel / analytic tests; a shadow ray ends at its first hit)
-        while (alive && leaf < 0) {
-            const uint32_t ref = (uint32_t)(~leaf);
-            const uint32_t first = ref >> 4, end = first + (ref & 15u);
-            bool occl = false;
-            for (uint32_t i = first; i < end; ++i) {
-                if (STATS) cT++;
-                glb_tri *tr = trisArr + i;
-                const vf4 q0 = *reinterpret_cast<glb_f4 *>(&tr->k);
-                const vf4 q1 = *reinterpret_cast<glb_f4 *>(&tr->a_u);
-                const vf4 q2 = *reinterpret_cast<glb_f4 *>(&tr->c_nu);
-                const uint32_t k = __float_as_uint(q0.x);
-                float o_u, o_v, o_k, d_u, d_v, d_k;
-                if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
-                else if (k == 1) { o_u = o.z; o_v = o.x; o_k = o.y; d_u = d.z; d_v = d.x; d_k = d.y; }
-                else if (k == 2) { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
-                else {
-                    if constexpr (ANA) {
-                        float at, alx, aly;
-                        if (k == MTSG_K_ANALYTIC) {
-                            const GAna &an = ((GAna *)S.analytic)[__float_as_uint(q0.y)];
-                            const bool h = shadow ? ana_intersect<true>(an, o, d, mint, bt, at, alx, aly)
-                                                  : ana_intersect<false>(an, o, d, mint, bt, at, alx, aly);
-                            if (h) {
-                                if (shadow) { occl = true; break; }
-                                const uint32_t prim = __float_as_uint(q2.z);
-                                if (!found || at < bt || prim > bestPrim) {
-                                    found = true; bestPrim = prim; bestSlot = i; bt = at; bu = alx; bv = aly;
-                                }
-                            }
-                        }
-                    }
-                    continue;
-                }
-                const float n_u = q0.y, n_v = q0.z, n_d = q0.w;
-                const float a_u = q1.x, a_v = q1.y, b_nu = q1.z, b_nv = q1.w;
-                const float c_nu = q2.x, c_nv = q2.y;
-                const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
-                if (t < mint || t > bt) continue;
-                const float hu = o_u + t * d_u - a_u;
-                const float hv = o_v + t * d_v - a_v;
-                const float u = hv * b_nu + hu * b_nv;
-                const float v = hu * c_nu + hv * c_nv;
-                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
-                    if (shadow) { occl = true; break; }
-                    const uint32_t prim = __float_as_uint(q2.z);
-                    if (!found || t < bt || prim > bestPrim) {   // ties: the larger primitive index
-                        found = true; bestPrim = prim; bestSlot = i; bt = t; bu = u; bv = v;
-                    }
-                }
-            }
-            if (occl) { found = true; node = DONE; leaf = 0; break; }
-            leaf = 0;
-            if (node < 0) {   // the next stack entry is a leaf too: take it now
-                leaf = node;
-                node = pop();
-            }
-        }
-        // ---- finished rays: results by slot, closest-hit slots into the next bounce's kind queues
-        const bool fin = alive && node == DONE && leaf == 0;
-        uint32_t kind = MTSG_WK_KINDS;
-        if (fin) {
-            alive = false;
-            if (shadow) {
-                W.occl[s] = found ? 1u : 0u;
-            } else {
-                uint32_t w = MTSG_WF_NONE, shape = 0;
-                if (found) {
-                    const uint2 ps = *reinterpret_cast<const uint2 *>(&S.tris[bestSlot].prim);   // prim, shape
-                    w = ANA ? bestSlot : ps.x;
-                    shape = ps.y;
-                }
-                W.hit[s] = make_float4(bt, bu, bv, __uint_as_float(w));
-                kind = found ? W.shape_kind[shape] : (uint32_t)MTSG_WK_MISS;
-            }
-        }
-        if (__any(kind < MTSG_WK_KINDS)) {
-#pragma unroll
-            for (uint32_t q = 0; q < MTSG_WK_KINDS; ++q) {
-                const uint32_t pos = wave_append(wf_cnt(W, p ^ 1u, 2 + q) + region, kind == q);
-                if (kind == q) next[((size_t)q * WF_R + region) * W.cap + pos] = s;
-            }
-        }
-    }
-    if (STATS) {
-        uint32_t v[16] = {};
-        v[4] = (uint32_t)cN;
-        v[5] = (uint32_t)cT;
-        block_counters(part, v, red);
-    }
-}
+// (Round 4 measured a persistent trace kernel with dynamic ray fetch, Aila & Laine's
+// while-while with terminated rays replaced: bit-identical, but C3 604 -> 489,
+// C4 172 -> 149, C5 607 -> 497 Msamples/s, profiles/r04_ab_wf_dyn.log; removed.)
 
 // waves per SIMD each shade kind is compiled for
 #ifndef MTSG_WF_WAVES_MISS

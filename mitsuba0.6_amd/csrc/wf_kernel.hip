@@ -23,16 +23,10 @@ __global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsign
 // host-side launchers (capi.cpp)
 // ---------------------------------------------------------------------------
 size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) { return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16) * 4; }
-bool mtsg_wf_trace_dynamic(const MtsgLaunch &L);
-// the kd trace kernel's mailbox + first stack entries in LDS (MTSGPU_KD_LDS=1):
-// C4 62.2 -> 65.0, C3 356.8 -> 330.2 Msamples/s (profiles/r04_ab_kd_lds.log), so
-// opt-in; the default keeps them in scratch
-static bool kd_lds() {
-    const char *e = std::getenv("MTSGPU_KD_LDS");
-    return e && e[0] == '1';
-}
+// (the kd trace kernel's mailbox and first stack entries in LDS, round 4: C4 62.2 -> 65.0,
+// C3 356.8 -> 330.2 Msamples/s, profiles/r04_ab_kd_lds.log; the opt-in knob is removed)
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
-    if (L.kd_nodes) return kd_lds() ? (size_t)MTSG_WF_KD_LDSK * BLOCK * 16 + 8 * BLOCK * 4 : 16;
+    if (L.kd_nodes) return 16;
     const bool scan = L.scene_lds && L.scan;
     const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
     const size_t K = std::min<size_t>(L.stack_depth, MTSG_WF_LDS_STACK);
@@ -52,32 +46,9 @@ static WfShadeFn wf_shade_pick(const MtsgLaunch &L, int wk, bool instr, bool ggx
 }
 
 typedef void (*WfTraceFn)(MtsgLaunch, MtsgWave, unsigned long long *);
-// the dynamic-fetch trace kernel (opt-in, MTSGPU_WF_DYN=1) serves BVHs in
-// HBM; it lost to the one-ray-per-thread kernel (C3 604 -> 489, C4 172 -> 149,
-// C5 607 -> 497 Msamples/s, profiles/r04_ab_wf_dyn.log).  HN: the half-float
-// node copy (valid when the scene's extent allows it, as for the BSDF-set
-// megakernels)
-bool mtsg_wf_trace_dynamic(const MtsgLaunch &L) {
-    const char *e = std::getenv("MTSGPU_WF_DYN");
-    return !L.kd_nodes && !L.scene_lds && e && e[0] == '1';
-}
-static WfTraceFn wf_trace_dyn_pick(const MtsgLaunch &L, bool stats) {
-    const bool ana = L.ana != 0, hn = L.bset != 0;
-#define MTSG_DYN(ST, A, H) wf_trace_dyn<ST, A, H>
-    if (stats) return ana ? (hn ? MTSG_DYN(true, true, true) : MTSG_DYN(true, true, false))
-                          : (hn ? MTSG_DYN(true, false, true) : MTSG_DYN(true, false, false));
-    return ana ? (hn ? MTSG_DYN(false, true, true) : MTSG_DYN(false, true, false))
-               : (hn ? MTSG_DYN(false, false, true) : MTSG_DYN(false, false, false));
-#undef MTSG_DYN
-}
 static WfTraceFn wf_trace_pick(const MtsgLaunch &L, bool stats) {
-    if (mtsg_wf_trace_dynamic(L)) return wf_trace_dyn_pick(L, stats);
     const bool ana = L.ana != 0;
-    if (L.kd_nodes) {
-        if (kd_lds()) return stats ? wf_trace<true, false, false, true, MTSG_WF_KD_LDSK>
-                                   : wf_trace<false, false, false, true, MTSG_WF_KD_LDSK>;
-        return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
-    }
+    if (L.kd_nodes) return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
     if (stats) {
         if (L.scene_lds) return ana ? wf_trace<true, true, true, false> : wf_trace<true, true, false, false>;
         return ana ? wf_trace<true, false, true, false> : wf_trace<true, false, false, false>;
