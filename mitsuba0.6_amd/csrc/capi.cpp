@@ -671,7 +671,8 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         // scene beyond half range would get infinite (still exact, but useless) boxes
         float extent = 0.0f;
         for (int a = 0; a < 3; ++a) extent = std::max(extent, std::max(std::fabs(H.aabb_min[a]), std::fabs(H.aabb_max[a])));
-        L.bset = (std::getenv("MTSGPU_NO_BSDF_SETS") || !(extent < 32768.0f)) ? 0u
+        // (the set kernels are built without strictNormals: MTSG_FEAT_NOSTRICT)
+        L.bset = (std::getenv("MTSGPU_NO_BSDF_SETS") || !(extent < 32768.0f) || P->strict_normals) ? 0u
                  : (ggx ? (uint32_t)MTSG_FEAT_GGX : 0u) | (rc ? 0u : (uint32_t)MTSG_FEAT_NORC) |
                        (rd ? 0u : (uint32_t)MTSG_FEAT_NORD);
     }

@@ -66,3 +66,15 @@ __device__ __forceinline__ f3 to_local(const Frame &f, f3 v) { return mk(dot(v, 
 __device__ __forceinline__ f3 to_world(const Frame &f, f3 v) {
     return add(add(mul(f.s, v.x), mul(f.t, v.y)), mul(f.n, v.z));
 }
+// A hit record's shading frame (computeShadingFrame, util.cpp:603-608) keeps s and
+// n: its t is cross(n, s) by construction, re-formed where it is used (the same
+// products, so the same bits) instead of held in three more registers across
+// the BSDF calls
+struct ShFrame {
+    f3 s, n;
+    __device__ __forceinline__ f3 t() const { return cross(n, s); }
+};
+__device__ __forceinline__ f3 to_local(const ShFrame &f, f3 v) { return mk(dot(v, f.s), dot(v, f.t()), dot(v, f.n)); }
+__device__ __forceinline__ f3 to_world(const ShFrame &f, f3 v) {
+    return add(add(mul(f.s, v.x), mul(f.t(), v.y)), mul(f.n, v.z));
+}

@@ -49,11 +49,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     lds_tri *ldsTris = V.tris;
     lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
     lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
-    PathCounters c = {};
+    PathCounters c = {};   // INSTR statistics only: the always-on counts are wave-uniform (wc)
+    WaveCounters wc = {};
     const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 
+    // static striding: lane g takes items g + k * lanes, k = 0, 1, ... (`round` is
+    // k, or the SFMT replay's position in its unit: 32 bits, not a 64-bit item
+    // index, live across the bounce loop)
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
-    uint64_t item = L.replay ? 0 : (uint64_t)xcd_block(L.xcds) * BLOCK + threadIdx.x;
+    const uint32_t g = xcd_block(L.xcds) * BLOCK + threadIdx.x;
+    uint32_t round = 0;
     bool done = false;
     PathState st;
     st.active = false;
@@ -90,15 +95,15 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
                 const uint32_t unit = blockIdx.x * BLOCK + threadIdx.x;
                 if (unit >= L.units) { done = true; break; }
                 const uint32_t k0 = L.unit_start[unit], n = L.unit_start[unit + 1] - k0;
-                if (item >= (uint64_t)n * L.chunk_spp) { done = true; break; }
-                const uint32_t k = k0 + (uint32_t)(item / L.chunk_spp), jj = (uint32_t)(item % L.chunk_spp);
-                ++item;
+                if ((uint64_t)round >= (uint64_t)n * L.chunk_spp) { done = true; break; }
+                const uint32_t k = k0 + round / L.chunk_spp, jj = round % L.chunk_spp;
+                ++round;
                 sh.start_xy(st, L.order[k], jj);
                 break;
             }
-            if (item >= L.num_items) { done = true; break; }
-            const uint64_t it = item;
-            item += lanes;
+            const uint64_t it = g + (uint64_t)round * lanes;
+            if (it >= L.num_items) { done = true; break; }
+            ++round;
             sh.start(st, it);
         }
         if (__all(done)) break;
@@ -114,13 +119,13 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             // both exist they leave the same point (ro was set to its.p)
             float minS = INFINITY, maxS = -INFINITY, minC = INFINITY, maxC = -INFINITY;
             bool okS = false, okC = false;
+            wc.shadow += wave_count(st.active && st.haveShadow);
+            wc.rays += wave_count(st.active && st.haveRay);
             if (st.active && st.haveShadow) {
-                c.shadow++;
                 if (!is_zero(st.P.neeC)) okS = ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, minS, maxS);
                 if (!okS) { minS = INFINITY; maxS = -INFINITY; }
             }
             if (st.active && st.haveRay) {
-                c.rays++;
                 okC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
                 if (!okC) { minC = INFINITY; maxC = -INFINITY; }
             }
@@ -132,8 +137,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         } else {
         // (round 4 measured both rays of a bounce through one per-lane loop, traverse_seq:
         // bit-identical, but C3 -5.5%, C4 -10%, C5 -1.7%, profiles/r04_ab_seq_traversal.log; removed)
+        wc.shadow += wave_count(st.active && st.haveShadow);
         if (st.active && st.haveShadow) {
-            c.shadow++;
             float mint, maxt;
             // a shadow ray whose estimate is zero cannot change Li: skip its traversal
             if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
@@ -158,8 +163,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             st.haveShadow = false;
         }
         MK_STAMP(mkT[1], mkT0);
+        wc.rays += wave_count(st.active && st.haveRay);
         if (st.active && st.haveRay) {
-            c.rays++;
             float mint, maxt;
             if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
@@ -185,9 +190,27 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         MK_STAMP(mkT[2], mkT0);
 
         // ---- C: shade -------------------------------------------------------
-        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) sh.finish(st);
+        // wave-uniform counts: a path's length is 1 + the bounces that advanced its
+        // depth (shade() advances it at most once), summed over finished samples
+        const bool was = st.active;
+        const int d0 = st.P.depth;
+        bool ended = false;
+        if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
+            ended = true;
+            sh.template finish<false>(st);
+        }
+        wc.len += wave_count(was && st.P.depth != d0);
+        wc.samples += wave_count(ended);
+        wc.err += wave_count(ended && st.smp.err);
+        if (__builtin_expect((wc.len | wc.rays | wc.shadow) >= 0x80000000u, 0)) {   // uniform: flush before a wrap
+            wc.len += wc.samples;
+            wave_counters_flush(L, wc);
+            wc = WaveCounters{};
+        }
         MK_STAMP(mkT[3], mkT0);
     }
+    wc.len += wc.samples;
+    wave_counters_flush(L, wc);
     path_counters_flush<STATS>(L, c);
 #ifdef MTSG_MK_STAMPS
     if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)

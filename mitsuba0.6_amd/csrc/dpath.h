@@ -196,7 +196,7 @@ struct Hit {
     int valid;
     float t;
     f3 p, geoN, wi;
-    Frame sh;
+    ShFrame sh;
     int shape;
     float u, v;       // its.uv (textured scenes only; dead otherwise)
 };
@@ -639,12 +639,11 @@ __device__ __forceinline__ bool ray_interval(const MtsgDeviceScene &S, f3 o, f3 
     return maxt > mint;
 }
 
-// computeShadingFrame (util.cpp:603-608)
-__device__ __forceinline__ Frame shading_frame(f3 n, f3 dpdu) {
-    Frame f;
+// computeShadingFrame (util.cpp:603-608); t = cross(n, s) is ShFrame::t()
+__device__ __forceinline__ ShFrame shading_frame(f3 n, f3 dpdu) {
+    ShFrame f;
     f.n = n;
     f.s = normalize(sub(dpdu, mul(f.n, dot(f.n, dpdu))));
-    f.t = cross(f.n, f.s);
     return f;
 }
 
@@ -721,8 +720,9 @@ __device__ __forceinline__ void fill_hit(const MtsgDeviceScene &S, const HS &hs,
 __device__ __forceinline__ void hit_store(float4 *r, const Hit &h, bool uv) {
     r[0] = make_float4(h.t, h.p.x, h.p.y, h.p.z);
     r[1] = make_float4(h.geoN.x, h.geoN.y, h.geoN.z, h.wi.x);
+    const f3 t = h.sh.t();
     r[2] = make_float4(h.wi.y, h.wi.z, h.sh.s.x, h.sh.s.y);
-    r[3] = make_float4(h.sh.s.z, h.sh.t.x, h.sh.t.y, h.sh.t.z);
+    r[3] = make_float4(h.sh.s.z, t.x, t.y, t.z);
     r[4] = make_float4(h.sh.n.x, h.sh.n.y, h.sh.n.z, __int_as_float(h.shape));
     if (uv) r[5] = make_float4(h.u, h.v, 0.0f, 0.0f);
 }
@@ -734,8 +734,7 @@ template <bool UV> __device__ __forceinline__ void hit_load(const float4 *r, Hit
     h.geoN = mk(b.x, b.y, b.z);
     h.wi = mk(b.w, c.x, c.y);
     h.sh.s = mk(c.z, c.w, d.x);
-    h.sh.t = mk(d.y, d.z, d.w);
-    h.sh.n = mk(e.x, e.y, e.z);
+    h.sh.n = mk(e.x, e.y, e.z);   // (d.yzw: t, re-formed as cross(n, s))
     h.shape = __float_as_int(e.w);
     if constexpr (UV) { const float4 f = r[5]; h.u = f.x; h.v = f.y; }
 }
@@ -807,17 +806,21 @@ __device__ __forceinline__ bool film_splat(const MtsgLaunch &L, int px, int py, 
 // ---------------------------------------------------------------------------
 // the persistent path kernel
 // ---------------------------------------------------------------------------
+// whether the BSDF sample that spawned the current ray chose a delta lobe
+// (BSDFSamplingRecord::sampledType & EDelta, path.cpp:262,280): one bit
+#define PV_DELTA(P) ((P).delta != 0)
+#define PV_SET_DELTA(P, t) ((P).delta = ((t) & MTSG_F_DELTA) != 0)
 struct PathVars {
     f3 L, thr;
     float eta;
     int depth;
-    bool scattered, emitted;
-    float alpha;
+    // flags as bits of one word (bools each took a lane-mask SGPR pair across the loop);
+    // alpha is the sample's film alpha, 0 or 1 (path.cpp:125-131, records.inl:117-144)
+    uint32_t scattered : 1, emitted : 1, delta : 1, alpha : 1;
     Hit its;          // current vertex
     f3 neeC;          // throughput*value*bsdfVal*weight, committed if the shadow ray is unoccluded
     f3 refN;          // DirectSamplingRecord::refN of the current vertex
     float bsdfPdf;
-    int sampledType;
 };
 
 __device__ __forceinline__ float next1d(const SobolCtx &C, SamplerState &s) {   // sobol.cpp:219-229
@@ -962,13 +965,12 @@ __device__ __forceinline__ uint64_t sobol_lookup_lds(const MtsgLookup &Lu, T *yc
 // and smp.sampleIndex give them where needed, two and one fewer registers
 // live across every bounce)
 struct PathState {
-    bool active;
+    uint32_t active : 1, haveRay : 1, primary : 1, haveShadow : 1;   // one word of bits
     uint32_t pix;
     float sx, sy;
     SamplerState smp;
     PathVars P;
     // rays of the next trace step: closest (camera / extension) and shadow (NEE)
-    bool haveRay, primary, haveShadow;
     f3 ro, rd, sd;
     float rmint, rmaxt, smaxt;
 };
@@ -1096,6 +1098,9 @@ struct PathShader {
     static constexpr bool ENV = (FEAT & MTSG_FEAT_ENV) != 0, EXT = (FEAT & MTSG_FEAT_EXT) != 0,
                           ANA = (FEAT & MTSG_FEAT_ANA) != 0, DIFF = (FEAT & MTSG_FEAT_DIFF) != 0;
     static constexpr int BSF = FEAT & BSET_BITS;   // the variant's BSDF set (dbsdf.h BSet)
+    // the BSDF-set megakernels are built without strictNormals (the geometric normal
+    // is then dead once the hit is formed); scenes with it run the generic kernel
+    static constexpr bool NOSTRICT = (FEAT & MTSG_FEAT_NOSTRICT) != 0;
     const MtsgLaunch &L;
     const HitSrc<SCENE_LDS> &hs;
     const SobolCtx &SC;
@@ -1112,7 +1117,6 @@ struct PathShader {
         begin(st, jj, px, py);
         return true;
     }
-
     // the SFMT replay's next sample: crop pixel xy (x | y << 16), sample jj of the chunk
     __device__ __forceinline__ void start_xy(PathState &st, uint32_t xy, uint32_t jj) const {
         const uint32_t lx = xy & 0xffffu, ly = xy >> 16;   // row_stride 1: compact row = ly
@@ -1126,7 +1130,6 @@ struct PathShader {
         PathVars &P = st.P;
         const uint32_t j = L.j0 + jj;
         float &sx = st.sx, &sy = st.sy;
-        bool &haveRay = st.haveRay, &primary = st.primary, &haveShadow = st.haveShadow;
         f3 &ro = st.ro, &rd = st.rd;
         float &rmint = st.rmint, &rmaxt = st.rmaxt;
         smp.dim = 0;
@@ -1161,9 +1164,9 @@ struct PathShader {
         P.depth = 1;
         P.scattered = false;
         P.emitted = true;
-        haveRay = true;
-        primary = true;
-        haveShadow = false;
+        st.haveRay = true;
+        st.primary = true;
+        st.haveShadow = false;
         st.active = true;
     }
 
@@ -1180,15 +1183,14 @@ struct PathShader {
         const float sx = st.sx, sy = st.sy;
         if constexpr (HITK == 1) hit = true;
         if constexpr (HITK == 2) hit = false;
-        bool &haveRay = st.haveRay, &primary = st.primary, &haveShadow = st.haveShadow;
         f3 &ro = st.ro, &rd = st.rd, &sd = st.sd;
         float &rmint = st.rmint, &rmaxt = st.rmaxt, &smaxt = st.smaxt;
         bool endPath = false;
         // NEE of the previous vertex (scene.cpp:838-842, path.cpp:176-199)
-        if (haveShadow && !occluded) P.L = add(P.L, P.neeC);
-        haveShadow = false;
+        if (st.haveShadow && !occluded) P.L = add(P.L, P.neeC);
+        st.haveShadow = false;
         bool vertex = false;
-        if (!haveRay) {
+        if (!st.haveRay) {
             endPath = true;   // the BSDF sample at the previous vertex failed
         } else {
             // rRec.rayIntersect / scene->rayIntersect (records.inl:117-144, path.cpp:226)
@@ -1201,8 +1203,8 @@ struct PathShader {
                 P.its = Hit{};
             }
             if (STATS && hit) c.hits++;
-            if (primary) {
-                P.alpha = L.has_alpha ? (P.its.valid ? 1.0f : 0.0f) : 1.0f;
+            if (st.primary) {
+                P.alpha = L.has_alpha ? (P.its.valid ? 1u : 0u) : 1u;
                 vertex = true;
             } else if (HITK == 2 || !P.its.valid) {
                 // missed: the environment emitter, if any (path.cpp:233-247)
@@ -1215,7 +1217,7 @@ struct PathShader {
                     // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
                     if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
                         float lumPdf = 0;
-                        if (!(P.sampledType & MTSG_F_DELTA))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
+                        if (!PV_DELTA(P))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
                             lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : vp.pdf) *
                                      (S.emitters[S.env_emitter].weight * S.em_norm);
                         const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
@@ -1230,7 +1232,7 @@ struct PathShader {
                 if (sh.emitter >= 0) {
                     const f3 value = area_Le(S, P.its, neg(rd));
                     float lumPdf = 0;
-                    if (!(P.sampledType & MTSG_F_DELTA)) {
+                    if (!PV_DELTA(P)) {
                         // Scene::pdfEmitterDirect (scene.cpp:949-952), area.cpp:175-181, shape.cpp:117-126;
                         // dRec after setQuery (records.inl:168-176): d = ray.d, n = its.shFrame.n, dist = its.t
                         const MtsgEmitter &e = S.emitters[sh.emitter];
@@ -1258,8 +1260,8 @@ struct PathShader {
                 vertex = !endPath;
             }
         }
-        haveRay = false;
-        primary = false;
+        st.haveRay = false;
+        st.primary = false;
 
         if (vertex) {
             // loop head of Li() (path.cpp:135-200); rd is the incoming ray direction
@@ -1311,7 +1313,7 @@ struct PathShader {
                 // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
                 const float snp = dot(rd, P.its.geoN) * P.its.wi.z;
                 if ((P.depth >= L.max_depth && L.max_depth > 0) ||
-                    (L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
+                    (!NOSTRICT && L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
                     endPath = true;
                 } else {
                     P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
@@ -1395,7 +1397,7 @@ struct PathShader {
                                 const EvalPdf ep = bsdf_eval_pdf_k<BSF, KIND>(*qb, (glb_f32 *)S.rtrans, qwi, qwo,
                                                                               P.its.u, P.its.v, rpPre(qb, qwi));
                                 const f3 bsdfVal = ep.val;
-                                if (!is_zero(bsdfVal) && (!L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
+                                if (!is_zero(bsdfVal) && (NOSTRICT || !L.strict_normals || dot(P.its.geoN, dd) * wo.z > 0)) {
                                     const float bsdfPdf = ep.pdf;
                                     const float pa = dpdf * dpdf, pb = bsdfPdf * bsdfPdf;
                                     const float weight = pa / (pa + pb);
@@ -1415,7 +1417,7 @@ struct PathShader {
                                 sd = divs(v, rem);
                                 smaxt = rem * (1 - D_SHADOW_EPSILON);
                             }
-                            haveShadow = true;
+                            st.haveShadow = true;
                         }
                     }
                     // BSDF sampling (path.cpp:206-226)
@@ -1441,22 +1443,22 @@ struct PathShader {
                     if (!is_zero(bs.weight) && !smp.err) {
                         P.scattered |= bs.sampledType != MTSG_F_NULL;
                         const f3 wo = to_world(P.its.sh, bs.wo);
-                        if (!L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
+                        if (NOSTRICT || !L.strict_normals || dot(P.its.geoN, wo) * bs.wo.z > 0) {
                             // throughput *= bsdfWeight; eta *= bRec.eta (path.cpp:256-257): the same
                             // products as after the hit, formed now so they need not stay live
                             P.thr = mulv(P.thr, bs.weight);
                             P.bsdfPdf = bs.pdf;
                             P.eta *= bs.eta;
-                            P.sampledType = bs.sampledType;
+                            PV_SET_DELTA(P, bs.sampledType);
                             ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
                             rd = wo;
                             rmint = D_EPSILON;
                             rmaxt = INFINITY;
-                            haveRay = true;
+                            st.haveRay = true;
                         }
                     }
                     // no next ray: the path ends once the pending shadow ray is resolved
-                    if (!haveRay && !haveShadow) endPath = true;
+                    if (!st.haveRay && !st.haveShadow) endPath = true;
                 }
             }
         }
@@ -1464,6 +1466,9 @@ struct PathShader {
     }
 
     // block->put(samplePos, spec, alpha) (integrator.cpp:184) and the sample's records
+    // LANE_COUNTS: count the sample into c (the wavefront engine); the megakernel
+    // counts finished samples per wave instead (WaveCounters)
+    template <bool LANE_COUNTS = true>
     __device__ __forceinline__ void finish(PathState &st) const {
         PathVars &P = st.P;
         SamplerState &smp = st.smp;
@@ -1471,26 +1476,31 @@ struct PathShader {
         int px = 0, py = 0;
         pixel_of(L, pix, px, py);
         const float sx = st.sx, sy = st.sy;
-        bool &haveRay = st.haveRay, &haveShadow = st.haveShadow;
         // block->put(samplePos, spec, alpha) (integrator.cpp:184): the own-pixel
         // splat is stored as {L.rgb, w} (alpha in {0,1} in the sign bit of w) and
         // film_reduce re-forms weight * value[k] -- the same products
-        const float val[5] = {P.L.x, P.L.y, P.L.z, P.alpha, 1.0f};
+        const float alpha = P.alpha ? 1.0f : 0.0f;
+        const float val[5] = {P.L.x, P.L.y, P.L.z, alpha, 1.0f};
         float ownW = 0.0f;
         const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
         float4 rec4;
-        if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha == 0.0f ? -ownW : ownW);
+        if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha ? ownW : -ownW);
         else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
         if (INSTR && L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
-            rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = P.alpha;
+            rec[0] = P.L.x; rec[1] = P.L.y; rec[2] = P.L.z; rec[3] = alpha;
             rec[4] = sx; rec[5] = sy; rec[6] = (float)P.depth; rec[7] = smp.err ? 1.0f : 0.0f;
+        }
+        if (STATS) c.sobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
+        if (!LANE_COUNTS) {
+            st.active = false;
+            st.haveRay = st.haveShadow = false;
+            return;
         }
         c.len += (uint32_t)P.depth;
         c.samples++;
-        if (STATS) c.sobol += (unsigned long long)smp.dim * (smp.dim < L.lds_dims ? 0 : L.nibbles);
         if (smp.err) c.err++;
         // a lane's rays and shadow rays never exceed its path lengths plus samples:
         // flush the 32-bit counts well before any of them can wrap
@@ -1502,9 +1512,25 @@ struct PathShader {
             c.samples = c.rays = c.shadow = c.len = 0;
         }
         st.active = false;
-        haveRay = haveShadow = false;
+        st.haveRay = st.haveShadow = false;
     }
 };
+
+// the megakernel's always-on counts, summed per wave (uniform: SGPRs, not a VGPR
+// per lane across the whole bounce loop)
+struct WaveCounters {
+    uint32_t rays, shadow, len, samples, err;
+};
+__device__ __forceinline__ uint32_t wave_count(bool b) { return (uint32_t)__popcll(__ballot(b)); }
+__device__ __forceinline__ void wave_counters_flush(const MtsgLaunch &L, const WaveCounters &w) {
+    if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+        atomicAdd(L.counters + 0, (unsigned long long)w.samples);
+        atomicAdd(L.counters + 1, (unsigned long long)w.rays);
+        atomicAdd(L.counters + 2, (unsigned long long)w.shadow);
+        atomicAdd(L.counters + 3, (unsigned long long)w.len);
+        if (w.err) atomicAdd(L.counters + 6, (unsigned long long)w.err);
+    }
+}
 
 template <bool STATS>
 __device__ __forceinline__ void path_counters_flush(const MtsgLaunch &L, const PathCounters &c) {

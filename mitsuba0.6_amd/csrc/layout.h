@@ -105,7 +105,8 @@ enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4,
        // BSDF-set specialisation of the megakernel (dbsdf.h BSet): every rough
        // BSDF uses GGX / no roughdielectric / no roughconductor in the scene
        MTSG_FEAT_GGX = 16, MTSG_FEAT_NORD = 32, MTSG_FEAT_NORC = 64,
-       MTSG_FEAT_INL = 128 };   // microfacet / Fresnel helpers inline (the wavefront per-type kernels)
+       MTSG_FEAT_INL = 128,     // microfacet / Fresnel helpers inline (the wavefront per-type kernels)
+       MTSG_FEAT_NOSTRICT = 256 };   // megakernel BSDF-set variants: strictNormals off (capi.cpp picks the generic kernel otherwise)
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
 enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
        MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*

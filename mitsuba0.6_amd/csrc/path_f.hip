@@ -6,6 +6,7 @@
 // path.cpp:171-211), for all-diffuse small scenes (PATH_FEAT 0) the DIFF
 // kernel, and the 7 BSDF-set specialisations of large scenes (dbsdf.h BSet):
 // bits = {every rough BSDF is GGX, no roughdielectric, no roughconductor}.
+// The set kernels are compiled without strictNormals (MTSG_FEAT_NOSTRICT).
 #include "dmega.h"
 
 #define PF_NAME2(a, N) a##N
@@ -13,8 +14,8 @@
 
 namespace {
 constexpr int spec_feat(int bits) {
-    return PATH_FEAT | ((bits & 1) ? (int)MTSG_FEAT_GGX : 0) | ((bits & 2) ? (int)MTSG_FEAT_NORD : 0) |
-           ((bits & 4) ? (int)MTSG_FEAT_NORC : 0);
+    return PATH_FEAT | (int)MTSG_FEAT_NOSTRICT | ((bits & 1) ? (int)MTSG_FEAT_GGX : 0) |
+           ((bits & 2) ? (int)MTSG_FEAT_NORD : 0) | ((bits & 4) ? (int)MTSG_FEAT_NORC : 0);
 }
 
 // variants: small scenes (BVH in LDS) run 3 waves/SIMD with 32 Sobol dims in

@@ -116,7 +116,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     }
     st.P.L = mk(a.x, a.y, a.z); st.P.eta = a.w;
     st.P.thr = mk(b.x, b.y, b.z); st.P.bsdfPdf = b.w;
-    st.P.neeC = mk(c.x, c.y, c.z); st.P.alpha = c.w;
+    st.P.neeC = mk(c.x, c.y, c.z); st.P.alpha = c.w != 0.0f;
     st.P.refN = mk(d.x, d.y, d.z); st.sx = d.w;
     st.ro = mk(e.x, e.y, e.z); st.sy = e.w;
     st.rd = mk(g.x, g.y, g.z); st.P.depth = __float_as_int(g.w);
@@ -125,7 +125,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     st.smp.sampleIndex = h.y;
     st.smp.dim = f.x >> 16;
     st.smp.err = (f.x & WF_ERR) != 0;
-    st.P.sampledType = (int)f.y;
+    PV_SET_DELTA(st.P, (int)f.y);
     st.haveRay = (f.x & WF_RAY) != 0;
     st.primary = (f.x & WF_PRIMARY) != 0;
     st.haveShadow = (f.x & WF_SHADOW) != 0;
@@ -140,7 +140,7 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
     f.x = extra | (st.active ? WF_ACTIVE : 0) | (st.haveRay ? WF_RAY : 0) | (st.primary ? WF_PRIMARY : 0) |
           (st.haveShadow ? WF_SHADOW : 0) | (st.P.scattered ? WF_SCATTERED : 0) | (st.P.emitted ? WF_EMITTED : 0) |
           (st.smp.err ? WF_ERR : 0) | (st.smp.dim << 16);
-    f.y = (uint32_t)st.P.sampledType;
+    f.y = PV_DELTA(st.P) ? (uint32_t)MTSG_F_DELTA : 0u;
     f.z = f.w = 0;
     reinterpret_cast<uint4 *>(v)[7] = f;
     reinterpret_cast<uint4 *>(v)[6] =
@@ -148,7 +148,7 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
     if (!st.active) return;
     v[0] = make_float4(st.P.L.x, st.P.L.y, st.P.L.z, st.P.eta);
     v[1] = make_float4(st.P.thr.x, st.P.thr.y, st.P.thr.z, st.P.bsdfPdf);
-    v[2] = make_float4(st.P.neeC.x, st.P.neeC.y, st.P.neeC.z, st.P.alpha);
+    v[2] = make_float4(st.P.neeC.x, st.P.neeC.y, st.P.neeC.z, st.P.alpha ? 1.0f : 0.0f);
     v[3] = make_float4(st.P.refN.x, st.P.refN.y, st.P.refN.z, st.sx);
     v[4] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.sy);
     v[5] = make_float4(st.rd.x, st.rd.y, st.rd.z, __int_as_float(st.P.depth));

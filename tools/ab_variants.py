@@ -48,14 +48,17 @@ for name, path in variants:
     ctxs[name] = c
 res = {n: [] for n, _ in variants}
 films = {}
+stats = {}
 for r in range(rounds):
     for name, _ in variants:
         film, _, st = with_env(name, lambda: ctxs[name].render(it, row=(8, stride, 0), engine=engines[name]))
         films.setdefault(name, film)
+        stats.setdefault(name, {k: st.get(k) for k in ('samples', 'rays', 'shadow_rays', 'path_length_sum', 'errors')})
         res[name].append(st['samples'] / st['kernel_ms'] / 1e3)
 first = variants[0][0]
 for name, v in res.items():
     v = sorted(v)
     same = films[name].tobytes() == films[first].tobytes()
-    print('%-14s median %8.1f  min %8.1f  max %8.1f Msamples/s  film bit-identical to %s: %s' % (
-        name, v[len(v) // 2], v[0], v[-1], first, same))
+    print('%-14s median %8.1f  min %8.1f  max %8.1f Msamples/s  film bit-identical to %s: %s  counters equal: %s' % (
+        name, v[len(v) // 2], v[0], v[-1], first, same, stats[name] == stats[first]))
+print('counters', stats[first])
