@@ -66,7 +66,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     st.smp.sobolIndex = 0; st.smp.sampleIndex = 0; st.smp.dim = 0; st.smp.err = false;
     st.sx = st.sy = 0;
     st.haveRay = st.primary = st.haveShadow = false;
-    st.ro = mk(0, 0, 0); st.rd = mk(0, 0, 1); st.sd = mk(0, 0, 1);
+    st.P.its.p = mk(0, 0, 0); st.rd = mk(0, 0, 1); st.sd = mk(0, 0, 1);
     st.rmint = st.rmaxt = st.smaxt = 0;
 #ifdef MTSG_MK_STAMPS
     unsigned long long mkT[4] = {0, 0, 0, 0}, mkT0;
@@ -115,8 +115,8 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         uint32_t slot = 0, prim = 0;
         float hu = 0, hv = 0, ht = 0;
         if (SCENE_LDS && L.scan) {
-            // tiny scene: both rays of the bounce in one pass (scan_pair); when
-            // both exist they leave the same point (ro was set to its.p)
+            // tiny scene: both rays of the bounce in one pass (scan_pair); both
+            // leave the same point, P.its.p
             float minS = INFINITY, maxS = -INFINITY, minC = INFINITY, maxC = -INFINITY;
             bool okS = false, okC = false;
             wc.shadow += wave_count(st.active && st.haveShadow);
@@ -126,11 +126,11 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
                 if (!okS) { minS = INFINITY; maxS = -INFINITY; }
             }
             if (st.active && st.haveRay) {
-                okC = ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
+                okC = ray_interval(S, st.P.its.p, st.rd, st.rmint, st.rmaxt, false, minC, maxC);
                 if (!okC) { minC = INFINITY; maxC = -INFINITY; }
             }
             if (__any(okS || okC))
-                scan_pair<STATS>(L, okC ? st.ro : st.P.its.p, st.sd, st.rd, minS, maxS, minC, maxC, occluded, hit,
+                scan_pair<STATS>(L, st.P.its.p, st.sd, st.rd, minS, maxS, minC, maxC, occluded, hit,
                                  prim, hu, hv, ht, c.tests);
             hit = hit && okC;
             occluded = occluded && okS;
@@ -166,16 +166,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         wc.rays += wave_count(st.active && st.haveRay);
         if (st.active && st.haveRay) {
             float mint, maxt;
-            if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
+            if (ray_interval(S, st.P.its.p, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
-                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.ro, st.rd, mint, maxt, stkN, stkD, slot,
+                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.rd, mint, maxt, stkN, stkD, slot,
                                                       hu, hv, ht, c.nodes, c.tests, S.analytic);
                 else if constexpr (HNODES)
-                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
+                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.rd, mint,
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
                                                       S.analytic);
                 else
-                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.ro, st.rd, mint,
+                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.rd, mint,
                                                       maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
                                                       S.analytic);
             }

@@ -970,8 +970,10 @@ struct PathState {
     float sx, sy;
     SamplerState smp;
     PathVars P;
-    // rays of the next trace step: closest (camera / extension) and shadow (NEE)
-    f3 ro, rd, sd;
+    // rays of the next trace step: closest (camera / extension) and shadow (NEE).
+    // Both leave P.its.p (the camera position for the primary ray, set by begin()):
+    // the closest-hit ray's origin is not held separately
+    f3 rd, sd;
     float rmint, rmaxt, smaxt;
 };
 
@@ -1130,7 +1132,7 @@ struct PathShader {
         PathVars &P = st.P;
         const uint32_t j = L.j0 + jj;
         float &sx = st.sx, &sy = st.sy;
-        f3 &ro = st.ro, &rd = st.rd;
+        f3 &rd = st.rd;
         float &rmint = st.rmint, &rmaxt = st.rmaxt;
         smp.dim = 0;
         smp.sampleIndex = j;
@@ -1153,8 +1155,8 @@ struct PathShader {
         rmint = cam.near_clip * invZ;
         rmaxt = cam.far_clip * invZ;
         const float *W = cam.to_world;
-        ro = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
-                W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);
+        P.its.p = mk(W[0] * 0.0f + W[1] * 0.0f + W[2] * 0.0f + W[3], W[4] * 0.0f + W[5] * 0.0f + W[6] * 0.0f + W[7],
+                     W[8] * 0.0f + W[9] * 0.0f + W[10] * 0.0f + W[11]);   // the ray's origin
         rd = mk(W[0] * dl.x + W[1] * dl.y + W[2] * dl.z, W[4] * dl.x + W[5] * dl.y + W[6] * dl.z,
                 W[8] * dl.x + W[9] * dl.y + W[10] * dl.z);
         // Li() prologue (path.cpp:119-133)
@@ -1183,7 +1185,8 @@ struct PathShader {
         const float sx = st.sx, sy = st.sy;
         if constexpr (HITK == 1) hit = true;
         if constexpr (HITK == 2) hit = false;
-        f3 &ro = st.ro, &rd = st.rd, &sd = st.sd;
+        f3 &rd = st.rd, &sd = st.sd;
+        const f3 ro = P.its.p;   // the ray's origin: the previous vertex (or the camera)
         float &rmint = st.rmint, &rmaxt = st.rmaxt, &smaxt = st.smaxt;
         bool endPath = false;
         // NEE of the previous vertex (scene.cpp:838-842, path.cpp:176-199)
@@ -1450,7 +1453,7 @@ struct PathShader {
                             P.bsdfPdf = bs.pdf;
                             P.eta *= bs.eta;
                             PV_SET_DELTA(P, bs.sampledType);
-                            ro = P.its.p;         // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf
+                            // Ray(its.p, wo, ray.time): mint = Epsilon, maxt = inf (origin P.its.p)
                             rd = wo;
                             rmint = D_EPSILON;
                             rmaxt = INFINITY;

@@ -39,7 +39,21 @@
 #define GLF_TABLE static __constant__ const
 #define GLF_FMA(a, b, c) __builtin_fma((a), (b), (c))
 #define GLF_SQRTF(x) __builtin_sqrtf(x)
+// A double polynomial / reduction constant, materialised by two s_mov_b32 where
+// it is used.  As a plain literal, LICM hoisted the constants out of the
+// persistent megakernel's loop into VGPR pairs, and register pressure then put
+// them in scratch: every powf reloaded three of them from memory.  Without
+// the SLP vectoriser, C2 107 instead of 123 VGPRs, C4 106 instead of 112, C5
+// 96 instead of 112 B of scratch per lane (tools/r05/spills.sh).  Volatile asm is not hoisted; the value is the same.
+template <uint64_t B> __device__ __forceinline__ double glf_kd_bits() {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "n"((uint32_t)(B & 0xffffffffu)));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "n"((uint32_t)(B >> 32)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+#define GLF_KD(c) glf_kd_bits<__builtin_bit_cast(uint64_t, (double)(c))>()
 #else
+#define GLF_KD(c) (c)
 #include <math.h>
 #define GLF_FN static inline
 #define GLF_TABLE static const
@@ -63,16 +77,16 @@ GLF_FN float glf_nan(void) { return glf_asfloat(0x7fc00000u); }
 // __sincosf_table[2]: sign[4], 2/pi * 2^24, pi/2, then the cosine polynomial
 // c0..c4 and the sine polynomial s1..s3.  Entry 1 computes -cos for the odd
 // quadrants' swap (c0..c4 negated).
-#define GLF_HPI_INV 0x1.45f306dc9c883p+23
-#define GLF_HPI 0x1.921fb54442d18p+0
-#define GLF_PI63 0x1.921fb54442d18p-62
-#define GLF_S1 -0x1.555545995a603p-3
-#define GLF_S2 0x1.1107605230bc4p-7
-#define GLF_S3 -0x1.994eb3774cf24p-13
-#define GLF_C1 -0x1.ffffffd0c621cp-2
-#define GLF_C2 0x1.55553e1068f19p-5
-#define GLF_C3 -0x1.6c087e89a359dp-10
-#define GLF_C4 0x1.99343027bf8c3p-16
+#define GLF_HPI_INV GLF_KD(0x1.45f306dc9c883p+23)
+#define GLF_HPI GLF_KD(0x1.921fb54442d18p+0)
+#define GLF_PI63 GLF_KD(0x1.921fb54442d18p-62)
+#define GLF_S1 GLF_KD(-0x1.555545995a603p-3)
+#define GLF_S2 GLF_KD(0x1.1107605230bc4p-7)
+#define GLF_S3 GLF_KD(-0x1.994eb3774cf24p-13)
+#define GLF_C1 GLF_KD(-0x1.ffffffd0c621cp-2)
+#define GLF_C2 GLF_KD(0x1.55553e1068f19p-5)
+#define GLF_C3 GLF_KD(-0x1.6c087e89a359dp-10)
+#define GLF_C4 GLF_KD(0x1.99343027bf8c3p-16)
 
 // 4/pi to 192 bits; 8 new bits per entry (__inv_pio4)
 GLF_TABLE uint32_t glf_inv_pio4[24] = {
@@ -171,15 +185,15 @@ GLF_TABLE uint64_t glf_exp2f_tab[32] = {
     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
-#define GLF_EXP2F_SHIFT 0x1.8p+52
-#define GLF_EXP2F_SHIFT_SCALED 0x1.8p+47
-#define GLF_EXP2F_C0 0x1.c6af84b912394p-5
-#define GLF_EXP2F_C1 0x1.ebfce50fac4f3p-3
-#define GLF_EXP2F_C2 0x1.62e42ff0c52d6p-1
-#define GLF_EXPF_INVLN2N 0x1.71547652b82fep+5
-#define GLF_EXPF_C0 0x1.c6af84b912394p-20
-#define GLF_EXPF_C1 0x1.ebfce50fac4f3p-13
-#define GLF_EXPF_C2 0x1.62e42ff0c52d6p-6
+#define GLF_EXP2F_SHIFT GLF_KD(0x1.8p+52)
+#define GLF_EXP2F_SHIFT_SCALED GLF_KD(0x1.8p+47)
+#define GLF_EXP2F_C0 GLF_KD(0x1.c6af84b912394p-5)
+#define GLF_EXP2F_C1 GLF_KD(0x1.ebfce50fac4f3p-3)
+#define GLF_EXP2F_C2 GLF_KD(0x1.62e42ff0c52d6p-1)
+#define GLF_EXPF_INVLN2N GLF_KD(0x1.71547652b82fep+5)
+#define GLF_EXPF_C0 GLF_KD(0x1.c6af84b912394p-20)
+#define GLF_EXPF_C1 GLF_KD(0x1.ebfce50fac4f3p-13)
+#define GLF_EXPF_C2 GLF_KD(0x1.62e42ff0c52d6p-6)
 
 // __math_oflowf / __math_uflowf / __math_may_uflowf (math_errf.c): the
 // product of two same-signed constants, rounded
@@ -221,11 +235,11 @@ GLF_TABLE double glf_powf_log2_tab[16][2] = {
     {0x1.e608cfd9a47acp-1, 0x1.338ca9f24f53dp-4},  {0x1.ca4b31f026aa0p-1, 0x1.476a9543891bap-3},
     {0x1.b2036576afce6p-1, 0x1.e840b4ac4e4d2p-3},  {0x1.9c2d163a1aa2dp-1, 0x1.40645f0c6651cp-2},
     {0x1.886e6037841edp-1, 0x1.88e9c2c1b9ff8p-2},  {0x1.767dcf5534862p-1, 0x1.ce0a44eb17bccp-2}};
-#define GLF_POWF_A0 0x1.27616c9496e0bp-2
-#define GLF_POWF_A1 -0x1.71969a075c67ap-2
-#define GLF_POWF_A2 0x1.ec70a6ca7baddp-2
-#define GLF_POWF_A3 -0x1.7154748bef6c8p-1
-#define GLF_POWF_A4 0x1.71547652ab82bp+0
+#define GLF_POWF_A0 GLF_KD(0x1.27616c9496e0bp-2)
+#define GLF_POWF_A1 GLF_KD(-0x1.71969a075c67ap-2)
+#define GLF_POWF_A2 GLF_KD(0x1.ec70a6ca7baddp-2)
+#define GLF_POWF_A3 GLF_KD(-0x1.7154748bef6c8p-1)
+#define GLF_POWF_A4 GLF_KD(0x1.71547652ab82bp+0)
 
 // log2_inline: x = 2^k z with z in [0x3f330000, 2*0x3f330000)
 GLF_FN double glf_powf_log2(uint32_t ix) {

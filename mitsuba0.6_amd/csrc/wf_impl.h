@@ -97,7 +97,7 @@ __device__ __forceinline__ uint32_t *wf_cnt(const MtsgWave &W, uint32_t parity, 
 }
 
 // path state <-> slot s (AoS, 128 B): [0] L, eta  [1] thr, bsdfPdf  [2] neeC, alpha
-// [3] refN, sx  [4] ro, sy  [5] rd, depth  [6] pix, j, sobol index
+// [3] refN, sx  [4] ray origin (P.its.p), sy  [5] rd, depth  [6] pix, j, sobol index
 // [7] flags | dim << 16, sampledType, -, -
 enum { WF_ACTIVE = 1, WF_RAY = 2, WF_PRIMARY = 4, WF_SHADOW = 8, WF_SCATTERED = 16, WF_EMITTED = 32, WF_ERR = 64,
        WF_DONE = 128,      // the slot's items are used up
@@ -118,7 +118,7 @@ __device__ __forceinline__ bool wf_load(const MtsgLaunch &L, const MtsgWave &W, 
     st.P.thr = mk(b.x, b.y, b.z); st.P.bsdfPdf = b.w;
     st.P.neeC = mk(c.x, c.y, c.z); st.P.alpha = c.w != 0.0f;
     st.P.refN = mk(d.x, d.y, d.z); st.sx = d.w;
-    st.ro = mk(e.x, e.y, e.z); st.sy = e.w;
+    st.P.its.p = mk(e.x, e.y, e.z); st.sy = e.w;
     st.rd = mk(g.x, g.y, g.z); st.P.depth = __float_as_int(g.w);
     st.pix = h.x;
     st.smp.sobolIndex = (uint64_t)h.z | ((uint64_t)h.w << 32);
@@ -150,7 +150,7 @@ __device__ __forceinline__ void wf_store(const MtsgWave &W, uint32_t s, const Pa
     v[1] = make_float4(st.P.thr.x, st.P.thr.y, st.P.thr.z, st.P.bsdfPdf);
     v[2] = make_float4(st.P.neeC.x, st.P.neeC.y, st.P.neeC.z, st.P.alpha ? 1.0f : 0.0f);
     v[3] = make_float4(st.P.refN.x, st.P.refN.y, st.P.refN.z, st.sx);
-    v[4] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.sy);
+    v[4] = make_float4(st.P.its.p.x, st.P.its.p.y, st.P.its.p.z, st.sy);
     v[5] = make_float4(st.rd.x, st.rd.y, st.rd.z, __int_as_float(st.P.depth));
 }
 
@@ -241,9 +241,9 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
     if (st.active && st.haveRay) {
         c.rays++;
         float mint, maxt;
-        if (ray_interval(S, st.ro, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
+        if (ray_interval(S, st.P.its.p, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
             pr = true;
-            r0 = make_float4(st.ro.x, st.ro.y, st.ro.z, mint);
+            r0 = make_float4(st.P.its.p.x, st.P.its.p.y, st.P.its.p.z, mint);
             r1 = make_float4(st.rd.x, st.rd.y, st.rd.z, maxt);
         }
     }
