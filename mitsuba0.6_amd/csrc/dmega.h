@@ -43,15 +43,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     constexpr bool ANA = (FEAT & MTSG_FEAT_ANA) != 0;
     constexpr bool HNODES = (FEAT & (MTSG_FEAT_GGX | MTSG_FEAT_NORD | MTSG_FEAT_NORC)) != 0;
     extern __shared__ uint32_t lds[];
-    const MtsgDeviceScene &S = L.scene;
-    const LdsView<SCENE_LDS> V = stage_lds<SCENE_LDS>(L, lds);
-    lds_node *ldsNodes = V.nodes;
-    lds_tri *ldsTris = V.tris;
-    lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
-    lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
+    (void)stage_lds<SCENE_LDS>(L, lds);
     PathCounters c = {};   // INSTR statistics only: the always-on counts are wave-uniform (wc)
     WaveCounters wc = {};
-    const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
 
     // static striding: lane g takes items g + k * lanes, k = 0, 1, ... (`round` is
     // k, or the SFMT replay's position in its unit: 32 bits, not a 64-bit item
@@ -74,21 +68,17 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
 #endif
 
     while (true) {
-#ifndef MTSG_NO_FRESH_LAUNCH
-        // the launch record re-read per bounce instead of held (dpath.h launch_fresh)
+        // the launch record re-read per bounce instead of held (dpath.h launch_fresh),
+        // and the LDS / scene pointers re-derived from it (dpath.h lds_view): C2 +2.0%,
+        // C4 +3.8%, C5 +0.7%, C3 0 (profiles/r04_ab_fresh_view.log)
         const MtsgLaunch &L = launch_fresh();
         const MtsgDeviceScene &S = L.scene;
-#ifndef MTSG_NO_FRESH_VIEW
-        // the LDS / scene pointers re-derived from it as well (dpath.h lds_view):
-        // C2 +2.0%, C4 +3.8%, C5 +0.7%, C3 0 (profiles/r04_ab_fresh_view.log)
         const LdsView<SCENE_LDS> V = lds_view<SCENE_LDS>(L, lds);
         lds_node *ldsNodes = V.nodes;
         lds_tri *ldsTris = V.tris;
         lds_stk_n *stkN = (lds_stk_n *)(lds + V.stackBase) + threadIdx.x;
         lds_stk_d *stkD = (lds_stk_d *)(lds + V.stackBase + L.stack_depth * BLOCK) + threadIdx.x;
-#endif
         const PathShader<INSTR, SCENE_LDS, FEAT> sh{L, V.hs, V.SC, V.ycolTab, c};
-#endif
         // ---- A: start the next sample
         while (!st.active && !done) {
             if (L.replay) {   // SFMT replay: this lane's unit, pixel after pixel, in order
@@ -144,16 +134,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             if (!is_zero(st.P.neeC) && ray_interval(S, st.P.its.p, st.sd, D_EPSILON, st.smaxt, true, mint, maxt)) {
                 uint32_t sl; float a0, a1, a2;
                 if (SCENE_LDS)
-                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN, stkD,
-                                                          sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
+                    occluded = traverse<true, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.sd, mint, maxt, stkN,
+                                                                stkD, sl, a0, a1, a2, c.nodes, c.tests, S.analytic);
                 else if constexpr (HNODES)
-                    occluded = traverse<true, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
-                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
-                                                          S.analytic);
+                    occluded = traverse<true, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p,
+                                                                st.sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes,
+                                                                c.tests, S.analytic);
                 else
-                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.sd,
-                                                          mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes, c.tests,
-                                                          S.analytic);
+                    occluded = traverse<true, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p,
+                                                                st.sd, mint, maxt, stkN, stkD, sl, a0, a1, a2, c.nodes,
+                                                                c.tests, S.analytic);
             }
         }
         // the NEE estimate is added now (as shade() would first thing), so it
@@ -168,16 +158,16 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
             float mint, maxt;
             if (ray_interval(S, st.P.its.p, st.rd, st.rmint, st.rmaxt, false, mint, maxt)) {
                 if (SCENE_LDS)
-                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.rd, mint, maxt, stkN, stkD, slot,
-                                                      hu, hv, ht, c.nodes, c.tests, S.analytic);
+                    hit = traverse<false, STATS, ANA>(ldsNodes, ldsTris, st.P.its.p, st.rd, mint, maxt, stkN, stkD,
+                                                            slot, hu, hv, ht, c.nodes, c.tests, S.analytic);
                 else if constexpr (HNODES)
-                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.rd, mint,
-                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
-                                                      S.analytic);
+                    hit = traverse<false, STATS, ANA>((glb_hnode *)S.hnodes, (glb_tri *)S.tris, st.P.its.p, st.rd,
+                                                            mint, maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
+                                                            S.analytic);
                 else
-                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.rd, mint,
-                                                      maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
-                                                      S.analytic);
+                    hit = traverse<false, STATS, ANA>((glb_node *)S.nodes, (glb_tri *)S.tris, st.P.its.p, st.rd,
+                                                            mint, maxt, stkN, stkD, slot, hu, hv, ht, c.nodes, c.tests,
+                                                            S.analytic);
             }
             if (hit) prim = SCENE_LDS ? ldsTris[slot].prim : S.tris[slot].prim;
         }
