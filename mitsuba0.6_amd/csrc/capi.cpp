@@ -316,11 +316,28 @@ struct WfPlan {
 // live count of every POLL-th bounce is read back asynchronously; the host
 // stays at most LAG polls ahead of the GPU, so the queues never drain and the
 // overshoot (empty bounces) stays small.
+// Entries per region of the wavefront queues.  A kernel's block b appends to
+// region b % R, at most BLOCK entries per block.  Ray queues are filled by the
+// shade kernels, one per kind over n_k <= slots entries in all: a region gets at
+// most sum_k ceil(ceil(n_k / BLOCK) / R) <= ceil((slots / BLOCK + K) / R) + K
+// blocks.  A kind queue gets the trace kernel's closest-hit entries (its first
+// nc <= slots entries: ceil((slots / BLOCK + 1) / R) + 1 blocks per region), and
+// the miss queue the shade kernels' appends as well.  Round 4 sized every
+// region for all slots: 8x the ray-queue bytes that can be live.
+static void wf_caps(size_t slots, size_t &capRay, size_t &capCls) {
+    const size_t B = BLOCK_THREADS, R = MTSG_WF_REGIONS, K = MTSG_WK_KINDS, nb = (slots + B - 1) / B;
+    const size_t shade = (nb + K + R - 1) / R + K, trace = (nb + 1 + R - 1) / R + 1;
+    capRay = std::min(slots, B * shade);
+    capCls = std::min(slots, B * (shade + trace));
+}
+
 static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, bool stats, hipStream_t stream,
                            const WfPlan &plan, const volatile int *cancel) {
     hipError_t e;
     const uint32_t slots = plan.slots;
-    const size_t cap = slots, R = MTSG_WF_REGIONS;
+    const size_t R = MTSG_WF_REGIONS;
+    size_t cap, capCls;
+    wf_caps(slots, cap, capCls);
     // the shade kernels' launch record: their blocks are short-lived (one queue entry
     // per thread), so the Sobol dimensions they stage in LDS are a per-block cost;
     // MTSGPU_WF_SHADE_LDS_DIMS caps them (0: every dimension from HBM/L2)
@@ -333,7 +350,7 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     for (int p = 0; p < 2; ++p) {
         W.ray[p] = (float4 *)ctx->wf_ray.p + (size_t)p * 2 * R * cap * 2;
         W.rslot[p] = (uint32_t *)ctx->wf_rslot.p + (size_t)p * 2 * R * cap;
-        W.cls[p] = (uint32_t *)ctx->wf_cls.p + (size_t)p * MTSG_WK_KINDS * R * cap;
+        W.cls[p] = (uint32_t *)ctx->wf_cls.p + (size_t)p * MTSG_WK_KINDS * R * capCls;
     }
     W.cnt = (uint32_t *)ctx->wf_cnt.p;
     W.hit = (float4 *)ctx->wf_hit.p;
@@ -343,6 +360,7 @@ static int wf_render_chunk(mtsgpu_ctx *ctx, const MtsgLaunch &L, bool instr, boo
     W.shape_kind = (const uint32_t *)ctx->wf_kind.p;
     W.slots = slots;
     W.cap = (uint32_t)cap;
+    W.cap_cls = (uint32_t)capCls;
     W.ovf_depth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
     if (plan.hitrec) {
         W.hitrec = (float4 *)ctx->wf_hitrec.p;
@@ -810,14 +828,16 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             if (plan.kinds[k]) plan.shadeGrid[k] = (int)(plan.slots / BLOCK_THREADS);
         plan.traceGrid = (int)(2 * (uint64_t)plan.slots / BLOCK_THREADS);
         plan.hitrec = wf_hitrec_on();
-        const size_t slots = plan.slots, cap = slots;
+        const size_t slots = plan.slots;
+        size_t cap, capCls;
+        wf_caps(slots, cap, capCls);
         const size_t ovfDepth = L.stack_depth > MTSG_WF_LDS_STACK ? L.stack_depth - MTSG_WF_LDS_STACK : 0;
         int partBlocks = plan.traceGrid;
         for (int k = 0; k < MTSG_WK_KINDS; ++k) partBlocks = std::max(partBlocks, plan.shadeGrid[k]);
         if ((e = ctx->wf_state.ensure((size_t)MTSG_WF_STATE_VECS * slots * 16)) != hipSuccess ||
             (e = ctx->wf_ray.ensure((size_t)2 * 2 * R * cap * 32)) != hipSuccess ||
             (e = ctx->wf_rslot.ensure((size_t)2 * 2 * R * cap * 4)) != hipSuccess ||
-            (e = ctx->wf_cls.ensure((size_t)2 * MTSG_WK_KINDS * R * cap * 4)) != hipSuccess ||
+            (e = ctx->wf_cls.ensure((size_t)2 * MTSG_WK_KINDS * R * capCls * 4)) != hipSuccess ||
             (e = ctx->wf_cnt.ensure((size_t)2 * MTSG_WF_QUEUES * R * 4)) != hipSuccess ||
             (e = ctx->wf_hit.ensure(slots * 16)) != hipSuccess ||
             (plan.hitrec && (e = ctx->wf_hitrec.ensure(slots * MTSG_WF_HIT_VECS * 16)) != hipSuccess) ||

@@ -254,7 +254,8 @@ struct MtsgWave {
     uint32_t *live;                   // [2 parities] live slots after the bounce's shade kernels
     uint2 *ovf;                       // trace stack overflow: [trace lanes][ovf_depth]
     const uint32_t *shape_kind;       // [shapes] MTSG_WK_* of the shape's BSDF
-    uint32_t slots, cap;
+    uint32_t slots;
+    uint32_t cap, cap_cls;            // entries per region of a ray queue / of a kind queue (capi.cpp wf_caps)
     uint32_t parity;                  // bounce index & 1
     uint32_t seed;                    // first bounce: the MISS kernel takes every slot (identity queue)
     uint32_t ovf_depth;

@@ -172,7 +172,7 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
     const LdsView<false> V = stage_lds<false>(L, lds);   // ends with a barrier
     PathCounters c = {};
     const PathShader<INSTR, false, FEAT, KIND, HITK> sh{L, V.hs, V.SC, V.ycolTab, c};
-    const uint32_t *cls = W.cls[p] + (size_t)queue * WF_R * W.cap;
+    const uint32_t *cls = W.cls[p] + (size_t)queue * WF_R * W.cap_cls;
     float4 *qray = W.ray[p], *sray = W.ray[p] + (size_t)2 * WF_R * W.cap;
     uint32_t *qslot = W.rslot[p], *sslot = W.rslot[p] + (size_t)WF_R * W.cap;
     uint32_t *missQ = W.cls[p ^ 1u];   // MTSG_WK_MISS = 0: the first kind queue
@@ -180,7 +180,7 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
     uint32_t *cm = wf_cnt(W, p ^ 1u, 2 + MTSG_WK_MISS) + region;
     const uint32_t i = kb * BLOCK + threadIdx.x;
     const bool valid = i < n;
-    const uint32_t s = !valid ? 0u : W.seed ? i : cls[Q.pos(i, W.cap)];
+    const uint32_t s = !valid ? 0u : W.seed ? i : cls[Q.pos(i, W.cap_cls)];
     PathState st;
     uint32_t flags = 0;
     st.active = false;
@@ -261,7 +261,7 @@ __device__ __forceinline__ void wf_shade_block(const MtsgLaunch &L, const MtsgWa
         const size_t k = (size_t)region * W.cap + qpos;
         qray[2 * k] = r0; qray[2 * k + 1] = r1; qslot[k] = s;
     }
-    if (pm) missQ[(size_t)region * W.cap + mpos] = s;
+    if (pm) missQ[(size_t)region * W.cap_cls + mpos] = s;
     if (valid) wf_store(W, s, st, (done ? WF_DONE : 0u) | (ps ? WF_SQUEUED : 0u));
     uint32_t v[16] = {};
     v[0] = (uint32_t)c.samples; v[1] = (uint32_t)c.rays; v[2] = (uint32_t)c.shadow; v[3] = (uint32_t)c.len;
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
 #pragma unroll
         for (uint32_t q = 0; q < MTSG_WK_KINDS; ++q) {
             const uint32_t pos = wave_append(wf_cnt(W, p ^ 1u, 2 + q) + region, kind == q);
-            if (kind == q) next[((size_t)q * WF_R + region) * W.cap + pos] = s;
+            if (kind == q) next[((size_t)q * WF_R + region) * W.cap_cls + pos] = s;
         }
     }
     if (STATS) {
