@@ -87,7 +87,7 @@ struct mtsgpu_ctx {
     HostScene host;
     MtsgDeviceScene dscene;
     DevBuf scan_tris;   // k-grouped TriAccel records of scan-sized scenes
-    uint32_t scan_n[3] = {0, 0, 0};
+    uint32_t scan_n[6] = {0, 0, 0, 0, 0, 0};
     DevBuf nodes, hnodes, tris, prim_vtx, dpdu, positions, normals, shapes, bsdfs, emitters, area_cdf, em_cdf, sobol;
     DevBuf env, env_texels, env_rows, env_cols, env_weights, env_grows, env_gcols;
     DevBuf rtrans, texcoords, analytic;
@@ -212,15 +212,18 @@ int mtsgpu_upload_scene(mtsgpu_ctx *ctx, const mtsgpu_scene_desc *scene) {
         (e = upload(ctx->emitters, H.emitters, s)) != hipSuccess || (e = upload(ctx->area_cdf, H.area_cdf, s)) != hipSuccess ||
         (e = upload(ctx->em_cdf, H.em_cdf, s)) != hipSuccess || (e = upload(ctx->sobol, sobol_nibble_tables(), s)) != hipSuccess)
         return hip_fail(ctx, e, "scene upload");
-    // tiny scenes: the TriAccel records grouped by projection axis, so the scan
-    // runs three branch-free loops (the closest hit and its tie rule do not
-    // depend on the order the records are tested in)
-    ctx->scan_n[0] = ctx->scan_n[1] = ctx->scan_n[2] = 0;
+    // tiny scenes: the TriAccel records grouped by projection axis and, within
+    // an axis, planes normal to it (n_u = n_v = 0: the Cornell box's walls)
+    // last, so the scan runs six branch-free loops, the aligned ones without
+    // the numerator's and denominator's n_u/n_v terms (the closest hit and its
+    // tie rule do not depend on the order the records are tested in)
+    for (uint32_t &c : ctx->scan_n) c = 0;
     if (H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty()) {
         std::vector<MtsgTri> g;
         for (uint32_t k = 0; k < 3; ++k)
-            for (const MtsgTri &t : H.tris)
-                if (t.k == k) { g.push_back(t); ctx->scan_n[k]++; }
+            for (uint32_t al = 0; al < 2; ++al)
+                for (const MtsgTri &t : H.tris)
+                    if (t.k == k && (uint32_t)(t.n_u == 0.0f && t.n_v == 0.0f) == al) { g.push_back(t); ctx->scan_n[2 * k + al]++; }
         if (g.empty()) g.push_back(MtsgTri{});
         if ((e = upload(ctx->scan_tris, g, s)) != hipSuccess) return hip_fail(ctx, e, "scene upload");
     }
@@ -663,7 +666,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.scan = (L.scene_lds && H.tris.size() <= MTSG_SCAN_MAX && H.analytic.empty() && !std::getenv("MTSGPU_NO_SCAN"))
                  ? 1u : 0u;
     L.scan_tris = (const MtsgTri *)ctx->scan_tris.p;
-    for (int k = 0; k < 3; ++k) L.scan_n[k] = ctx->scan_n[k];
+    for (int k = 0; k < 6; ++k) L.scan_n[k] = ctx->scan_n[k];
     // large scenes are latency-bound: run 4 waves/SIMD when 4 blocks' traversal
     // stacks + look_up tables fit the 160 KiB LDS, with as many Sobol dims in
     // LDS as the rest allows (the others are read through L1/L2)
@@ -1030,9 +1033,14 @@ int ensure_kdtree(mtsgpu_ctx *ctx) {
     if (rc) return fail(ctx, rc, err);
     (void)hipSetDevice(ctx->device);
     hipError_t e;
+    // the TriAccel records in leaf-list order (one per primitive reference), so a
+    // leaf's records are read without the indices[e] -> record dependence
+    std::vector<MtsgTri> lt(ctx->kd.indices.size());
+    for (size_t i = 0; i < lt.size(); ++i) lt[i] = tg[ctx->kd.indices[i]];
+    if (lt.empty()) lt.push_back(MtsgTri{});
     if ((e = upload(ctx->kd_nodes, ctx->kd.nodes, ctx->stream)) != hipSuccess ||
         (e = upload(ctx->kd_indices, ctx->kd.indices, ctx->stream)) != hipSuccess ||
-        (e = upload(ctx->kd_tris, tg, ctx->stream)) != hipSuccess || (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
+        (e = upload(ctx->kd_tris, lt, ctx->stream)) != hipSuccess || (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)
         return hip_fail(ctx, e, "kd-tree upload");
     ctx->kd_built = true;
     return MTSGPU_OK;

@@ -357,7 +357,15 @@ typedef __attribute__((address_space(4))) const MtsgTri cst_tri;
 // one projection axis' records: the coordinate permutation is a compile-time
 // constant, so the loop is straight-line code around the correctly rounded
 // division; each record is read whole (two scalar loads) at the loop head
-template <int K, bool ANY, bool STATS>
+// AL: the group whose plane normal lies along axis K (n_u and n_v both +-0,
+// L.scan_n): then the numerator is n_d - o_k and the denominator d_k,
+// exactly (a +-0 product added to a nonzero value leaves it unchanged).  Where
+// the sum is zero the two forms may differ in the sign of that zero only: a
+// zero numerator gives t = +-0 either way, and +0 and -0 pass every comparison
+// alike; a zero d_k gives +-inf (rejected by the finite clipped [mint, maxt])
+// or NaN (rejected by the barycentric test).  C2 +1.75%
+// (profiles/r05_ab_aligned_scan.log)
+template <int K, bool AL, bool ANY, bool STATS>
 __device__ __forceinline__ bool scan_k(cst_tri *tris, uint32_t n, f3 o, f3 d, float mint, bool &found,
                                        uint32_t &bestPrim, float &bu, float &bv, float &bt,
                                        unsigned long long &tests) {
@@ -372,7 +380,7 @@ __device__ __forceinline__ bool scan_k(cst_tri *tris, uint32_t n, f3 o, f3 d, fl
                     b_nv = tr.b_nv, c_nu = tr.c_nu, c_nv = tr.c_nv;
         const uint32_t prim = tr.prim;
         // TriAccel::rayIntersect (triaccel.h:92-160)
-        const float t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+        const float t = AL ? (n_d - o_k) / d_k : (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
         if (t < mint || t > bt) continue;
         const float hu = o_u + t * d_u - a_u;
         const float hv = o_v + t * d_v - a_v;
@@ -391,7 +399,8 @@ __device__ __forceinline__ bool scan_k(cst_tri *tris, uint32_t n, f3 o, f3 d, fl
 // Tiny scenes (<= MTSG_SCAN_MAX triangles, no analytic shapes): every lane
 // tests every TriAccel record, read from the constant address space with a
 // uniform index (scalar loads into SGPRs): no traversal stack, no divergent
-// node loop.  The records come grouped by projection axis (L.scan_tris); the
+// node loop.  The records come grouped by projection axis (L.scan_tris, each
+// axis' records with an axis-aligned plane last); the
 // result -- the closest t, ties to the larger primitive index as in
 // traverse() -- does not depend on the test order.  Returns the
 // primitive index (not a slot) in bestPrim.
@@ -400,13 +409,16 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
                                           uint32_t &bestPrim, float &bu, float &bv, float &bt,
                                           unsigned long long &tests) {
     cst_tri *tris = (cst_tri *)L.scan_tris;
-    const uint32_t n0 = L.scan_n[0], n1 = L.scan_n[1], n2 = L.scan_n[2];
     bool found = false;
     bestPrim = 0;
     bt = maxt;
-    if (scan_k<0, ANY, STATS>(tris, n0, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
-    if (scan_k<1, ANY, STATS>(tris + n0, n1, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
-    if (scan_k<2, ANY, STATS>(tris + n0 + n1, n2, o, d, mint, found, bestPrim, bu, bv, bt, tests)) return true;
+#define MTSG_SCAN_GROUP(K, AL)                                                                                   \
+    if (scan_k<K, AL, ANY, STATS>(tris, L.scan_n[2 * K + AL], o, d, mint, found, bestPrim, bu, bv, bt, tests)) \
+        return true;                                                                                             \
+    tris += L.scan_n[2 * K + AL];
+    MTSG_SCAN_GROUP(0, false) MTSG_SCAN_GROUP(0, true) MTSG_SCAN_GROUP(1, false) MTSG_SCAN_GROUP(1, true)
+    MTSG_SCAN_GROUP(2, false) MTSG_SCAN_GROUP(2, true)
+#undef MTSG_SCAN_GROUP
     return found;
 }
 
@@ -416,7 +428,7 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
 // the records are loaded once, and the pairs of products pack into
 // v_pk_mul/v_pk_add.  Each ray's result is exactly that of its own scan_tris
 // (an empty interval, mint = +inf and maxt = -inf, disables a ray).
-template <int K, bool STATS>
+template <int K, bool AL, bool STATS>
 __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 ds, f3 dc, float minS, float maxS,
                                             float minC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
                                             float &bv, float &bt, unsigned long long &tests) {
@@ -433,9 +445,10 @@ __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 
                     b_nv = tr.b_nv, c_nu = tr.c_nu, c_nv = tr.c_nv;
         const uint32_t prim = tr.prim;
         // TriAccel::rayIntersect (triaccel.h:92-160) for both rays
-        const float num = n_d - o_u * n_u - o_v * n_v - o_k;
-        const float tS = num / (s_u * n_u + s_v * n_v + s_k);
-        const float tC = num / (c_u * n_u + c_v * n_v + c_k);
+        // (AL: as in scan_k)
+        const float num = AL ? n_d - o_k : n_d - o_u * n_u - o_v * n_v - o_k;
+        const float tS = num / (AL ? s_k : s_u * n_u + s_v * n_v + s_k);
+        const float tC = num / (AL ? c_k : c_u * n_u + c_v * n_v + c_k);
         if (!(tS < minS || tS > maxS)) {
             const float hu = o_u + tS * s_u - a_u;
             const float hv = o_v + tS * s_v - a_v;
@@ -462,14 +475,17 @@ __device__ __forceinline__ void scan_pair(const MtsgLaunch &L, f3 o, f3 ds, f3 d
                                           float maxC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
                                           float &bv, float &bt, unsigned long long &tests) {
     cst_tri *tris = (cst_tri *)L.scan_tris;
-    const uint32_t n0 = L.scan_n[0], n1 = L.scan_n[1], n2 = L.scan_n[2];
     occ = false;
     found = false;
     bestPrim = 0;
     bt = maxC;
-    scan_pair_k<0, STATS>(tris, n0, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
-    scan_pair_k<1, STATS>(tris + n0, n1, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
-    scan_pair_k<2, STATS>(tris + n0 + n1, n2, o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, bt, tests);
+#define MTSG_SCAN_GROUP(K, AL)                                                                                    \
+    scan_pair_k<K, AL, STATS>(tris, L.scan_n[2 * K + AL], o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, \
+                              bt, tests);                                                                         \
+    tris += L.scan_n[2 * K + AL];
+    MTSG_SCAN_GROUP(0, false) MTSG_SCAN_GROUP(0, true) MTSG_SCAN_GROUP(1, false) MTSG_SCAN_GROUP(1, true)
+    MTSG_SCAN_GROUP(2, false) MTSG_SCAN_GROUP(2, true)
+#undef MTSG_SCAN_GROUP
 }
 
 // AABB::rayIntersect (core/aabb.h:308-338) against the scene bounds
@@ -500,7 +516,8 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
 // maxt] with the 8-entry hashed mailbox (:138-152, MTS_KD_MAILBOX_ENABLED),
 // and ShapeKDTree::intersect's TriAccel test (skdtree.h:248-338), which keeps
 // a hit at t == maxt: among exactly tied triangles the last one tested wins,
-// as in the reference.  TriAccel records are in global primitive order.
+// as in the reference.  TriAccel records are in leaf-list order (tris[e] is
+// the record of primitive indices[e], duplicated where leaves share one).
 // The reference's stack entry holds the entry/exit point p = ray(t) with
 // p[axis] = split; here an entry keeps (node, t, split, prev | axis << 8),
 // 16 B instead of 24, and p[a] is re-formed as split (a == axis) or o[a] +
@@ -509,12 +526,13 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
 // compares against are held in registers (only a push or a pop changes them),
 // so a descent step reads no stack memory.  LDSK = 0: the stack and the
 // mailbox live in scratch; LDSK > 0 (the wavefront engine's kd trace kernel):
-// the mailbox and the first LDSK stack entries live in LDS, lane-strided
-// (lmbox[slot * BLOCK], lstk[entry * BLOCK]), deeper entries in scratch.
+// the first LDSK stack entries live in LDS, lane-strided (lstk[entry *
+// BLOCK]), deeper entries in scratch; MBL: the mailbox in LDS (lmbox[slot *
+// BLOCK]).
 struct KdEnt { uint32_t node; float t; float split; uint32_t prev_axis; };
 typedef __attribute__((address_space(3))) vu4 lds_kdent;
 typedef __attribute__((address_space(3))) uint32_t lds_w32;
-template <bool ANY, int LDSK = 0>
+template <bool ANY, int LDSK = 0, bool MBL = (LDSK > 0)>
 __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__restrict__ indices,
                             const MtsgTri *__restrict__ tris, f3 o, f3 d, float mint, float maxt, float &bt,
                             float &bu, float &bv, uint32_t &bprim, lds_kdent *lstk = nullptr,
@@ -522,7 +540,7 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
     typedef KdEnt Ent;
     constexpr uint32_t NONE = 0xffffffffu, NOAXIS = 3u;
     Ent stackS[48 - LDSK];
-    uint32_t mboxS[LDSK ? 1 : 8];
+    uint32_t mboxS[MBL ? 1 : 8];
     // entry i: LDS below LDSK, scratch above
     auto ld = [&](uint32_t i) -> Ent {
         if (LDSK && i < (uint32_t)LDSK) {
@@ -535,8 +553,8 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         if (LDSK && i < (uint32_t)LDSK) lstk[i * BLOCK] = vu4{e.node, __float_as_uint(e.t), __float_as_uint(e.split), e.prev_axis};
         else stackS[i - LDSK] = e;
     };
-    auto mb = [&](uint32_t k) -> uint32_t { if constexpr (LDSK > 0) return lmbox[k * BLOCK]; else return mboxS[k]; };
-    auto mbset = [&](uint32_t k, uint32_t v) { if constexpr (LDSK > 0) lmbox[k * BLOCK] = v; else mboxS[k] = v; };
+    auto mb = [&](uint32_t k) -> uint32_t { if constexpr (MBL) return lmbox[k * BLOCK]; else return mboxS[k]; };
+    auto mbset = [&](uint32_t k, uint32_t v) { if constexpr (MBL) lmbox[k * BLOCK] = v; else mboxS[k] = v; };
 #pragma unroll
     for (int i = 0; i < 8; ++i) mbset(i, 0xffffffffu);
     const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
@@ -585,9 +603,11 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             n = nodes[node];
         }
         for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
-            const uint32_t prim = indices[e];
-            if (mb(prim & 7u) == prim) continue;   // the hashed mailbox (sahkdtree3.h:138-152)
-            const MtsgTri &tr = tris[prim];
+            // the record of list entry e (tris in leaf-list order): its loads do
+            // not wait on indices[e], and the test is formed before the mailbox
+            // decides whether it counts, so no load sits behind that branch
+            const MtsgTri &tr = tris[e];
+            const uint32_t prim = tr.prim;
             const uint32_t k = tr.k;
             float o_u, o_v, o_k, d_u, d_v, d_k;
             if (k == 0) { o_u = o.y; o_v = o.z; o_k = o.x; d_u = d.y; d_v = d.z; d_k = d.x; }
@@ -595,17 +615,16 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             else { o_u = o.x; o_v = o.y; o_k = o.z; d_u = d.x; d_v = d.y; d_k = d.z; }
             // TriAccel::rayIntersect (triaccel.h:92-160) on [mint, maxt]
             const float t = (tr.n_d - o_u * tr.n_u - o_v * tr.n_v - o_k) / (d_u * tr.n_u + d_v * tr.n_v + d_k);
-            if (!(t < mint || t > maxt)) {
-                const float hu = o_u + t * d_u - tr.a_u;
-                const float hv = o_v + t * d_v - tr.a_v;
-                const float u = hv * tr.b_nu + hu * tr.b_nv;
-                const float v = hu * tr.c_nu + hv * tr.c_nv;
-                if (u >= 0 && v >= 0 && u + v <= 1.0f) {
-                    if (ANY) return true;
-                    maxt = t;
-                    found = true;
-                    bt = t; bu = u; bv = v; bprim = prim;
-                }
+            const float hu = o_u + t * d_u - tr.a_u;
+            const float hv = o_v + t * d_v - tr.a_v;
+            const float u = hv * tr.b_nu + hu * tr.b_nv;
+            const float v = hu * tr.c_nu + hv * tr.c_nv;
+            if (mb(prim & 7u) == prim) continue;   // the hashed mailbox (sahkdtree3.h:138-152)
+            if (!(t < mint || t > maxt) && u >= 0 && v >= 0 && u + v <= 1.0f) {
+                if (ANY) return true;
+                maxt = t;
+                found = true;
+                bt = t; bu = u; bv = v; bprim = prim;
             }
             mbset(prim & 7u, prim);
         }

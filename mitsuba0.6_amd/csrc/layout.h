@@ -299,10 +299,11 @@ struct MtsgLaunch {
     // MTSGPU_FLAG_KDTREE (wavefront engine): wf_trace traverses the reference's kd-tree
     const uint32_t *kd_nodes;         // KDNode words (2 per node), null: the BVH
     const uint32_t *kd_indices;
-    const MtsgTri *kd_tris;           // TriAccel records in global primitive order
+    const MtsgTri *kd_tris;           // TriAccel records in leaf-list order (kd_tris[e]: primitive kd_indices[e])
     uint32_t scan;                    // tiny scene: linear TriAccel scan instead of the BVH (SCENE_LDS only)
     const MtsgTri *scan_tris;         // the scan's TriAccel records grouped by projection axis k = 0, 1, 2
-    uint32_t scan_n[3];               // (degenerate k = 3 records dropped); counts per group
+    uint32_t scan_n[6];               // and within k by n_u = n_v = 0 (2k: general, 2k+1: axis-aligned plane);
+                                      // degenerate k = 3 records dropped; counts per group
     uint32_t num_verts, num_shapes;   // sizes of the triangle data SCENE_LDS kernels stage in LDS
     int32_t integrator;               // MTSGPU_INTEGRATOR_*
     uint32_t sampler;                 // MTSGPU_SAMPLER_*

@@ -289,15 +289,20 @@ __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave 
 // the trace kernel: both ray queues of the bounce; closest-hit rays' slots are
 // sorted into the next bounce's per-kind queues
 // ---------------------------------------------------------------------------
-// KD: the reference's kd-tree (kd_traverse); KDK > 0: its mailbox and first
-// KDK stack entries in LDS (40 KB per block at KDK = 8: 4 waves/SIMD, so the
-// kernel is compiled for 4 and keeps its state in registers)
+// KD: the reference's kd-tree (kd_traverse); its first KDK stack entries
+// (16 B per lane each) and, KDMB, its mailbox (32 B per lane) in LDS.  Up to
+// 80 B per lane the kernel keeps MTSG_WF_TRACE_WAVES = 8 waves/SIMD (160 KB
+// of LDS over 2048 lanes); above, it is compiled for 4
 #ifndef MTSG_WF_KD_LDSK
-#define MTSG_WF_KD_LDSK 8
+#define MTSG_WF_KD_LDSK 0
 #endif
-template <bool STATS, bool SCENE_LDS, bool ANA, bool KD, int KDK = 0>
-__global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) void wf_trace(MtsgLaunch L, MtsgWave W,
-                                                                       unsigned long long *part) {
+#ifndef MTSG_WF_KD_MBL
+#define MTSG_WF_KD_MBL 1
+#endif
+constexpr uint32_t wf_kd_lds_lane_bytes(int kdk, bool kdmb) { return (uint32_t)kdk * 16u + (kdmb ? 32u : 0u); }
+template <bool STATS, bool SCENE_LDS, bool ANA, bool KD, int KDK = 0, bool KDMB = false>
+__global__ __launch_bounds__(BLOCK, (KD && wf_kd_lds_lane_bytes(KDK, KDMB) > 80) ? 4 : MTSG_WF_TRACE_WAVES) void wf_trace(
+    MtsgLaunch L, MtsgWave W, unsigned long long *part) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t red[BLOCK / 64 * 16];
     const MtsgDeviceScene &S = L.scene;
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
     uint2 *ovf = W.ovf + ((size_t)blockIdx.x * BLOCK + threadIdx.x) * W.ovf_depth;
     const uint2 *kn = (const uint2 *)L.kd_nodes;
     lds_kdent *kstk = (lds_kdent *)lds + threadIdx.x;
-    lds_w32 *kmb = (lds_w32 *)(lds + (KDK > 0 ? KDK : 1) * BLOCK * 4) + threadIdx.x;
+    lds_w32 *kmb = (lds_w32 *)(lds + KDK * BLOCK * 4) + threadIdx.x;
     unsigned long long cN = 0, cT = 0;
     const float4 *rays = W.ray[p];
     const uint32_t *rslot = W.rslot[p];
@@ -356,7 +361,7 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
         if (!valid) {
         } else if (shadow) {
             bool occ;
-            if constexpr (KD) occ = kd_traverse<true, KDK>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot, kstk, kmb);
+            if constexpr (KD) occ = kd_traverse<true, KDK, KDMB>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot, kstk, kmb);
             else if (SCENE_LDS && L.scan)
                 occ = scan_tris<true, STATS>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);
             else if (SCENE_LDS)
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(BLOCK, (KD && KDK > 0) ? 4 : MTSG_WF_TRACE_WAVES) v
             bool hit;
             uint32_t w = MTSG_WF_NONE, shape = 0, prim = slot;
             if constexpr (KD) {
-                hit = kd_traverse<false, KDK>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot, kstk, kmb);
+                hit = kd_traverse<false, KDK, KDMB>(kn, L.kd_indices, L.kd_tris, o, d, mint, maxt, ht, hu, hv, slot, kstk, kmb);
                 if (hit) { w = prim = slot; shape = S.prim_vtx[4 * (size_t)slot + 3]; }
             } else if (SCENE_LDS && L.scan) {
                 hit = scan_tris<false, STATS>(L, o, d, mint, maxt, slot, hu, hv, ht, cT);

@@ -26,7 +26,10 @@ size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) { return ((size_t)L.lds_dims
 // (the kd trace kernel's mailbox and first stack entries in LDS, round 4: C4 62.2 -> 65.0,
 // C3 356.8 -> 330.2 Msamples/s, profiles/r04_ab_kd_lds.log; the opt-in knob is removed)
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
-    if (L.kd_nodes) return 16;
+#ifdef MTSG_WF_KD_LDS_BYTES   // A/B builds: occupancy capped through the block's LDS
+    if (L.kd_nodes) return MTSG_WF_KD_LDS_BYTES;
+#endif
+    if (L.kd_nodes) return (size_t)wf_kd_lds_lane_bytes(MTSG_WF_KD_LDSK, MTSG_WF_KD_MBL) * BLOCK + 16;
     const bool scan = L.scene_lds && L.scan;
     const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
     const size_t K = std::min<size_t>(L.stack_depth, MTSG_WF_LDS_STACK);
@@ -48,7 +51,9 @@ static WfShadeFn wf_shade_pick(const MtsgLaunch &L, int wk, bool instr, bool ggx
 typedef void (*WfTraceFn)(MtsgLaunch, MtsgWave, unsigned long long *);
 static WfTraceFn wf_trace_pick(const MtsgLaunch &L, bool stats) {
     const bool ana = L.ana != 0;
-    if (L.kd_nodes) return stats ? wf_trace<true, false, false, true> : wf_trace<false, false, false, true>;
+    constexpr int KDK = MTSG_WF_KD_LDSK;
+    constexpr bool KDMB = MTSG_WF_KD_MBL;
+    if (L.kd_nodes) return stats ? wf_trace<true, false, false, true, KDK, KDMB> : wf_trace<false, false, false, true, KDK, KDMB>;
     if (stats) {
         if (L.scene_lds) return ana ? wf_trace<true, true, true, false> : wf_trace<true, true, false, false>;
         return ana ? wf_trace<true, false, true, false> : wf_trace<true, false, false, false>;

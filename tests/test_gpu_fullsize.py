@@ -115,3 +115,24 @@ def test_bsdf_set_beckmann_conductor_scene(gpu_ctx, oracle, monkeypatch):
     _, smp_o, st_o = oracle.render(sc, it, samples=True, libm_mode=0, threads=THREADS)
     _records_equal(smp_s, smp_o)
     assert st_s['rays'] == st_g['rays'] == st_o['rays']
+
+
+def test_strict_normals_runs_generic_kernel_bitexact(gpu_ctx, oracle):
+    """The BSDF-set megakernels are built without strictNormals (MTSG_FEAT_NOSTRICT,
+    round 5): a large scene with strictNormals runs the generic kernel (counter 15
+    shows no set bits) and stays bit-exact against the oracle, path and volpath
+    (path.cpp:158-160, 196-197, 243-246; volpath.cpp:214-221)."""
+    from mitsuba_amd.scene import VolpathIntegrator
+    sc, it = scenes.build('C4')
+    win = (0, 300, 320, 1)
+    gpu_ctx.upload(sc)
+    it.strictNormals = True
+    for integ in (it, VolpathIntegrator(sampleCount=64, rfilter='box', strictNormals=True)):
+        _, smp_g, st_g = gpu_ctx.render(integ, window=win, samples=True)
+        assert gpu_ctx.debug_counters()[15] & (FEAT_GGX | FEAT_NORD | FEAT_NORC) == 0, 'a BSDF-set kernel ran'
+        _, smp_o, st_o = oracle.render(sc, integ, window=win, samples=True, libm_mode=0, threads=THREADS)
+        _records_equal(smp_g, smp_o)
+        assert st_g['rays'] == st_o['rays'] and st_g['path_length_sum'] == st_o['path_length_sum']
+    it.strictNormals = False
+    _, smp_s, _ = gpu_ctx.render(it, window=win, samples=True)
+    assert gpu_ctx.debug_counters()[15] & (FEAT_GGX | FEAT_NORD | FEAT_NORC), 'no BSDF-set kernel ran'
