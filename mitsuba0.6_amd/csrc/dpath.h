@@ -518,18 +518,24 @@ __device__ __forceinline__ bool aabb_clip(const MtsgDeviceScene &S, f3 o, f3 d, 
 // a hit at t == maxt: among exactly tied triangles the last one tested wins,
 // as in the reference.  TriAccel records are in leaf-list order (tris[e] is
 // the record of primitive indices[e], duplicated where leaves share one).
-// The reference's stack entry holds the entry/exit point p = ray(t) with
-// p[axis] = split; here an entry keeps (node, t, split, prev | axis << 8),
-// 16 B instead of 24, and p[a] is re-formed as split (a == axis) or o[a] +
-// d[a] * t — the same rounded product and sum the reference stores, so every
-// comparison sees the same floats.  The entry and exit points the descent
-// compares against are held in registers (only a push or a pop changes them),
-// so a descent step reads no stack memory.  LDSK = 0: the stack and the
-// mailbox live in scratch; LDSK > 0 (the wavefront engine's kd trace kernel):
-// the first LDSK stack entries live in LDS, lane-strided (lstk[entry *
-// BLOCK]), deeper entries in scratch; MBL: the mailbox in LDS (lmbox[slot *
-// BLOCK]).
-struct KdEnt { uint32_t node; float t; float split; uint32_t prev_axis; };
+// The reference's stack (entries indexed by enPt / exPt, each with a prev
+// link to the exit point below it) holds the pending far children in push
+// order: every pop takes the most recent live push, and a push never
+// overwrites a live entry (it lands above exPt, skipping enPt).  So here it is
+// a plain LIFO whose entry keeps the far child and, by value, the exit point
+// that was current when it was pushed -- what the reference reaches through
+// prev -- and a pop is one stack read instead of three dependent ones.  A
+// point (t, split, axis) is p = ray(t) with p[axis] = split; p[a] is re-formed
+// as split (a == axis) or o[a] + d[a] * t, the same rounded product and sum
+// the reference stores, so every comparison sees the same floats.  The entry
+// and exit points the descent compares against are held in registers (only a
+// push or a pop changes them), so a descent step reads no stack memory.  The
+// reference's bottom entries, ray(mint) and ray(maxt) with node NONE, become
+// the initial registers and the empty stack.  LDSK = 0: the stack lives in
+// scratch; LDSK > 0: its first LDSK entries live in LDS, lane-strided
+// (lstk[entry * BLOCK]), deeper entries in scratch; MBL: the mailbox in LDS
+// (lmbox[slot * BLOCK]), else in scratch.
+struct KdEnt { uint32_t node; float t; float split; uint32_t axis; };
 typedef __attribute__((address_space(3))) vu4 lds_kdent;
 typedef __attribute__((address_space(3))) uint32_t lds_w32;
 template <bool ANY, int LDSK = 0, bool MBL = (LDSK > 0)>
@@ -538,8 +544,8 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
                             float &bu, float &bv, uint32_t &bprim, lds_kdent *lstk = nullptr,
                             lds_w32 *lmbox = nullptr) {
     typedef KdEnt Ent;
-    constexpr uint32_t NONE = 0xffffffffu, NOAXIS = 3u;
-    Ent stackS[48 - LDSK];
+    constexpr uint32_t NOAXIS = 3u, DEPTH = 46;   // MTS_KD_MAXDEPTH = 48 entries, two of them the bottom
+    Ent stackS[DEPTH - LDSK];
     uint32_t mboxS[MBL ? 1 : 8];
     // entry i: LDS below LDSK, scratch above
     auto ld = [&](uint32_t i) -> Ent {
@@ -550,7 +556,7 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         return stackS[i - LDSK];
     };
     auto st = [&](uint32_t i, const Ent &e) {
-        if (LDSK && i < (uint32_t)LDSK) lstk[i * BLOCK] = vu4{e.node, __float_as_uint(e.t), __float_as_uint(e.split), e.prev_axis};
+        if (LDSK && i < (uint32_t)LDSK) lstk[i * BLOCK] = vu4{e.node, __float_as_uint(e.t), __float_as_uint(e.split), e.axis};
         else stackS[i - LDSK] = e;
     };
     auto mb = [&](uint32_t k) -> uint32_t { if constexpr (MBL) return lmbox[k * BLOCK]; else return mboxS[k]; };
@@ -558,21 +564,19 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
 #pragma unroll
     for (int i = 0; i < 8; ++i) mbset(i, 0xffffffffu);
     const float rcp[3] = {1.0f / d.x, 1.0f / d.y, 1.0f / d.z};   // Ray::setDirection (ray.h:86-93)
-    // p[a] of an entry (t, split, eaxis): the stored point of sahkdtree3.h:239-244
+    // p[a] of a point (t, split, eaxis): the stored point of sahkdtree3.h:239-244
     auto pt = [&](float t, float split, uint32_t eaxis, int a) -> float {
         if ((uint32_t)a == eaxis) return split;
         const float oa = a == 0 ? o.x : (a == 1 ? o.y : o.z);
         const float da = a == 0 ? d.x : (a == 1 ? d.y : d.z);
         return oa + da * t;
     };
-    uint32_t enPt = 0, exPt = 1;
-    st(0, Ent{0u, mint, 0.0f, NOAXIS << 8});              // ray(mint)
-    st(1, Ent{NONE, maxt, 0.0f, NOAXIS << 8});            // ray(maxt)
-    float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;
+    uint32_t sp = 0;
+    float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;   // ray(mint), ray(maxt)
     uint32_t en_axis = NOAXIS, ex_axis = NOAXIS;
     bool found = false;
     uint32_t node = 0;
-    while (node != NONE) {
+    while (true) {
         uint2 n = nodes[node];
         while (!(n.x & 0x80000000u)) {
             const float split = __uint_as_float(n.y);
@@ -593,20 +597,26 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             }
             const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
             const float distToSplit = (split - oa) * rcp[axis];
-            const uint32_t tmp = exPt++;
-            if (exPt == enPt) ++exPt;
-            if (exPt >= 48) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-            st(exPt, Ent{farChild, distToSplit, split, tmp | ((uint32_t)axis << 8)});
+            if (sp >= DEPTH) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
+            st(sp++, Ent{farChild, ex_t, ex_split, ex_axis});
             ex_t = distToSplit;
             ex_split = split;
             ex_axis = (uint32_t)axis;
             n = nodes[node];
         }
+#ifdef MTSG_KD_PREFETCH
+        MtsgTri nx = tris[n.x & 0x7fffffffu];   // (an empty leaf's start is at most the padding record)
+#endif
         for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
             // the record of list entry e (tris in leaf-list order): its loads do
             // not wait on indices[e], and the test is formed before the mailbox
             // decides whether it counts, so no load sits behind that branch
+#ifdef MTSG_KD_PREFETCH
+            const MtsgTri tr = nx;
+            nx = tris[e + 1];   // the array holds one record past the last entry
+#else
             const MtsgTri &tr = tris[e];
+#endif
             const uint32_t prim = tr.prim;
             const uint32_t k = tr.k;
             float o_u, o_v, o_k, d_u, d_v, d_k;
@@ -629,16 +639,15 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             mbset(prim & 7u, prim);
         }
         if (ex_t > maxt) break;
-        enPt = exPt;
+        if (sp == 0) break;   // the exit point was ray(maxt), whose node is NONE
         en_t = ex_t;
         en_split = ex_split;
         en_axis = ex_axis;
-        node = ld(exPt).node;
-        exPt = ld(enPt).prev_axis & 0xffu;
-        const Ent e = ld(exPt);
+        const Ent e = ld(--sp);
+        node = e.node;
         ex_t = e.t;
         ex_split = e.split;
-        ex_axis = e.prev_axis >> 8;
+        ex_axis = e.axis;
     }
     return found;
 }

@@ -23,12 +23,13 @@ __global__ void wf_flush(const unsigned long long *part, uint32_t blocks, unsign
 // host-side launchers (capi.cpp)
 // ---------------------------------------------------------------------------
 size_t mtsg_wf_shade_lds_bytes(const MtsgLaunch &L) { return ((size_t)L.lds_dims * L.nibbles * 16 + 16 * 16) * 4; }
-// (the kd trace kernel's mailbox and first stack entries in LDS, round 4: C4 62.2 -> 65.0,
-// C3 356.8 -> 330.2 Msamples/s, profiles/r04_ab_kd_lds.log; the opt-in knob is removed)
+// The kd trace kernel: its mailbox in LDS at 8 waves/SIMD, the stack in scratch
+// (round 5, profiles/r05_ab_kd_mailbox_lds.log: C4 65.8 -> 76.9, C3 370 -> 398
+// Msamples/s; with the first 3 stack entries in LDS as well 75.1 / 371; the
+// scratch-only kernel capped at 4 waves through its LDS 54.0 / 278).  Round 4's
+// mailbox plus 8 entries at 4 waves: C4 62.2 -> 65.0, C3 356.8 -> 330.2
+// (profiles/r04_ab_kd_lds.log)
 size_t mtsg_wf_trace_lds_bytes(const MtsgLaunch &L) {
-#ifdef MTSG_WF_KD_LDS_BYTES   // A/B builds: occupancy capped through the block's LDS
-    if (L.kd_nodes) return MTSG_WF_KD_LDS_BYTES;
-#endif
     if (L.kd_nodes) return (size_t)wf_kd_lds_lane_bytes(MTSG_WF_KD_LDSK, MTSG_WF_KD_MBL) * BLOCK + 16;
     const bool scan = L.scene_lds && L.scan;
     const size_t scene = (L.scene_lds && !L.scan) ? ((size_t)L.num_nodes * 16 + (size_t)L.scene.num_prims * 12) : 0;
