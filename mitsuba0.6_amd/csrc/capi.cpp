@@ -1037,7 +1037,7 @@ int ensure_kdtree(mtsgpu_ctx *ctx) {
     // leaf's records are read without the indices[e] -> record dependence
     std::vector<MtsgTri> lt(ctx->kd.indices.size());
     for (size_t i = 0; i < lt.size(); ++i) lt[i] = tg[ctx->kd.indices[i]];
-    lt.push_back(MtsgTri{});   // one record past the last entry: the leaf loop may read ahead
+    lt.push_back(MtsgTri{});   // one record past the last entry (reading ahead in the leaf loop lost 1-3%, r05)
     if ((e = upload(ctx->kd_nodes, ctx->kd.nodes, ctx->stream)) != hipSuccess ||
         (e = upload(ctx->kd_indices, ctx->kd.indices, ctx->stream)) != hipSuccess ||
         (e = upload(ctx->kd_tris, lt, ctx->stream)) != hipSuccess || (e = hipStreamSynchronize(ctx->stream)) != hipSuccess)

@@ -604,19 +604,11 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             ex_axis = (uint32_t)axis;
             n = nodes[node];
         }
-#ifdef MTSG_KD_PREFETCH
-        MtsgTri nx = tris[n.x & 0x7fffffffu];   // (an empty leaf's start is at most the padding record)
-#endif
         for (uint32_t e = n.x & 0x7fffffffu; e != n.y; ++e) {
             // the record of list entry e (tris in leaf-list order): its loads do
             // not wait on indices[e], and the test is formed before the mailbox
             // decides whether it counts, so no load sits behind that branch
-#ifdef MTSG_KD_PREFETCH
-            const MtsgTri tr = nx;
-            nx = tris[e + 1];   // the array holds one record past the last entry
-#else
             const MtsgTri &tr = tris[e];
-#endif
             const uint32_t prim = tr.prim;
             const uint32_t k = tr.k;
             float o_u, o_v, o_k, d_u, d_v, d_k;
