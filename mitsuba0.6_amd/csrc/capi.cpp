@@ -1035,6 +1035,7 @@ int ensure_kdtree(mtsgpu_ctx *ctx) {
     hipError_t e;
     // the TriAccel records in leaf-list order (one per primitive reference), so a
     // leaf's records are read without the indices[e] -> record dependence
+    if (ctx->kd.nodes.size() / 2 >= (1u << 30)) return fail(ctx, MTSGPU_EINVAL, "kd-tree: more than 2^30 nodes");
     std::vector<MtsgTri> lt(ctx->kd.indices.size());
     for (size_t i = 0; i < lt.size(); ++i) lt[i] = tg[ctx->kd.indices[i]];
     lt.push_back(MtsgTri{});   // one record past the last entry (reading ahead in the leaf loop lost 1-3%, r05)

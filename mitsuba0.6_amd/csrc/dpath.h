@@ -436,10 +436,29 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
 // the records are loaded once, and the pairs of products pack into
 // v_pk_mul/v_pk_add.  Each ray's result is exactly that of its own scan_tris
 // (an empty interval, mint = +inf and maxt = -inf, disables a ray).
-template <int K, bool AL, bool STATS>
+// a / b from y = RN(1/b) (correctly rounded, computed once per ray): the
+// quotient a * y with two residual corrections, r = a - b q exact by FMA and
+// q' = RN(q + r y) (Markstein's theorem: with y = RN(1/b) and q within an ulp
+// of a/b, q' = RN(a/b)).  It equals IEEE a / b wherever nothing underflows;
+// scan_pair takes it only for rays with |b| >= 2^-60 and mint >= 2^-30, where
+// a quotient small enough to underflow is rejected by mint either way.  Host
+// check: 1.6e9 random and edge-mantissa pairs over that range, bit-equal to
+// IEEE division (tools/r05/fast_div_check.c).
+__device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
+    float q = a * y;
+    float r = __builtin_fmaf(-b, q, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-b, q, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// FAST (axis-aligned groups only): the two quotients through div_by_rcp with
+// the rays' reciprocals yS = RN(1/s_k), yC = RN(1/c_k)
+template <int K, bool AL, bool FAST, bool STATS>
 __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 ds, f3 dc, float minS, float maxS,
                                             float minC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
-                                            float &bv, float &bt, unsigned long long &tests) {
+                                            float &bv, float &bt, unsigned long long &tests, float yS = 0,
+                                            float yC = 0) {
     const float o_u = K == 0 ? o.y : K == 1 ? o.z : o.x, o_v = K == 0 ? o.z : K == 1 ? o.x : o.y,
                 o_k = K == 0 ? o.x : K == 1 ? o.y : o.z;
     const float s_u = K == 0 ? ds.y : K == 1 ? ds.z : ds.x, s_v = K == 0 ? ds.z : K == 1 ? ds.x : ds.y,
@@ -455,8 +474,8 @@ __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 
         // TriAccel::rayIntersect (triaccel.h:92-160) for both rays
         // (AL: as in scan_k)
         const float num = AL ? n_d - o_k : n_d - o_u * n_u - o_v * n_v - o_k;
-        const float tS = num / (AL ? s_k : s_u * n_u + s_v * n_v + s_k);
-        const float tC = num / (AL ? c_k : c_u * n_u + c_v * n_v + c_k);
+        const float tS = (AL && FAST) ? div_by_rcp(num, s_k, yS) : num / (AL ? s_k : s_u * n_u + s_v * n_v + s_k);
+        const float tC = (AL && FAST) ? div_by_rcp(num, c_k, yC) : num / (AL ? c_k : c_u * n_u + c_v * n_v + c_k);
         if (!(tS < minS || tS > maxS)) {
             const float hu = o_u + tS * s_u - a_u;
             const float hv = o_v + tS * s_v - a_v;
@@ -487,12 +506,25 @@ __device__ __forceinline__ void scan_pair(const MtsgLaunch &L, f3 o, f3 ds, f3 d
     found = false;
     bestPrim = 0;
     bt = maxC;
-#define MTSG_SCAN_GROUP(K, AL)                                                                                    \
-    scan_pair_k<K, AL, STATS>(tris, L.scan_n[2 * K + AL], o, ds, dc, minS, maxS, minC, occ, found, bestPrim, bu, bv, \
-                              bt, tests);                                                                         \
-    tris += L.scan_n[2 * K + AL];
-    MTSG_SCAN_GROUP(0, false) MTSG_SCAN_GROUP(0, true) MTSG_SCAN_GROUP(1, false) MTSG_SCAN_GROUP(1, true)
-    MTSG_SCAN_GROUP(2, false) MTSG_SCAN_GROUP(2, true)
+    // a disabled ray (empty interval) may take the fast quotient whatever its direction
+    const bool offS = !(minS <= maxS), offC = !(minC <= maxC);
+#define MTSG_SCAN_GROUP(K)                                                                                         \
+    scan_pair_k<K, false, false, STATS>(tris, L.scan_n[2 * K], o, ds, dc, minS, maxS, minC, occ, found, bestPrim,   \
+                                        bu, bv, bt, tests);                                                        \
+    tris += L.scan_n[2 * K];                                                                                       \
+    if (L.scan_n[2 * K + 1]) {                                                                                     \
+        const float s_k = K == 0 ? ds.x : K == 1 ? ds.y : ds.z, c_k = K == 0 ? dc.x : K == 1 ? dc.y : dc.z;        \
+        const bool fast = (offS || (minS >= 0x1p-30f && fabsf(s_k) >= 0x1p-60f)) &&                                \
+                          (offC || (minC >= 0x1p-30f && fabsf(c_k) >= 0x1p-60f));                                  \
+        if (__all(fast))                                                                                           \
+            scan_pair_k<K, true, true, STATS>(tris, L.scan_n[2 * K + 1], o, ds, dc, minS, maxS, minC, occ, found,  \
+                                              bestPrim, bu, bv, bt, tests, 1.0f / s_k, 1.0f / c_k);                \
+        else                                                                                                       \
+            scan_pair_k<K, true, false, STATS>(tris, L.scan_n[2 * K + 1], o, ds, dc, minS, maxS, minC, occ, found, \
+                                               bestPrim, bu, bv, bt, tests);                                       \
+        tris += L.scan_n[2 * K + 1];                                                                               \
+    }
+    MTSG_SCAN_GROUP(0) MTSG_SCAN_GROUP(1) MTSG_SCAN_GROUP(2)
 #undef MTSG_SCAN_GROUP
 }
 
@@ -580,6 +612,16 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         return oa + da * t;
     };
     uint32_t sp = 0;
+    // the newest stack entries held in registers (entries sp - 1, sp - 2, ... of
+    // the nr cached), the rest in memory; a cached entry packs its axis into the
+    // node word's top bits (kd node indices stay below 2^30)
+#if MTSG_KD_REGTOP == 2
+    uint32_t nr = 0, c0n = 0, c1n = 0;
+    float c0t = 0, c0s = 0, c1t = 0, c1s = 0;
+#else
+    bool top = false;
+    Ent topE = Ent{0u, 0.0f, 0.0f, 0u};
+#endif
     float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;   // ray(mint), ray(maxt)
     uint32_t en_axis = NOAXIS, ex_axis = NOAXIS;
     bool found = false;
@@ -606,7 +648,18 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
             const float distToSplit = (split - oa) * rcp[axis];
             if (sp >= DEPTH) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-            st(sp++, Ent{farChild, ex_t, ex_split, ex_axis});
+#if MTSG_KD_REGTOP == 2
+            if (nr == 2) st(sp - 2, Ent{c1n & 0x3fffffffu, c1t, c1s, c1n >> 30});
+            c1n = c0n; c1t = c0t; c1s = c0s;
+            c0n = farChild | (ex_axis << 30); c0t = ex_t; c0s = ex_split;
+            nr = nr < 2 ? nr + 1 : 2;
+            ++sp;
+#else
+            if (top) st(sp - 1, topE);
+            topE = Ent{farChild, ex_t, ex_split, ex_axis};
+            top = true;
+            ++sp;
+#endif
             ex_t = distToSplit;
             ex_split = split;
             ex_axis = (uint32_t)axis;
@@ -643,7 +696,21 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         en_t = ex_t;
         en_split = ex_split;
         en_axis = ex_axis;
-        const Ent e = ld(--sp);
+#if MTSG_KD_REGTOP == 2
+        Ent e;
+        if (nr) {
+            e = Ent{c0n & 0x3fffffffu, c0t, c0s, c0n >> 30};
+            c0n = c1n; c0t = c1t; c0s = c1s;
+            --nr;
+        } else {
+            e = ld(sp - 1);
+        }
+        --sp;
+#else
+        const Ent e = top ? topE : ld(sp - 1);
+        top = false;
+        --sp;
+#endif
         node = e.node;
         ex_t = e.t;
         ex_split = e.split;
