@@ -612,16 +612,11 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         return oa + da * t;
     };
     uint32_t sp = 0;
-    // the newest stack entries held in registers (entries sp - 1, sp - 2, ... of
-    // the nr cached), the rest in memory; a cached entry packs its axis into the
-    // node word's top bits (kd node indices stay below 2^30)
-#if MTSG_KD_REGTOP == 2
+    // the two newest stack entries held in registers (entries sp - 1 and sp - 2
+    // when nr = 2), the rest in memory; a cached entry packs its axis into the
+    // node word's top bits (kd node indices stay below 2^30, capi.cpp)
     uint32_t nr = 0, c0n = 0, c1n = 0;
     float c0t = 0, c0s = 0, c1t = 0, c1s = 0;
-#else
-    bool top = false;
-    Ent topE = Ent{0u, 0.0f, 0.0f, 0u};
-#endif
     float en_t = mint, en_split = 0, ex_t = maxt, ex_split = 0;   // ray(mint), ray(maxt)
     uint32_t en_axis = NOAXIS, ex_axis = NOAXIS;
     bool found = false;
@@ -648,18 +643,11 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
             const float distToSplit = (split - oa) * rcp[axis];
             if (sp >= DEPTH) return found;   // MTS_KD_MAXDEPTH bounds the tree depth; never taken
-#if MTSG_KD_REGTOP == 2
             if (nr == 2) st(sp - 2, Ent{c1n & 0x3fffffffu, c1t, c1s, c1n >> 30});
             c1n = c0n; c1t = c0t; c1s = c0s;
             c0n = farChild | (ex_axis << 30); c0t = ex_t; c0s = ex_split;
             nr = nr < 2 ? nr + 1 : 2;
             ++sp;
-#else
-            if (top) st(sp - 1, topE);
-            topE = Ent{farChild, ex_t, ex_split, ex_axis};
-            top = true;
-            ++sp;
-#endif
             ex_t = distToSplit;
             ex_split = split;
             ex_axis = (uint32_t)axis;
@@ -696,7 +684,6 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
         en_t = ex_t;
         en_split = ex_split;
         en_axis = ex_axis;
-#if MTSG_KD_REGTOP == 2
         Ent e;
         if (nr) {
             e = Ent{c0n & 0x3fffffffu, c0t, c0s, c0n >> 30};
@@ -706,11 +693,6 @@ __device__ bool kd_traverse(const uint2 *__restrict__ nodes, const uint32_t *__r
             e = ld(sp - 1);
         }
         --sp;
-#else
-        const Ent e = top ? topE : ld(sp - 1);
-        top = false;
-        --sp;
-#endif
         node = e.node;
         ex_t = e.t;
         ex_split = e.split;
