@@ -241,10 +241,12 @@ __device__ __forceinline__ bool traverse(NodeT *nodesArr, TriT *trisArr, f3 o, f
         while (sp > 0) {
             --sp;
             if (LDSK == 0 || sp < LDSK) {
-                // the entry's node and distance read together: the empty asm keeps
-                // the node read ahead of the cull test instead of behind it, one LDS
-                // round trip per pop instead of two (round 5: C3 +2.0%, C4 +1.6%,
-                // C5 +1.2%, profiles/r05_ab_pop_both.log)
+                // the entry's node read ahead of the cull test (the empty asm pins it
+                // there) instead of inside the taken branch: C3 +2.0%, C4 +1.6%, C5
+                // +1.2% (round 5, profiles/r05_ab_pop_both.log).  Both reads issued
+                // before one wait lost 1.1-1.6% against this (r05_ab_pop_onewait.log),
+                // so the gain is in the shape of the compiled pop loop, not in LDS
+                // round trips
                 int n = stkN[sp * BLOCK];
                 asm volatile("" : "+v"(n));
                 if (ANY || dist_up16(stkD[sp * BLOCK]) <= bt) return n;
