@@ -52,6 +52,26 @@ def oracle():
 
 
 @pytest.fixture(scope='session')
+def c5_reference_tables(tmp_path_factory):
+    """A directory holding a ggx.dat whose eta layers at C5's relative IOR are the
+    reference's own (tests/golden/rtrans_c5_ggx_layers.npz, made by
+    make_rtrans_layers.py from data/microfacet/ggx.dat) and whose other layers
+    are the generated table's.  setEta reads only those layers
+    (spline.cpp:379-450), so C5's reduced 2D tables are the reference file's."""
+    import numpy as np
+    from mitsuba_amd import rtrans
+    fx = np.load(os.path.join(REPO, 'tests', 'golden', 'rtrans_c5_ggx_layers.npz'))
+    raw = open(os.path.join(rtrans.GENERATED_DIR, 'ggx.dat'), 'rb').read()
+    hdr = fx['header'].tobytes()
+    assert raw[:len(hdr)] == hdr, 'generated ggx.dat header differs from the reference file'
+    t = np.frombuffer(raw, '<f4', offset=len(hdr)).copy().reshape((-1,) + fx['layers'].shape[1:])
+    t[fx['rows']] = fx['layers']
+    d = tmp_path_factory.mktemp('c5_reference_tables')
+    (d / 'ggx.dat').write_bytes(hdr + t.astype('<f4').tobytes())
+    return str(d)
+
+
+@pytest.fixture(scope='session')
 def gpu_ctx():
     from mitsuba_amd.integrator import Context
     return Context()

@@ -63,6 +63,26 @@ def test_full_resolution_row_band_bitexact(gpu_ctx, oracle, cfg, rows):
     assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
 
 
+def test_c5_row_band_on_reference_table_layers(gpu_ctx, oracle, c5_reference_tables):
+    """C5's configuration (1280 wide, 1024 spp, full envmap and blob) on the
+    reference's own ggx.dat values at C5's eta (conftest.c5_reference_tables):
+    the row band bit-exact against the oracle on the same table."""
+    from mitsuba_amd import rtrans
+    sc, it = scenes.build('C5')
+    for b in sc.bsdfs:
+        if b.type == 'roughplastic':
+            b.rtransDir = c5_reference_tables
+    rtrans._cache.clear()
+    win = (0, 360, sc.sensor.width, 1)
+    gpu_ctx.upload(sc)
+    _, smp_g, st_g = gpu_ctx.render(it, window=win, samples=True)
+    _, smp_o, st_o = oracle.render(sc, it, window=win, samples=True, libm_mode=0, threads=THREADS)
+    rtrans._cache.clear()
+    assert st_g['samples'] == st_o['samples'] == 1280 * 1024
+    _records_equal(smp_g, smp_o)
+    assert st_g['rays'] == st_o['rays'] and st_g['shadow_rays'] == st_o['shadow_rays']
+
+
 @pytest.mark.parametrize('cfg', ['C3', 'C4', 'C5'])
 def test_bsdf_set_variant_equals_generic(gpu_ctx, cfg, monkeypatch):
     """C3-C5 render through a megakernel specialised to the scene's BSDF set

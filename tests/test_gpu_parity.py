@@ -191,6 +191,31 @@ def test_c5_textured_roughplastic_bitexact(gpu_ctx, oracle):
     _compare(film_g, smp_g, film_o, smp_o)
 
 
+def test_c5_reference_table_layers_bitexact(gpu_ctx, oracle, c5_reference_tables):
+    """C5 on the reference's own rough-transmittance values: ggx.dat with the eta
+    layers C5's roughplastic reads taken from data/microfacet/ggx.dat
+    (tests/golden/rtrans_c5_ggx_layers.npz; the host test
+    test_c5_layer_fixture_equals_reference_file shows the oracle renders it as it
+    renders the full reference file).  GPU = oracle bit for bit, and the records
+    differ from the generated table's: the values reached the device."""
+    from mitsuba_amd import rtrans
+    recs = []
+    for d in (c5_reference_tables, rtrans.GENERATED_DIR):
+        sc, it = scenes.build('C5', width=48, height=27, spp=8, env_size=(128, 64), blob=(60, 38))
+        for b in sc.bsdfs:
+            if b.type == 'roughplastic':
+                b.rtransDir = d
+        rtrans._cache.clear()
+        gpu_ctx.upload(sc)
+        film_g, smp_g, _ = gpu_ctx.render(it, samples=True)
+        recs.append(_bits(smp_g))
+        if d == c5_reference_tables:
+            film_o, smp_o, _ = oracle.render(sc, it, samples=True, libm_mode=0)
+            _compare(film_g, smp_g, film_o, smp_o)
+    rtrans._cache.clear()
+    assert not np.array_equal(recs[0], recs[1])
+
+
 def test_smooth_bsdfs_bitexact(gpu_ctx, oracle):
     """Delta BSDFs (conductor, dielectric, plastic with textured nonlinear base) and
     twosided (one nested BSDF; two nested with the back side in view): no NEE on

@@ -112,6 +112,55 @@ def test_c5_configuration_row_band_reference_vs_generated_tables(oracle):
     assert per_pixel.max() < 1e-3, per_pixel.max()
 
 
+def _set_rtrans_dir(sc, d):
+    n = 0
+    for b in sc.bsdfs:
+        if b.type == 'roughplastic':
+            b.rtransDir = d
+            n += 1
+    assert n > 0
+    rtrans._cache.clear()
+
+
+def test_c5_layer_fixture_carries_reference_values(c5_reference_tables):
+    """The fixture's layers are not the generated table's (34-46% of the entries
+    differ), and the hybrid file is a valid table for configure()."""
+    import numpy as np
+    fx = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'rtrans_c5_ggx_layers.npz'))
+    _, _, gen = _load(os.path.join(rtrans.GENERATED_DIR, 'ggx.dat'))
+    _, _, hyb = _load(os.path.join(c5_reference_tables, 'ggx.dat'))
+    assert np.array_equal(hyb[fx['rows']], fx['layers'])
+    assert (gen[fx['rows']] != fx['layers']).mean() > 0.2
+    others = np.setdiff1d(np.arange(hyb.shape[0]), fx['rows'])
+    assert np.array_equal(hyb[others], gen[others])
+    sc, _ = scenes.build('C5', width=16, height=16, spp=1, blob=(24, 16), env_size=(64, 32))
+    _set_rtrans_dir(sc, c5_reference_tables)
+    check_scene(sc)
+    rtrans._cache.clear()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason='reference data not in this container')
+def test_c5_layer_fixture_equals_reference_file(oracle, c5_reference_tables):
+    """The fixture against the file it was cut from (make_rtrans_layers.py), and the
+    proof that the layers it keeps are all C5 reads: the oracle renders a reduced
+    C5 on the reference's ggx.dat and on the hybrid file with the same per-sample
+    records bit for bit (and differently on the generated table)."""
+    import numpy as np
+    fx = np.load(os.path.join(os.path.dirname(__file__), 'golden', 'rtrans_c5_ggx_layers.npz'))
+    _, _, ref = _load(os.path.join(REF, 'ggx.dat'))
+    assert np.array_equal(ref[fx['rows']], fx['layers'])
+    assert open(os.path.join(REF, 'ggx.dat'), 'rb').read(57) == fx['header'].tobytes()
+    recs = []
+    for d in (REF, c5_reference_tables, rtrans.GENERATED_DIR):
+        sc, it = scenes.build('C5', width=48, height=27, spp=8, env_size=(128, 64), blob=(60, 38))
+        _set_rtrans_dir(sc, d)
+        _, smp, _ = oracle.render(sc, it, samples=True, libm_mode=0)
+        recs.append(np.ascontiguousarray(smp, np.float32).view(np.uint32))
+    rtrans._cache.clear()
+    assert np.array_equal(recs[0], recs[1])
+    assert not np.array_equal(recs[0], recs[2])
+
+
 def test_table_resolution_order(tmp_path, monkeypatch):
     (tmp_path / 'ggx.dat').write_bytes(open(os.path.join(rtrans.GENERATED_DIR, 'ggx.dat'), 'rb').read())
     monkeypatch.setenv('MTSGPU_MICROFACET_DIR', str(tmp_path))
