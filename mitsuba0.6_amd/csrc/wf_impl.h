@@ -291,7 +291,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave 
 // ---------------------------------------------------------------------------
 // KD: the reference's kd-tree (kd_traverse); its first KDK stack entries
 // (16 B per lane each) and, KDMB, its mailbox (32 B per lane) in LDS.  Up to
-// 80 B per lane the kernel keeps MTSG_WF_TRACE_WAVES = 8 waves/SIMD (160 KB
+// 80 B per lane the kernel keeps MTSG_WF_KD_TRACE_WAVES = 7 waves/SIMD (160 KB
 // of LDS over 2048 lanes); above, it is compiled for 4
 #ifndef MTSG_WF_KD_LDSK
 #define MTSG_WF_KD_LDSK 0
@@ -300,8 +300,14 @@ __global__ __launch_bounds__(BLOCK, WAVES) void wf_shade(MtsgLaunch L, MtsgWave 
 #define MTSG_WF_KD_MBL 1
 #endif
 constexpr uint32_t wf_kd_lds_lane_bytes(int kdk, bool kdmb) { return (uint32_t)kdk * 16u + (kdmb ? 32u : 0u); }
+// the kd trace kernel at 7 waves/SIMD: 70 VGPRs and no spills, against 64 VGPRs
+// and 19 spilled at 8: C4 91.3 -> 93.4, C3 451.1 -> 456.0 Msamples/s, bit-identical
+// (round 5, profiles/r05_ab_kd_waves.log; 6 waves compiles to the same 70 VGPRs)
+#ifndef MTSG_WF_KD_TRACE_WAVES
+#define MTSG_WF_KD_TRACE_WAVES 7
+#endif
 template <bool STATS, bool SCENE_LDS, bool ANA, bool KD, int KDK = 0, bool KDMB = false>
-__global__ __launch_bounds__(BLOCK, (KD && wf_kd_lds_lane_bytes(KDK, KDMB) > 80) ? 4 : MTSG_WF_TRACE_WAVES) void wf_trace(
+__global__ __launch_bounds__(BLOCK, KD ? (wf_kd_lds_lane_bytes(KDK, KDMB) > 80 ? 4 : MTSG_WF_KD_TRACE_WAVES) : MTSG_WF_TRACE_WAVES) void wf_trace(
     MtsgLaunch L, MtsgWave W, unsigned long long *part) {
     extern __shared__ uint32_t lds[];
     __shared__ uint32_t red[BLOCK / 64 * 16];
