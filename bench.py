@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """bench.py -- Msamples/s of the MI355X `path` integrator on BASELINE config C2,
 and on C3 (matpreview, BASELINE's second north-star scene), C4 (the 200k-triangle
-atrium BASELINE names for tile sharding) and C5 (roughplastic with the
-rough-transmittance lookup) in the same run, as the line's `secondary` blocks
-(one per config, each with its own value, ms_per_step, roofline and CPU
-baseline).
+atrium BASELINE names for tile sharding), C5 (roughplastic with the
+rough-transmittance lookup) and C2g (C2 with the reference's default gaussian
+reconstruction filter) in the same run, as the line's `secondary` blocks (one
+per config, each with its own value, ms_per_step, roofline and CPU baseline).
 
 Workload (BASELINE.json configs[1]): Cornell box, 1280x720, 512 spp, sobol,
 path maxDepth=-1 rrDepth=5, box filter.  One step = one full frame
@@ -46,6 +46,8 @@ WORKLOADS = {
           'envmap only), path maxDepth=-1 rrDepth=5, sobol, box filter',
     'C4': 'C4: atrium (195k tris, 24 fluted columns, roughdielectric GGX a=0.2 eta=1.5 on ~30% of meshes, '
           'diffuse elsewhere, 4 area lights) 1280x720 256 spp, path maxDepth=-1 rrDepth=5, sobol, box filter',
+    'C2g': 'C2g: C2 with the reference\'s default reconstruction filter (gaussian stddev 0.5, 5x5 footprint), '
+           'the film gathered per pixel in a fixed order (film_gather)',
     'C5': 'C5: matpreview with the object in roughplastic GGX, checkerboard-textured alpha (0.05/0.3) -> '
           '2D rough-transmittance slice (50 alpha x 100 theta) per shading point, 1024x512 envmap, 1024 spp, '
           'path maxDepth=-1 rrDepth=5, sobol, box filter',
@@ -64,9 +66,13 @@ def parse_args(argv=None):
     ap.add_argument('--share-device', action='store_true',
                     help='every rank on GPU 0, films reduced over gloo through host memory: a one-GPU rehearsal '
                          'of the N-rank path (tests only; never a measurement)')
+    ap.add_argument('--rccl', action='store_true',
+                    help='create the nccl (RCCL) process group and reduce the film over it even at --gpus 1 '
+                         '(launched through torch.distributed.run --nproc-per-node 1): executes the RCCL merge '
+                         'path on a one-GPU box')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=0)
-    ap.add_argument('--secondary', default='C3,C4,C5',
+    ap.add_argument('--secondary', default='C3,C4,C5,C2g',
                     help="further workloads timed in the same run (comma-separated), each emitted as a block of "
                          "the line's `secondary` object; 'none' to skip")
     return ap.parse_args(argv)
@@ -90,7 +96,7 @@ def launch_ranks(args):
             sys.exit('bench.py: --gpus %d but WORLD_SIZE=%s; launch with --nproc-per-node %d' %
                      (args.gpus, world_env, args.gpus))
         return None
-    if args.gpus == 1:
+    if args.gpus == 1 and not args.rccl:
         return None
     if args.gpus < 1:
         sys.exit('bench.py: --gpus must be >= 1')
@@ -278,7 +284,8 @@ def cpu_baseline(scene, integ, threads):
     rate = (s2 - s1) / max(1e-6, t2 - t1) if t2 > t1 else s2 / max(1e-6, t2)
     fit = 20.0 * rate / (scene.sensor.width * scene.sensor.height)
     spp = 1
-    while spp * 2 <= min(integ.sampleCount, 256) and spp * 2 <= fit * 1.41421356:
+    cap = 256 if integ.rfilter == 'box' else 64   # gather mode keeps every sample's record (28 B) in host memory
+    while spp * 2 <= min(integ.sampleCount, cap) and spp * 2 <= fit * 1.41421356:
         spp *= 2
     it.sampleCount = spp
     t0 = time.perf_counter()
@@ -296,11 +303,13 @@ def build_scene(config, size=None):
     from pkgimport import mitsuba_amd
     mitsuba_amd()
     from mitsuba_amd import scenes
-    kw = {'rfilter': 'box'}
+    # C2g: C2 with Mitsuba's default reconstruction filter, gaussian stddev 0.5
+    # (film.cpp:89-95, gaussian.cpp:35-56), the film gathered in a fixed order (film_gather)
+    kw = {'rfilter': 'gaussian' if config.endswith('g') else 'box'}
     if size:
         w, h, spp = (int(v) for v in size.lower().split('x'))
         kw.update(width=w, height=h, spp=spp)
-    return scenes.build(config, **kw)
+    return scenes.build(config[:-1] if config.endswith('g') else config, **kw)
 
 
 def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
@@ -332,6 +341,8 @@ def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
                 host = film.cpu()
                 shard.reduce(host, dist)
                 film.copy_(host)
+            elif args.rccl and world == 1:        # the RCCL reduce of a one-rank job
+                dist.reduce(film, dst=0, op=dist.ReduceOp.SUM)
             else:
                 shard.reduce(film, dist)
 
@@ -421,12 +432,13 @@ def run_workload(config, args, world, rank, local, dist, torch, lib_hash):
         roofline = roofline_line(bps, per_launch_samples, avg_kernel_s, config, lib_hash)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(scene, integ, args.cpu_threads)
+    film_reduce = ('gloo' if args.share_device and world > 1 else
+                   ('RCCL' if gpu and (world > 1 or args.rccl) else ('gloo' if world > 1 else 'none')))
     return {'value': round(value, 2), 'ms_per_step': round(elapsed_max / args.steps * 1e3, 2),
             'config': {'workload': WORKLOADS.get(config, config), 'width': W, 'height': H, 'spp': spp,
                        'samples_per_frame': frame_samples,
-                       'parallelism': '8x8 tiles dealt over %d rank(s) + %s film reduce' % (
-                           world, 'RCCL' if gpu and not args.share_device else 'gloo'),
-                       'world_size_reported': dist.get_world_size() if world > 1 else 1,
+                       'parallelism': '8x8 tiles dealt over %d rank(s), film reduce: %s' % (world, film_reduce),
+                       'world_size_reported': dist.get_world_size() if dist.is_initialized() else 1,
                        'reduce_ms_max': round(float(r.item()) * 1e3, 3),
                        's_per_frame': round(elapsed_max / args.steps, 4), 'scene_upload_s': round(upload_s, 3)},
             'roofline': roofline, 'cpu_baseline': cpu, 'spp': spp, 'W': W, 'H': H}
@@ -454,7 +466,7 @@ def main():
         torch.cuda.set_device(dev)
         if world > 1 and args.share_device:
             dist.init_process_group('gloo')   # RCCL refuses two ranks on one device
-        elif world > 1:
+        elif world > 1 or args.rccl:
             dist.init_process_group('nccl', device_id=torch.device('cuda', dev))
         lib_hash = lib_sha256()
     elif world > 1:
@@ -493,7 +505,7 @@ def main():
         elif args.share_device:
             out['device'] = 'shared-GPU rehearsal: %d ranks on GPU 0, gloo reduce (not a scaling measurement)' % world
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

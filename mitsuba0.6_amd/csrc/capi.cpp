@@ -23,6 +23,7 @@
 #include "kdtree.h"
 
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
+hipError_t mtsg_launch_gather(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
@@ -728,6 +729,19 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         const int w = std::atoi(env);
         L.waves = w == 4 ? 4u : 3u;
     }
+    // gather mode (film_gather, path_kernel.hip): filters whose footprint covers the
+    // neighbours (gaussian) -- every film pixel sums its neighbourhood's sample records in
+    // a fixed order instead of taking atomic splats.  H = the largest footprint offset from a
+    // sample's pixel: |x - px| <= floor(radius + 1/2) (film_splat's ceil/floor bounds)
+    L.gather = 0;
+    L.gather_h = 0;
+    if (P->rfilter != MTSGPU_RFILTER_BOX) {
+        const int H = std::max(L.filter.border, (int)std::floor(L.filter.radius + 0.5f));
+        if (H >= 1 && H <= MTSG_GATHER_HMAX && !std::getenv("MTSGPU_NO_GATHER")) {
+            L.gather = 1;
+            L.gather_h = (uint32_t)H;
+        }
+    }
     if (const char *env = std::getenv("MTSGPU_SOBOL_LDS_DIMS"))
         L.lds_dims = (uint32_t)std::min(1024l, std::max(0l, std::strtol(env, nullptr, 10)));
     // own-pixel splat buffer [chunk][pixels] of float4; spp processed in chunks
@@ -740,7 +754,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             budget = std::min<size_t>(freeB / 4 + ctx->contrib.bytes, (size_t)32 << 30);
     }
     if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);
-    const size_t perSample = (size_t)L.num_pixels * 4 * 4;   // float4 per sample
+    const size_t perSample = (size_t)L.num_pixels * (L.gather ? 5 : 4) * 4;   // float4 (+ sy) per sample
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));
     const size_t filmFloats = (size_t)L.fw * L.fh * 5;
     if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||
@@ -760,6 +774,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.film_spill = (float *)ctx->film_spill.p;
     L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
     L.contrib = (float *)ctx->contrib.p;
+    L.contrib_y = L.gather ? L.contrib + (size_t)4 * chunk * L.num_pixels : nullptr;
     unsigned long long *cnt = (unsigned long long *)ctx->counters.p;
     L.counters = cnt;
 
@@ -874,7 +889,8 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
                 return fail(ctx, MTSGPU_EINVAL, "SFMT replay: more 32x32 blocks than resident lanes (crop too large)");
             if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
         }
-        if ((e = mtsg_launch_reduce(L, stream)) != hipSuccess) return hip_fail(ctx, e, "reduce launch");
+        if ((e = L.gather ? mtsg_launch_gather(L, stream) : mtsg_launch_reduce(L, stream)) != hipSuccess)
+            return hip_fail(ctx, e, "film reduce launch");
     }
     if ((e = hipEventRecord(ctx->ev1, stream)) != hipSuccess) return hip_fail(ctx, e, "event");
     if ((e = mtsg_launch_finalize(own, L.film_spill, filmFloats, stream)) != hipSuccess) return hip_fail(ctx, e, "finalize launch");
@@ -886,10 +902,17 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         return hip_fail(ctx, e, "sample copy");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel");
     std::memcpy(ctx->last_counters, hc, sizeof hc);
-    // counter 15: which kernel ran -- the megakernel's FEAT | waves << 8 | scene_lds << 12,
-    // or 1 << 16 for the wavefront engine (tests and A/B logs read it)
-    ctx->last_counters[15] = wave ? (1ull << 16)
-                                  : (unsigned long long)(mtsg_path_variant(L) | (int)(L.waves << 8) | (int)(L.scene_lds << 12));
+    // counter 15: which kernel ran -- for the megakernel path_kernel<INSTR, SCENE_LDS, FEAT, WAVES>:
+    // FEAT's low 8 bits | WAVES << 8 | SCENE_LDS << 12 | INSTR << 13 | (FEAT & NOSTRICT) << 14 (the
+    // set kernels' strictNormals-free build); 1 << 16 for the wavefront engine (tests and A/B logs read it)
+    if (wave) {
+        ctx->last_counters[15] = 1ull << 16;
+    } else {
+        const int v = mtsg_path_variant(L);
+        ctx->last_counters[15] = (unsigned long long)((v & 0xff) | (int)(L.waves << 8) | (int)(L.scene_lds << 12) |
+                                                      ((nsamp != 0 || stats_mode) ? 1 << 13 : 0) |
+                                                      ((v & MTSG_FEAT_NOSTRICT) ? 1 << 14 : 0));
+    }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     if (stats) {

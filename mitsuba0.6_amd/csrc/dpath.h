@@ -451,7 +451,7 @@ __device__ __forceinline__ bool scan_tris(const MtsgLaunch &L, f3 o, f3 d, float
 // scan_pair takes it only for rays with |b| >= 2^-60 and mint >= 2^-30, where
 // a quotient small enough to underflow is rejected by mint either way.  Host
 // check: 1.6e9 random and edge-mantissa pairs over that range, bit-equal to
-// IEEE division (tools/r05/fast_div_check.c).
+// IEEE division (tools/gpu_runs/r05/fast_div_check.c).
 __device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
     float q = a * y;
     float r = __builtin_fmaf(-b, q, a);
@@ -886,6 +886,30 @@ __device__ __forceinline__ bool film_splat(const MtsgLaunch &L, int px, int py, 
         }
     }
     return true;
+}
+
+// block->put(samplePos, spec, alpha) (integrator.cpp:184) as the sample's record in
+// the splat buffer (slot = (j - j0) * num_pixels + pix).  Box filter: {L.rgb, w} with
+// the own-pixel weight w (alpha in {0,1} in its sign bit; film_reduce re-forms
+// weight * value[k]) and the rare neighbour splats as atomics.  Gather mode: the
+// sample's value and film position, {L.rgb, sx (alpha in its sign bit: sx >= +0)}
+// and sy (-1: an invalid sample, which ImageBlock::put drops whole); film_gather
+// forms every footprint weight from them with film_splat's arithmetic.
+__device__ __forceinline__ void film_record(const MtsgLaunch &L, size_t slot, int px, int py, float sx, float sy,
+                                            const float *val, bool alpha) {
+    float4 rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (L.gather) {
+        bool valid = true;
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (!isfinite(val[i]) || val[i] < 0) valid = false;   // (alpha and 1 are valid)
+        if (valid) rec4 = make_float4(val[0], val[1], val[2], alpha ? sx : -sx);
+        L.contrib_y[slot] = valid ? sy : -1.0f;
+    } else {
+        float ownW = 0.0f;
+        if (film_splat(L, px, py, sx, sy, val, ownW)) rec4 = make_float4(val[0], val[1], val[2], alpha ? ownW : -ownW);
+    }
+    reinterpret_cast<float4 *>(L.contrib)[slot] = rec4;
 }
 
 // ---------------------------------------------------------------------------
@@ -1569,12 +1593,7 @@ struct PathShader {
         // film_reduce re-forms weight * value[k] -- the same products
         const float alpha = P.alpha ? 1.0f : 0.0f;
         const float val[5] = {P.L.x, P.L.y, P.L.z, alpha, 1.0f};
-        float ownW = 0.0f;
-        const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
-        float4 rec4;
-        if (valid) rec4 = make_float4(P.L.x, P.L.y, P.L.z, P.alpha ? ownW : -ownW);
-        else rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
+        film_record(L, (size_t)(j - L.j0) * L.num_pixels + pix, px, py, sx, sy, val, P.alpha);
         if (INSTR && L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;

@@ -44,7 +44,7 @@
 // persistent megakernel's loop into VGPR pairs, and register pressure then put
 // them in scratch: every powf reloaded three of them from memory.  Without
 // the SLP vectoriser, C2 107 instead of 123 VGPRs, C4 106 instead of 112, C5
-// 96 instead of 112 B of scratch per lane (tools/r05/spills.sh).  Volatile asm is not hoisted; the value is the same.
+// 96 instead of 112 B of scratch per lane (tools/gpu_runs/r05/spills.sh).  Volatile asm is not hoisted; the value is the same.
 template <uint64_t B> __device__ __forceinline__ double glf_kd_bits() {
     uint32_t lo, hi;
     asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "n"((uint32_t)(B & 0xffffffffu)));

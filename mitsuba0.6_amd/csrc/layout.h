@@ -20,6 +20,7 @@
 #define MTSG_SOBOL_SIZE 52
 #define MTSG_FILTER_RES 31
 #define MTSG_BLOCK_SIZE 32
+#define MTSG_GATHER_HMAX 4   // film_gather<H> instantiations: footprints up to 9x9 pixels
 #define MTSG_SCAN_MAX 64      // primitives up to which SCENE_LDS scenes scan instead of traversing
 
 // node child reference: >= 0 inner node index; < 0 leaf: ~ref = first << 4 | count
@@ -318,9 +319,15 @@ struct MtsgLaunch {
     uint32_t replay, units;
     const uint32_t *order, *unit_start;
     uint32_t *sfmt;
-    float *contrib;                   // [5][chunk_spp][num_pixels] own-pixel splats
-    float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction)
-    float *film_spill;                // fw*fh*5: splats into other pixels (atomics)
+    float *contrib;                   // [chunk_spp][num_pixels] float4 per sample: box filter {L.rgb, own-pixel
+                                      // weight, alpha in its sign}; gather mode {L.rgb, sx, alpha in its sign}
+    float *contrib_y;                 // gather mode: [chunk_spp][num_pixels] sy (negative: invalid sample)
+    float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction), or the gathered film
+    float *film_spill;                // fw*fh*5: splats into other pixels (atomics; box filter only)
+    // gather mode (filters whose footprint covers neighbours, e.g. gaussian): the kernels store
+    // each sample's value and position; film_gather<H> forms every pixel's sum in a fixed order
+    uint32_t gather;                  // 1: gather mode
+    uint32_t gather_h;                // largest footprint offset from a sample's pixel (<= MTSG_GATHER_HMAX)
     float *samples;                   // optional per-sample records
     unsigned long long *counters;     // [0] samples [1] rays [2] shadow [3] pathlen [4] nodes [5] tests
                                       // [6] dim errors [7] hits [9] nee [10] sobol words

@@ -405,10 +405,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         }
         // block->put(samplePos, spec, alpha) (integrator.cpp:184), as path_kernel
         const float val[5] = {Li.x, Li.y, Li.z, alpha, 1.0f};
-        float ownW = 0.0f;
-        const bool valid = film_splat(L, px, py, sx, sy, val, ownW);
-        float4 rec4 = valid ? make_float4(Li.x, Li.y, Li.z, alpha == 0.0f ? -ownW : ownW) : make_float4(0, 0, 0, 0);
-        reinterpret_cast<float4 *>(L.contrib)[(size_t)(j - L.j0) * L.num_pixels + pix] = rec4;
+        film_record(L, (size_t)(j - L.j0) * L.num_pixels + pix, px, py, sx, sy, val, alpha != 0.0f);
         if (L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
@@ -503,6 +500,151 @@ __global__ void film_reduce(MtsgLaunch L) {
     }
 #pragma unroll
     for (int k = 0; k < 5; ++k) dst[k] = acc[k];
+}
+
+// ---------------------------------------------------------------------------
+// gather mode (gaussian and other filters whose footprint covers neighbours):
+// every film pixel forms its own sum from the sample records of the pixels
+// around it, in one fixed order, so the film is deterministic and equal to the
+// oracle's (oracle/mts_oracle.c film_gather) bit for bit: for each sample
+// index j (ascending), the source pixels q of the (2H+1)^2 neighbourhood in
+// row-major order, each adding weight * value[k] with weight =
+// weightsX[x] * weightsY[y] as ImageBlock::put forms them (imageblock.h:
+// 124-204; footprint and discretised filter exactly as film_splat, so the
+// 32x32 block bitmap's clip and the film edge are kept).  The reference's own
+// order is its block schedule's (Film::put merges blocks as they finish,
+// renderproc.cpp:142-149); this one replaces the atomic neighbour splats, which
+// had no order at all.
+//
+// One workgroup: a 16x16 tile of film pixels.  Per sample index the tile's
+// (16+2H)^2 source records are staged in LDS together with their per-axis
+// weights towards every offset -H..H (formed once per record, not once per
+// neighbour), then each thread adds its (2H+1)^2 neighbours from LDS.
+// ---------------------------------------------------------------------------
+// the compact pixel index p (work items' pixel, pixel_of's inverse) of image
+// pixel (qx, qy), or -1 when this launch does not render it (outside the
+// window, or another shard's rows / tiles)
+__device__ __forceinline__ long long pix_index(const MtsgLaunch &L, int qx, int qy) {
+    const int lx = qx - (int)L.x0, ly = qy - (int)L.y0;
+    if (lx < 0 || ly < 0 || lx >= (int)L.width || ly >= (int)L.height) return -1;
+    uint32_t tile, in;
+    if (L.tile_shard) {
+        const uint32_t t = (uint32_t)(ly >> 3) * L.tiles_x + (uint32_t)(lx >> 3);
+        if (t % L.row_stride != L.row_phase) return -1;
+        tile = t / L.row_stride;
+        in = (uint32_t)(ly & 7) * 8u + (uint32_t)(lx & 7);
+    } else {
+        const uint32_t blkAbs = (uint32_t)ly / L.row_block;
+        if (blkAbs % L.row_stride != L.row_phase) return -1;
+        const uint32_t r = (blkAbs / L.row_stride) * L.row_block + (uint32_t)ly % L.row_block;
+        tile = (r >> 3) * L.tiles_x + (uint32_t)(lx >> 3);
+        in = (r & 7u) * 8u + (uint32_t)(lx & 7);
+    }
+    return (long long)tile * 64 + in;
+}
+
+#define GATHER_T 16
+__host__ __device__ constexpr size_t gather_lds_floats(int H) {
+    return (size_t)(GATHER_T + 2 * H) * (GATHER_T + 2 * H) * (4 + 2 * (2 * H + 1)) + 32;
+}
+
+template <int H>
+__global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy0, int gx1, int gy1) {
+    constexpr int SW = GATHER_T + 2 * H, S = SW * SW, NW = 2 * H + 1, SLOTS = (S + 255) / 256;
+    extern __shared__ float glds[];
+    float4 *val = reinterpret_cast<float4 *>(glds);   // [S] {L.rgb, alpha}
+    float *wxs = glds + 4 * S;                          // [NW][S] weight towards film x = q's + (o - H)
+    float *wys = wxs + NW * S;                          // [NW][S]
+    float *fv = wys + NW * S;                           // the discretised filter (32 values)
+    const MtsgFilter &F = L.filter;
+    const int b = F.border, bw = MTSG_BLOCK_SIZE + 2 * b;
+    const int tx = threadIdx.x & (GATHER_T - 1), ty = threadIdx.x / GATHER_T;
+    const int ox = gx0 + blockIdx.x * GATHER_T, oy = gy0 + blockIdx.y * GATHER_T;
+    const int gx = ox + tx, gy = oy + ty;
+    const bool live = gx < gx1 && gy < gy1;
+    // source s = image pixel (sx0 + s % SW, sy0 + s / SW): film position q + b = g + d, d in [-H, H]
+    const int sx0 = ox - b - H, sy0 = oy - b - H;
+    for (int i = threadIdx.x; i <= MTSG_FILTER_RES; i += 256) fv[i] = F.values[i];
+    long long pi[SLOTS];
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) {
+        const int s = threadIdx.x + 256 * k;
+        pi[k] = s < S ? pix_index(L, sx0 + s % SW, sy0 + s / SW) : -1;
+    }
+    float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    float *dst = L.film_own + ((size_t)gy * L.fw + gx) * 5;
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) acc[k] = dst[k];   // the previous chunks' running sums
+    }
+    const float4 *rec = reinterpret_cast<const float4 *>(L.contrib);
+    for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
+        __syncthreads();   // the previous sample's neighbours are summed
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) {
+            const int s = threadIdx.x + 256 * k;
+            if (s >= S) break;
+            float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float wx[NW], wy[NW];
+#pragma unroll
+            for (int o = 0; o < NW; ++o) wx[o] = wy[o] = 0.0f;
+            if (pi[k] >= 0) {
+                const size_t slot = (size_t)jj * L.num_pixels + (size_t)pi[k];
+                const float4 r = rec[slot];
+                const float sy = L.contrib_y[slot];
+                if (!signbit(sy)) {
+                    const int qx = sx0 + s % SW, qy = sy0 + s / SW;
+                    const float sx = fabsf(r.w);
+                    v = make_float4(r.x, r.y, r.z, signbit(r.w) ? 0.0f : 1.0f);
+                    // film_splat's footprint in the block bitmap of q's 32x32 block
+                    const int bx = (qx / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE, by = (qy / MTSG_BLOCK_SIZE) * MTSG_BLOCK_SIZE;
+                    const float posx = sx - 0.5f - (float)(bx - b), posy = sy - 0.5f - (float)(by - b);
+                    const int minx = max((int)ceilf(posx - F.radius), 0), miny = max((int)ceilf(posy - F.radius), 0);
+                    const int maxx = min((int)floorf(posx + F.radius), bw - 1), maxy = min((int)floorf(posy + F.radius), bw - 1);
+#pragma unroll
+                    for (int o = 0; o < NW; ++o) {
+                        const int x = qx + b + (o - H) - bx, y = qy + b + (o - H) - by;   // block-local
+                        if (x >= minx && x <= maxx && qx + b + (o - H) < L.fw) {
+                            int i = (int)fabsf(((float)x - posx) * F.scale);
+                            wx[o] = fv[min(i, MTSG_FILTER_RES)];
+                        }
+                        if (y >= miny && y <= maxy && qy + b + (o - H) < L.fh) {
+                            int i = (int)fabsf(((float)y - posy) * F.scale);
+                            wy[o] = fv[min(i, MTSG_FILTER_RES)];
+                        }
+                    }
+                }
+            }
+            val[s] = v;
+#pragma unroll
+            for (int o = 0; o < NW; ++o) {
+                wxs[o * S + s] = wx[o];
+                wys[o * S + s] = wy[o];
+            }
+        }
+        __syncthreads();
+        if (live) {
+            // neighbour d = (dx, dy): source q at film position g + d; g sits at offset -d from it
+#pragma unroll
+            for (int dy = -H; dy <= H; ++dy) {
+#pragma unroll
+                for (int dx = -H; dx <= H; ++dx) {
+                    const int s = (ty + H + dy) * SW + (tx + H + dx);
+                    const float w = wxs[(H - dx) * S + s] * wys[(H - dy) * S + s];
+                    const float4 v = val[s];
+                    acc[0] += w * v.x;
+                    acc[1] += w * v.y;
+                    acc[2] += w * v.z;
+                    acc[3] += w * v.w;
+                    acc[4] += w * 1.0f;
+                }
+            }
+        }
+    }
+    if (live) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dst[k] = acc[k];
+    }
 }
 
 __global__ void film_finalize(float *__restrict__ own, const float *__restrict__ spill, size_t n) {
@@ -607,6 +749,25 @@ hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// gather mode: the film pixels the launch's samples can reach, [x0 + b - H, x0 + w + b + H)
+// x [y0 + b - H, y0 + h + b + H) clipped to the film, in 16x16 tiles
+hipError_t mtsg_launch_gather(const MtsgLaunch &L, hipStream_t stream) {
+    const int H = (int)L.gather_h, b = L.filter.border;
+    const int gx0 = std::max(0, (int)L.x0 + b - H), gy0 = std::max(0, (int)L.y0 + b - H);
+    const int gx1 = std::min(L.fw, (int)(L.x0 + L.width) + b + H), gy1 = std::min(L.fh, (int)(L.y0 + L.height) + b + H);
+    if (gx1 <= gx0 || gy1 <= gy0) return hipSuccess;
+    const dim3 grid((gx1 - gx0 + GATHER_T - 1) / GATHER_T, (gy1 - gy0 + GATHER_T - 1) / GATHER_T);
+    const size_t lds = gather_lds_floats(H) * 4;
+    switch (H) {
+        case 1: hipLaunchKernelGGL(film_gather<1>, grid, dim3(256), lds, stream, L, gx0, gy0, gx1, gy1); break;
+        case 2: hipLaunchKernelGGL(film_gather<2>, grid, dim3(256), lds, stream, L, gx0, gy0, gx1, gy1); break;
+        case 3: hipLaunchKernelGGL(film_gather<3>, grid, dim3(256), lds, stream, L, gx0, gy0, gx1, gy1); break;
+        case 4: hipLaunchKernelGGL(film_gather<4>, grid, dim3(256), lds, stream, L, gx0, gy0, gx1, gy1); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream) {
     const int threads = 256;
     const int blocks = (int)((n + threads - 1) / threads);
@@ -654,7 +815,8 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
 // (reported through debug counter 15 so the tests can see which one ran)
 int mtsg_path_variant(const MtsgLaunch &L) {
     const int bits = spec_bits(L), f = mtsg_path_features(L);
-    if (bits) return f | ((bits & 1) ? MTSG_FEAT_GGX : 0) | ((bits & 2) ? MTSG_FEAT_NORD : 0) | ((bits & 4) ? MTSG_FEAT_NORC : 0);
+    if (bits) return f | MTSG_FEAT_NOSTRICT | ((bits & 1) ? MTSG_FEAT_GGX : 0) | ((bits & 2) ? MTSG_FEAT_NORD : 0) |
+                     ((bits & 4) ? MTSG_FEAT_NORC : 0);
     return (f == 0 && L.all_diffuse) ? (int)MTSG_FEAT_DIFF : f;
 }
 

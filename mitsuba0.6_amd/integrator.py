@@ -186,6 +186,20 @@ class Context:
         self._check(self.L.mtsgpu_debug_counters(self.h, out))
         return list(out)
 
+    def kernel_variant(self):
+        """The megakernel instantiation the last render launched, decoded from debug
+        counter 15 (capi.cpp): {'instr', 'scene_lds', 'feat', 'waves', 'name'}, where
+        name is the template as rocprofv3 reports it, e.g.
+        'path_kernel<false, false, 336, 4>'; None after a wavefront-engine render."""
+        c = self.debug_counters()[15]
+        if c & (1 << 16):
+            return None
+        feat = (c & 0xff) | (256 if c & (1 << 14) else 0)
+        instr, lds, waves = bool(c & (1 << 13)), bool(c & (1 << 12)), (c >> 8) & 0xf
+        b = lambda v: 'true' if v else 'false'
+        return {'instr': instr, 'scene_lds': lds, 'feat': feat, 'waves': waves,
+                'name': 'path_kernel<%s, %s, %d, %d>' % (b(instr), b(lds), feat, waves)}
+
     def debug_sfmt(self, seed, n, clone=0):
         """n nextULong draws of the device's SFMT19937 from Random(seed) (or its clone-th clone)."""
         out = np.zeros(n, np.uint64)

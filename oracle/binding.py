@@ -73,6 +73,7 @@ def lib(variant='strict'):
                                            C.POINTER(C.c_float), C.c_uint32, C.c_int, C.POINTER(C.c_float)]
         L.oracle_intersect.argtypes = [C.POINTER(abi.SceneDesc), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(C.c_float)]
+        L.oracle_filter.argtypes = [C.c_int, C.c_float, C.POINTER(C.c_float)]
         L.oracle_sfmt_u64.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.c_int, C.c_int]
         L.oracle_render_order.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                           C.POINTER(C.c_int)]
@@ -171,6 +172,20 @@ def sfmt_u64(seed, n, clone=0):
     out = np.zeros(n, np.uint64)
     lib().oracle_sfmt_u64(C.c_uint64(seed), out.ctypes.data_as(C.POINTER(C.c_uint64)), n, clone)
     return out
+
+
+def filter_table(rfilter, param):
+    """The oracle's configured filter: (radius, scale, border, values (FILTER_RES + 1,) float32)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    from pkgimport import mitsuba_amd
+    abi = mitsuba_amd().abi
+    out = np.zeros(64, np.float32)
+    t = {'box': abi.RFILTER_BOX, 'gaussian': abi.RFILTER_GAUSSIAN}[rfilter] if isinstance(rfilter, str) else rfilter
+    rc = lib().oracle_filter(t, param, out.ctypes.data_as(C.POINTER(C.c_float)))
+    if rc:
+        raise ValueError('oracle_filter failed (%d)' % rc)
+    return float(out[0]), np.float32(out[1]), int(out[2]), out[3:3 + 32].copy()
 
 
 def render_order(width, height, block=32):

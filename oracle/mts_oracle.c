@@ -57,6 +57,10 @@ static int g_cr = 0; /* libm mode */
 /* oracle_set_kdtree: traverse this kd-tree (KDNode words, primitive lists) in
    Scene::rayIntersect / isOccluded instead of the BVH (NULL: the BVH) */
 static const uint32_t *g_kd_nodes = NULL, *g_kd_indices = NULL;
+/* diagnostics (tools/diag_bench_kernel.py): ORACLE_TRACE="px,py,j" prints every ray query
+   of that one sample with its exact bits and answer to stderr (render threads = 1) */
+static int g_trace_px = -1, g_trace_py = -1, g_trace_j = -1;
+static _Thread_local int g_trace_on = 0;
 
 /* std::max / std::min semantics (NaN handling matters) */
 static inline float smax(float a, float b) { return (a < b) ? b : a; }
@@ -2667,6 +2671,13 @@ static void compute_uv_tangents(Mesh *m) { /* trimesh.cpp:683-739 */
  * and the product break towards the larger primitive index) -------------- */
 typedef struct { float c[3]; float bmin[3], bmax[3]; } PrimBox;
 
+/* absolute part of the node boxes' conservative inflation: 1e-7 of the scene diagonal (as
+   scene_build.cpp's Builder::absEps).  A box of zero extent at coordinate 0 -- a floor at
+   y = 0 -- gets no relative inflation at all, and its slab t can round one ulp beyond the
+   TriAccel t of a triangle it holds: without this the traversal could cull an exact-t tie
+   partner (C4's coplanar hall and floor meshes), and the closest hit would depend on the
+   traversal order instead of the (t, larger primitive) rule */
+static float g_bvh_abs_eps = 1e-30f;
 static uint32_t bvh_build(Scene *S, PrimBox *pb, uint32_t *order, uint32_t first, uint32_t count, uint32_t *nnodes) {
     uint32_t id = (*nnodes)++;
     BNode *n = &S->nodes[id];
@@ -2682,7 +2693,7 @@ static uint32_t bvh_build(Scene *S, PrimBox *pb, uint32_t *order, uint32_t first
         }
     }
     for (int a = 0; a < 3; ++a) { /* conservative inflation: never loses a hit */
-        float e = (bmax[a] - bmin[a]) * 1e-4f + 1e-6f * (fabsf(bmin[a]) + fabsf(bmax[a])) + 1e-30f;
+        float e = (bmax[a] - bmin[a]) * 1e-4f + 1e-6f * (fabsf(bmin[a]) + fabsf(bmax[a])) + g_bvh_abs_eps;
         n->bmin[a] = bmin[a] - e; n->bmax[a] = bmax[a] + e;
     }
     if (count <= 4) { n->first = first; n->count = count; n->left = n->right = 0; return id; }
@@ -2886,6 +2897,9 @@ static int scene_configure(const mtsgpu_scene_desc *D, Scene *S) {
     for (uint32_t i = 0; i < prims; ++i) S->order[i] = i;
     S->nodes = (BNode *)malloc(sizeof(BNode) * (2 * prims + 1));
     uint32_t nn = 0;
+    float diag = 0;
+    for (int a = 0; a < 3; ++a) diag += (S->aabbMax[a] - S->aabbMin[a]) * (S->aabbMax[a] - S->aabbMin[a]);
+    g_bvh_abs_eps = 1e-7f * sqrtf(diag) + 1e-30f;   /* read by bvh_build only (scene setup is single-threaded) */
     bvh_build(S, pb, S->order, 0, prims, &nn);
     S->nnodes = nn;
     free(pb);
@@ -3013,8 +3027,13 @@ static void scene_intersect(const Scene *S, const Ray *ray, Its *its, Counters *
     if (ray->maxt < maxt) maxt = ray->maxt;
     if (!(maxt > mint)) return;
     uint32_t prim; float u, v, t;
-    if (g_kd_nodes ? !kd_havran(S, g_kd_nodes, g_kd_indices, ray, mint, maxt, 0, &prim, &u, &v, &t)
-                   : !trace_closest(S, ray, mint, maxt, &prim, &u, &v, &t, C)) return;
+    const int hit = g_kd_nodes ? kd_havran(S, g_kd_nodes, g_kd_indices, ray, mint, maxt, 0, &prim, &u, &v, &t)
+                               : trace_closest(S, ray, mint, maxt, &prim, &u, &v, &t, C);
+    if (g_trace_on)
+        fprintf(stderr, "ORACLE_TRACE closest o %a %a %a d %a %a %a mint %a maxt %a (ray %a %a) -> %s prim %u t %a u %a v %a\n",
+                ray->o.x, ray->o.y, ray->o.z, ray->d.x, ray->d.y, ray->d.z, mint, maxt, ray->mint, ray->maxt,
+                hit ? "hit" : "miss", hit ? prim : 0u, hit ? t : 0.0f, hit ? u : 0.0f, hit ? v : 0.0f);
+    if (!hit) return;
     const Mesh *m = &S->meshes[S->taMesh[prim]];
     uint32_t tri = S->taTri[prim];
     its->valid = 1; its->t = t; its->mesh = (int)S->taMesh[prim]; its->tri = tri;
@@ -3068,7 +3087,11 @@ static int scene_occluded(const Scene *S, const Ray *ray, Counters *C) {
         uint32_t prim; float u, v, t;
         return kd_havran(S, g_kd_nodes, g_kd_indices, ray, mint, maxt, 1, &prim, &u, &v, &t);
     }
-    return trace_any(S, ray, mint, maxt, C);
+    const int occ = trace_any(S, ray, mint, maxt, C);
+    if (g_trace_on)
+        fprintf(stderr, "ORACLE_TRACE shadow o %a %a %a d %a %a %a mint %a maxt %a (ray %a %a) -> %d\n", ray->o.x, ray->o.y,
+                ray->o.z, ray->d.x, ray->d.y, ray->d.z, mint, maxt, ray->mint, ray->maxt, occ);
+    return occ;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -3586,6 +3609,78 @@ static int film_put(const Filter *f, int W, int H, int px, int py, float sx, flo
 }
 
 /* ------------------------------------------------------------------------ */
+/* gather mode (filters whose footprint covers neighbours: gaussian).  The    */
+/* reference sums a pixel's splats in its block schedule's order (ImageBlock  */
+/* ::put per block, Film::put as blocks finish, renderproc.cpp:142-149); the  */
+/* GPU's film_gather (path_kernel.hip) and this restatement use one fixed     */
+/* order instead: per film pixel, for each sample index j ascending, the      */
+/* source pixels of the (2H+1)^2 neighbourhood in row-major order, each       */
+/* adding weight * value[k] with film_put's footprint and weights.            */
+/* ------------------------------------------------------------------------ */
+#define GATHER_HMAX 4 /* the GPU's MTSG_GATHER_HMAX */
+typedef struct { float v[4]; float sx, sy; int valid; } GatherRec;
+
+static int gather_h(int rfilter, const Filter *f) {
+    if (rfilter == MTSGPU_RFILTER_BOX) return 0;
+    int H = (int)floorf(f->radius + 0.5f);
+    if (H < f->border) H = f->border;
+    return (H >= 1 && H <= GATHER_HMAX) ? H : 0;
+}
+
+/* the render loop's pixel predicate: window, row blocks or 8x8 tiles of this shard */
+static int pixel_rendered(const mtsgpu_render_params *P, int qx, int qy) {
+    const int lx = qx - (int)P->x0, ly = qy - (int)P->y0;
+    if (lx < 0 || ly < 0 || lx >= (int)P->width || ly >= (int)P->height) return 0;
+    const uint32_t rb = P->row_block ? P->row_block : 1, rs = P->row_stride ? P->row_stride : 1;
+    if (P->flags & MTSGPU_FLAG_TILE_SHARD) {
+        const uint32_t t = (uint32_t)(ly / 8) * ((P->width + 7) / 8) + (uint32_t)(lx / 8);
+        return t % rs == P->row_phase;
+    }
+    return ((uint32_t)ly / rb) % rs == P->row_phase;
+}
+
+static void film_gather(const Filter *f, const mtsgpu_render_params *P, int fw, int fh, int H, const GatherRec *recs,
+                        float *film) {
+    const int b = f->border, bw = BLOCK_SIZE + 2 * b, bh = BLOCK_SIZE + 2 * b;
+    const int gx0 = (int)P->x0 + b - H < 0 ? 0 : (int)P->x0 + b - H;
+    const int gy0 = (int)P->y0 + b - H < 0 ? 0 : (int)P->y0 + b - H;
+    const int gx1 = (int)(P->x0 + P->width) + b + H > fw ? fw : (int)(P->x0 + P->width) + b + H;
+    const int gy1 = (int)(P->y0 + P->height) + b + H > fh ? fh : (int)(P->y0 + P->height) + b + H;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int gy = gy0; gy < gy1; ++gy) {
+        for (int gx = gx0; gx < gx1; ++gx) {
+            float *dst = film + ((size_t)gy * fw + gx) * 5;
+            for (uint32_t j = 0; j < P->spp; ++j) {
+                for (int dy = -H; dy <= H; ++dy) {
+                    for (int dx = -H; dx <= H; ++dx) {
+                        const int qx = gx - b + dx, qy = gy - b + dy;
+                        if (!pixel_rendered(P, qx, qy)) continue;
+                        const GatherRec *r = recs + (((size_t)(qy - (int)P->y0) * P->width + (size_t)(qx - (int)P->x0)) * P->spp + j);
+                        if (!r->valid) continue;
+                        /* film_put's footprint in the block bitmap of q's block */
+                        const int bx = (qx / BLOCK_SIZE) * BLOCK_SIZE, by = (qy / BLOCK_SIZE) * BLOCK_SIZE;
+                        const float posx = r->sx - 0.5f - (float)(bx - b), posy = r->sy - 0.5f - (float)(by - b);
+                        int minx = (int)ceilf(posx - f->radius), miny = (int)ceilf(posy - f->radius);
+                        int maxx = (int)floorf(posx + f->radius), maxy = (int)floorf(posy + f->radius);
+                        if (minx < 0) minx = 0;
+                        if (miny < 0) miny = 0;
+                        if (maxx > bw - 1) maxx = bw - 1;
+                        if (maxy > bh - 1) maxy = bh - 1;
+                        const int x = gx - bx, y = gy - by;
+                        if (x < minx || x > maxx || y < miny || y > maxy) continue;
+                        const float weight = filter_eval_disc(f, x - posx) * filter_eval_disc(f, y - posy);
+                        const float val5[5] = {r->v[0], r->v[1], r->v[2], r->v[3], 1.0f};
+                        for (int k = 0; k < 5; ++k) dst[k] += weight * val5[k];
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
 /* SamplingIntegrator::renderBlock (librender/integrator.cpp:140-188)        */
 /* ------------------------------------------------------------------------ */
 typedef struct {
@@ -3597,6 +3692,7 @@ typedef struct {
     const Filter *F;
     int W, H, fw, fh;
     float *film, *spill, *samples;
+    GatherRec *recs; /* gather mode: each sample's value and position instead of a splat */
 } RenderCtx;
 
 /* one pixel's sampleCount samples: sampler->generate(offset), then per sample
@@ -3626,11 +3722,22 @@ static void render_pixel(const RenderCtx *R, long pi, int px, int py, Sfmt *rng,
         ray.rxD = vadd(ray.d, vmul(vsub(ray.rxD, ray.d), R->diffScale));
         ray.ryD = vadd(ray.d, vmul(vsub(ray.ryD, ray.d), R->diffScale));
         float alpha; int depth = 1;
+        g_trace_on = px == g_trace_px && py == g_trace_py && (int)j == g_trace_j;
+        if (g_trace_on) fprintf(stderr, "ORACLE_TRACE sample px %d py %d j %u\n", px, py, j);
         V3 L = R->direct ? Li_direct(R->S, R->PP, &DP, ray, &smp, &alpha, &C) : Li(R->S, R->PP, ray, &smp, &alpha, &depth, &C);
         if (smp.err) *err = 1;
         *pathLen += (uint64_t)depth; ++*nsamples;
         float val5[5] = {L.x, L.y, L.z, alpha, 1.0f};
-        film_put(R->F, R->W, R->H, px, py, sx, sy, val5, R->film, R->spill, R->fw, R->fh);
+        if (R->recs) {
+            GatherRec *g = R->recs + ((size_t)pi * P->spp + j);
+            g->valid = 1;
+            for (int i = 0; i < 5; ++i)
+                if (!isfinite(val5[i]) || val5[i] < 0) g->valid = 0;
+            for (int i = 0; i < 4; ++i) g->v[i] = val5[i];
+            g->sx = sx; g->sy = sy;
+        } else {
+            film_put(R->F, R->W, R->H, px, py, sx, sy, val5, R->film, R->spill, R->fw, R->fh);
+        }
         if (R->samples) {
             float *rec = R->samples + ((size_t)pi * P->spp + j) * MTSGPU_SAMPLE_RECORD_FLOATS;
             rec[0] = L.x; rec[1] = L.y; rec[2] = L.z; rec[3] = alpha;
@@ -3671,6 +3778,10 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     if (replay && (P->row_stride > 1 || direct))   /* path / volpath, as the GPU */
         return MTSGPU_EINVAL;
     g_cr = libm_mode;
+    {
+        const char *tr = getenv("ORACLE_TRACE");
+        if (!tr || sscanf(tr, "%d,%d,%d", &g_trace_px, &g_trace_py, &g_trace_j) != 3) g_trace_px = g_trace_py = g_trace_j = -1;
+    }
     Scene S;
     int rc = scene_configure(scene, &S);
     if (rc) { scene_free(&S); return rc; }
@@ -3688,7 +3799,10 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     Counters tot = {0, 0, 0, 0};
     uint64_t pathLen = 0, nsamples = 0;
     int err = 0;
-    RenderCtx R = {&S, &PP, P, direct, 1.0f / sqrtf((float)P->spp), &F, W, H, fw, fh, film, spill, samples};
+    const int gh = gather_h(P->rfilter, &F);
+    GatherRec *recs = gh ? (GatherRec *)calloc((size_t)P->width * P->height * P->spp, sizeof(GatherRec)) : NULL;
+    if (gh && !recs) { free(spill); scene_free(&S); return MTSGPU_ENOMEM; }
+    RenderCtx R = {&S, &PP, P, direct, 1.0f / sqrtf((float)P->spp), &F, W, H, fw, fh, film, spill, samples, recs};
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #endif
@@ -3737,6 +3851,10 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
             render_pixel(&R, pi, px, py, NULL, &tot, &pathLen, &nsamples, &err);
         }
     }
+    if (recs) {
+        film_gather(&F, P, fw, fh, gh, recs, film);
+        free(recs);
+    }
     for (size_t i = 0; i < filmFloats; ++i) film[i] += spill[i];
     free(spill);
     if (stats) {
@@ -3751,6 +3869,17 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
 /* ------------------------------------------------------------------------ */
 /* unit-level probes                                                          */
 /* ------------------------------------------------------------------------ */
+/* the configured reconstruction filter (filter_configure): out = {radius, scale,
+   border, values[0..FILTER_RES]} (tests restate the film's gather order with it) */
+int oracle_filter(int type, float param, float *out) {
+    Filter f;
+    int rc = filter_configure(type, param, &f);
+    if (rc) return rc;
+    out[0] = f.radius; out[1] = f.scale; out[2] = (float)f.border;
+    for (int i = 0; i <= FILTER_RES; ++i) out[3 + i] = f.values[i];
+    return MTSGPU_OK;
+}
+
 int oracle_triaccel_load(const float *A, const float *B, const float *C, float *out10) {
     TriAccel ta;
     int r = triaccel_load(&ta, v3(A[0], A[1], A[2]), v3(B[0], B[1], B[2]), v3(C[0], C[1], C[2]));

@@ -1,7 +1,7 @@
 """div_by_rcp (csrc/dpath.h), the axis-aligned scan groups' quotient: a * RN(1/b)
 with two FMA residual corrections must equal IEEE a / b bit for bit over the range
 scan_pair admits it for (|b| >= 2^-60, quotients >= 2^-31 in magnitude).  Runs
-tools/r05/fast_div_check.c (the host restatement, x86 FMA) on a few million random
+tools/gpu_runs/r05/fast_div_check.c (the host restatement, x86 FMA) on a few million random
 and edge-mantissa pairs; the round-5 run covered 1.6e9."""
 import os
 import subprocess

@@ -42,7 +42,8 @@ def _check(gpu_ctx, oracle, sc, it, what, window=None):
     _records_equal(smp_m, smp_o, what + ' megakernel vs oracle')
     for k in ('samples', 'rays', 'shadow_rays', 'path_length_sum'):
         assert st_w[k] == st_o[k] == st_m[k], (what, k, st_w[k], st_m[k], st_o[k])
-    np.testing.assert_allclose(film_w, film_o, rtol=2e-6, atol=1e-6)
+    # box: ordered own-pixel sums (+ rare neighbour splats); gaussian: the fixed gather order
+    assert np.array_equal(_bits(film_w), _bits(film_o)), (what, np.argwhere(_bits(film_w) != _bits(film_o))[:4])
     return film_w, film_m
 
 

@@ -4,7 +4,7 @@
  * magnitude; smaller ones fall below every admitted mint).  Random signs,
  * exponents and mantissas, 3 in 8 of them edge mantissas (near all-ones, near
  * zero, near the half).
- *   gcc -O2 -ffp-contract=off -mfma -o /tmp/fdc tools/r05/fast_div_check.c -lm && /tmp/fdc 400000000
+ *   gcc -O2 -ffp-contract=off -mfma -o /tmp/fdc tools/gpu_runs/r05/fast_div_check.c -lm && /tmp/fdc 400000000
  * r05: 1.6e9 pairs over three runs (numerators 2^-40..2^20 and 2^-40..2^60), 0 mismatches. */
 #include <math.h>
 #include <stdio.h>

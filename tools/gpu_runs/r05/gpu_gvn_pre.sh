@@ -1,6 +1,6 @@
 #!/bin/bash
 # r05: the GVN-PRE defect on today's source: the shipped build (PRE off) and the PRE-on build of
-# path_kernel.hip (tools/r05/gvn_pre_repro.sh) against the oracle on the direct-integrator scenes
+# path_kernel.hip (tools/gpu_runs/r05/gvn_pre_repro.sh) against the oracle on the direct-integrator scenes
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1

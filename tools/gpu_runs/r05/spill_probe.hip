@@ -1,4 +1,4 @@
-// Compile-only probe (tools/r05/spills.sh): the four benchmark megakernels
+// Compile-only probe (tools/gpu_runs/r05/spills.sh): the four benchmark megakernels
 // (C2 DIFF+LDS, C3 set 49, C4 set 80, C5 set 115), for register/spill counts
 // without building every variant.
 #include "../../mitsuba0.6_amd/csrc/dmega.h"
