@@ -155,24 +155,44 @@ def measured_profile(kind, cfg):
     return t
 
 
+def valu_calibration():
+    """The newest committed VALU calibration (tools/valu_calib.hip -> tools/calib_summary.py
+    -> profiles/<round>_valu_calib.json): the SIMD-cycles per wave64 VALU instruction a
+    pure-VALU kernel sustains at saturation, measured with the same SQ counters as the
+    path kernel's pass; None when none is committed."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_valu_calib.json')))
+    if not files:
+        return None
+    c = json.load(open(files[-1]))
+    c['source'] = os.path.basename(files[-1])
+    return c
+
+
 def roofline_line(bps, launch_samples, kernel_s, cfg, lib_hash=None):
     """The dominant kernel's roofline, from the live kernel time of this run and
     per-sample work measured once per build by rocprofv3 (profiles/<round>_*):
       hbm   -- measured HBM bytes per sample (separate FETCH_SIZE / WRITE_SIZE
                passes, FETCH doubled per MI355X_MICROARCH.md) x samples / time,
                against the 8 TB/s HBM3E peak;
-      valu  -- VALU-busy SIMD cycles per sample (4 x SQ_ACTIVE_INST_VALU, which
-               counts quad-cycles) x samples / time, against the SIMD cycles
-               available (1024 SIMDs x the pass's measured shader clock, clock =
-               GRBM_GUI_ACTIVE / 8 XCDs / kernel time): the fraction of cycles
-               the vector ALUs are busy.  The issue-based rate (SQ_INSTS_VALU x
-               64 lanes against one wave64 VALU instruction per SIMD per 2
-               cycles) is kept beside it: the gap is multi-cycle instructions
-               (f64, transcendentals, correctly rounded division).
-    `bound` is the one of the two with the larger fraction; the other is kept,
-    and so is the SURVEY.md 8(d) no-reuse byte model (`hbm_model`)."""
+      valu  -- wave64 VALU instructions per sample (SQ_INSTS_VALU of the SQ pass)
+               x samples / time, against the calibrated issue peak: 1024 SIMDs x
+               the pass's shader clock / the SIMD-cycles per VALU instruction that
+               a pure-VALU kernel sustains at saturation (profiles/r*_valu_calib
+               .json: 4.19 at 8 waves/SIMD, for v_fma_f32 and for the packed v_pk_*
+               alike).  Beside it: `busy` (4 x SQ_ACTIVE_INST_VALU quad-cycles per
+               SIMD-cycle; the calibration kernel saturates at 0.955) and
+               `spec_lane_issue` (f32 lane-ops against the 157 TF spec rate of 32
+               lane-FMAs per SIMD-cycle, which only packed instructions reach: the
+               calibration measures 15.3 unpacked vs 30.5 packed lane-ops per cycle).
+    `bound` is the resource with the larger calibrated fraction; the other is kept,
+    as is the SURVEY.md 8(d) no-reuse byte model (`hbm_model`), and, when committed,
+    the stall attribution (profiles/r*_stalls_<cfg>.json: per-kind instruction
+    counts and latencies)."""
     traffic = measured_profile('traffic', cfg)
     valu = measured_profile('valu', cfg)
+    stalls = measured_profile('stalls', cfg)
+    calib = valu_calibration()
     # a per-sample profile only describes the build it was taken on (tools/prof_round.sh
     # stamps each with the library's sha256): another build's profile gives no `frac`
     stale = []
@@ -193,16 +213,24 @@ def roofline_line(bps, launch_samples, kernel_s, cfg, lib_hash=None):
                'bytes_per_sample': round(traffic['hbm_bytes_per_sample'], 1),
                'write_bytes_per_sample': traffic.get('write_bytes_per_sample'), 'source': traffic['source']}
     vl = None
-    if valu and valu.get('valu_busy_cycles_per_sample') and valu.get('clock_hz'):
-        a = valu['valu_busy_cycles_per_sample'] * launch_samples / kernel_s / 1e9
-        pk = 1024 * valu['clock_hz'] / 1e9
+    if valu and valu.get('valu_insts_per_sample') and valu.get('clock_hz') and calib:
+        clk = valu['clock_hz']
+        cpi = calib['peak']['simd_cycles_per_wave_valu_inst']
+        a = valu['valu_insts_per_sample'] * launch_samples / kernel_s / 1e9
+        pk = 1024 * clk / cpi / 1e9
+        busy = valu['valu_busy_cycles_per_sample'] * launch_samples / kernel_s / 1e9
         ia = valu['valu_insts_per_sample'] * 64 * launch_samples / kernel_s / 1e12
-        ipk = 1024 * 32 * valu['clock_hz'] / 1e12
-        vl = {'achieved': round(a, 1), 'peak': round(pk, 1), 'unit': 'G VALU-busy SIMD-cycles/s',
-              'frac': round(a / pk, 5),
-              'issue': {'achieved': round(ia, 3), 'peak': round(ipk, 3), 'unit': 'Tlane-op/s',
-                        'frac': round(ia / ipk, 5), 'valu_insts_per_sample': round(valu['valu_insts_per_sample'], 2)},
-              'clock_mhz': round(valu['clock_hz'] / 1e6, 1),
+        ipk = 1024 * 32 * clk / 1e12
+        vl = {'achieved': round(a, 2), 'peak': round(pk, 2), 'unit': 'G wave64 VALU instructions/s',
+              'frac': round(a / pk, 5), 'valu_insts_per_sample': round(valu['valu_insts_per_sample'], 2),
+              'calibration': {'simd_cycles_per_wave_valu_inst': cpi, 'source': calib['source'],
+                              'kernel': calib['peak']['kernel'], 'busy_at_saturation': calib['peak']['valu_busy_per_simd']},
+              'busy': {'achieved': round(busy, 1), 'peak': round(1024 * clk / 1e9, 1),
+                       'unit': 'G VALU-busy SIMD-cycles/s', 'frac': round(busy / (1024 * clk / 1e9), 5)},
+              'spec_lane_issue': {'achieved': round(ia, 3), 'peak': round(ipk, 3), 'unit': 'Tlane-op/s',
+                                  'frac': round(ia / ipk, 5),
+                                  'note': 'unpacked f32 VALU reaches at most ~0.48 of this (calibration)'},
+              'clock_mhz': round(clk / 1e6, 1),
               'wait_frac_per_wave': round(valu['wait_frac_per_wave'], 4), 'source': valu['source']}
     cands = [(k, v) for k, v in (('hbm', hbm), ('valu', vl)) if v]
     reason = None
@@ -218,6 +246,8 @@ def roofline_line(bps, launch_samples, kernel_s, cfg, lib_hash=None):
             'traffic_unit': 'B per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)',
             'hbm': hbm, 'valu': vl, 'hbm_model': model, 'kernel_ms_avg': round(kernel_s * 1e3, 3),
             'lib_sha256': lib_hash}
+    if stalls:
+        line['stalls'] = {k: stalls.get(k) for k in ('per_sample', 'latency_cycles', 'source', 'lib_sha256')}
     if reason:
         line['frac_null_reason'] = reason
     elif stale:

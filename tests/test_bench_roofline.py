@@ -23,7 +23,7 @@ VALU = {'valu_busy_cycles_per_sample': 700.0, 'clock_hz': 2.4e9, 'valu_insts_per
 def _line(monkeypatch, stamp_t, stamp_v, lib):
     b = _bench()
     profs = {'traffic': dict(TRAFFIC, lib_sha256=stamp_t), 'valu': dict(VALU, lib_sha256=stamp_v)}
-    monkeypatch.setattr(b, 'measured_profile', lambda kind, cfg: dict(profs[kind]))
+    monkeypatch.setattr(b, 'measured_profile', lambda kind, cfg: dict(profs[kind]) if kind in profs else None)
     return b.roofline_line(2000.0, 4.7e8, 0.18, 'C2', lib)
 
 
@@ -44,6 +44,21 @@ def test_one_stale_profile_is_dropped(monkeypatch):
     ln = _line(monkeypatch, 'new', 'old', 'new')
     assert ln['bound'] == 'hbm' and ln['frac'] is not None and ln['valu'] is None
     assert any('rX_valu_C2.json' in x for x in ln['stale_profiles_ignored'])
+
+
+def test_valu_frac_is_against_the_calibrated_issue_peak(monkeypatch):
+    """the valu roof is the instruction rate a pure-VALU kernel
+    sustains (profiles/r*_valu_calib.json), not the 4-cycle busy metric."""
+    b = _bench()
+    cal = b.valu_calibration()
+    assert cal is not None and 3.5 < cal['peak']['simd_cycles_per_wave_valu_inst'] < 5.0
+    ln = _line(monkeypatch, 'abc', 'abc', 'abc')
+    v = ln['valu']
+    rate = VALU['valu_insts_per_sample'] * 4.7e8 / 0.18
+    peak = 1024 * VALU['clock_hz'] / cal['peak']['simd_cycles_per_wave_valu_inst']
+    assert abs(v['frac'] - rate / peak) < 1e-4 and v['calibration']['source'] == cal['source']
+    assert abs(v['busy']['frac'] - VALU['valu_busy_cycles_per_sample'] * 4.7e8 / 0.18 / (1024 * 2.4e9)) < 1e-4
+    assert v['spec_lane_issue']['frac'] < v['frac']
 
 
 def test_lib_sha256_is_the_file_hash(tmp_path):
