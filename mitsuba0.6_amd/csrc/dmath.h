@@ -61,39 +61,6 @@ __device__ __forceinline__ float d_powf(float x, float y) { return glf_powf(x, y
 __device__ __forceinline__ float d_fastexp(float x) { return (float)exp((double)x); }
 __device__ __forceinline__ float d_fastlog(float x) { return (float)log((double)x); }
 
-// Two lanes of f32 work in one VALU instruction: v_pk_mul_f32 / v_pk_add_f32 /
-// v_pk_fma_f32 issue at the same rate as the unpacked v_fma_f32 (tools/valu_calib.hip,
-// profiles/r06_valu_calib.json: 4.19 SIMD-cycles per wave instruction either way), so a
-// pair of independent f32 operations packed into one costs half.  Each half is the
-// IEEE operation of its own operands: the same bits as the two scalar operations.
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// {a / b.x, a / b.y}, IEEE correctly rounded: the compiler's own lowering of an f32
-// division (v_div_scale of denominator and numerator, v_rcp, Newton-Raphson FMAs,
-// v_div_fmas with the numerator's scale flag, v_div_fixup for the special cases),
-// with the six FMA / multiply steps of the two quotients packed pairwise.  Denormals
-// are on (-fno-gpu-flush-denormals-to-zero), so no mode switch surrounds the FMAs.
-// Checked against `/` on the device: tools/div2_check.hip.
-__device__ __forceinline__ f2v div2(float a, f2v b) {
-    bool vd0, vd1, vn0, vn1;
-    const float d0 = __builtin_amdgcn_div_scalef(a, b.x, false, &vd0);
-    const float d1 = __builtin_amdgcn_div_scalef(a, b.y, false, &vd1);
-    const float n0 = __builtin_amdgcn_div_scalef(a, b.x, true, &vn0);
-    const float n1 = __builtin_amdgcn_div_scalef(a, b.y, true, &vn1);
-    const f2v den = {d0, d1}, num = {n0, n1};
-    f2v r = {__builtin_amdgcn_rcpf(d0), __builtin_amdgcn_rcpf(d1)};
-    const f2v one = {1.0f, 1.0f};
-    const f2v e = __builtin_elementwise_fma(-den, r, one);
-    r = __builtin_elementwise_fma(e, r, r);
-    f2v q = num * r;
-    const f2v e2 = __builtin_elementwise_fma(-den, q, num);
-    q = __builtin_elementwise_fma(e2, r, q);
-    const f2v e3 = __builtin_elementwise_fma(-den, q, num);
-    const float f0 = __builtin_amdgcn_div_fmasf(e3.x, r.x, q.x, vn0);
-    const float f1 = __builtin_amdgcn_div_fmasf(e3.y, r.y, q.y, vn1);
-    return f2v{__builtin_amdgcn_div_fixupf(f0, b.x, a), __builtin_amdgcn_div_fixupf(f1, b.y, a)};
-}
-
 struct Frame { f3 s, t, n; };
 __device__ __forceinline__ f3 to_local(const Frame &f, f3 v) { return mk(dot(v, f.s), dot(v, f.t), dot(v, f.n)); }
 __device__ __forceinline__ f3 to_world(const Frame &f, f3 v) {

@@ -460,91 +460,6 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float y) {
     return __builtin_fmaf(r, y, q);
 }
 
-// the same two quotients a / b.x, a / b.y with both rays' steps packed pairwise
-__device__ __forceinline__ f2v div_by_rcp2(float a, f2v b, f2v y) {
-    const f2v av = {a, a};
-    f2v q = av * y;
-    f2v r = __builtin_elementwise_fma(-b, q, av);
-    q = __builtin_elementwise_fma(r, y, q);
-    r = __builtin_elementwise_fma(-b, q, av);
-    return __builtin_elementwise_fma(r, y, q);
-}
-
-#ifndef MTSG_SCAN_PK
-#define MTSG_SCAN_PK 2
-#endif
-#if MTSG_SCAN_PK
-// scan_pair's record loop with the two rays' arithmetic packed: C2 is VALU-issue
-// bound (profiles/r06_valu_calib.json: its kernel issues VALU at 0.96 of the rate a
-// pure-VALU kernel sustains), and the shadow and closest-hit rays of a record
-// repeat the same operations on their own operands -- the denominators, the
-// FMA / multiply steps of the two correctly rounded divisions (div2), and the
-// barycentric test.  Each pair is one v_pk_* instruction (the same rate as one
-// unpacked one), each half the IEEE result of its own operands in the reference's
-// order (triaccel.h:92-160), so the hits are those of scan_pair_k below.  Both
-// rays' barycentrics are formed for every record (no branch per ray): the
-// acceptance tests read them.
-template <int K, bool AL, bool FAST, bool STATS>
-__device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 ds, f3 dc, float minS, float maxS,
-                                            float minC, bool &occ, bool &found, uint32_t &bestPrim, float &bu,
-                                            float &bv, float &bt, unsigned long long &tests, float yS = 0,
-                                            float yC = 0) {
-    const float o_u = K == 0 ? o.y : K == 1 ? o.z : o.x, o_v = K == 0 ? o.z : K == 1 ? o.x : o.y,
-                o_k = K == 0 ? o.x : K == 1 ? o.y : o.z;
-    const f2v du = {K == 0 ? ds.y : K == 1 ? ds.z : ds.x, K == 0 ? dc.y : K == 1 ? dc.z : dc.x};
-    const f2v dv = {K == 0 ? ds.z : K == 1 ? ds.x : ds.y, K == 0 ? dc.z : K == 1 ? dc.x : dc.y};
-    const f2v dk = {K == 0 ? ds.x : K == 1 ? ds.y : ds.z, K == 0 ? dc.x : K == 1 ? dc.y : dc.z};
-    const f2v ou = {o_u, o_u}, ov = {o_v, o_v}, y = {yS, yC};
-    for (uint32_t i = 0; i < n; ++i) {
-        if (STATS) tests += 2;
-        cst_tri &tr = tris[i];
-        const float n_u = tr.n_u, n_v = tr.n_v, n_d = tr.n_d, a_u = tr.a_u, a_v = tr.a_v, b_nu = tr.b_nu,
-                    b_nv = tr.b_nv, c_nu = tr.c_nu, c_nv = tr.c_nv;
-        const uint32_t prim = tr.prim;
-        // TriAccel::rayIntersect (triaccel.h:92-160) for both rays (x: shadow, y: closest)
-        const float num = AL ? n_d - o_k : n_d - o_u * n_u - o_v * n_v - o_k;
-        f2v t;
-        if (AL && FAST) t = div_by_rcp2(num, dk, y);
-        else if (AL) t = div2(num, dk);
-        else t = div2(num, du * n_u + dv * n_v + dk);
-#if MTSG_SCAN_PK == 1
-        const f2v hu = ou + t * du - a_u;
-        const f2v hv = ov + t * dv - a_v;
-        const f2v u = hv * b_nu + hu * b_nv;
-        const f2v v = hu * c_nu + hv * c_nv;
-        const f2v w = u + v;
-        if (!(t.x < minS || t.x > maxS) && u.x >= 0 && v.x >= 0 && w.x <= 1.0f) occ = true;
-        if (!(t.y < minC || t.y > bt) && u.y >= 0 && v.y >= 0 && w.y <= 1.0f) {
-            if (!found || t.y < bt || prim > bestPrim) {
-                found = true; bestPrim = prim; bt = t.y; bu = u.y; bv = v.y;
-            }
-        }
-#else
-        // the barycentric tests stay per ray behind their interval tests: a wave
-        // skips a ray's whole test when no lane's t falls in its interval
-        const float tS = t.x, tC = t.y;
-        if (!(tS < minS || tS > maxS)) {
-            const float hu = o_u + tS * du.x - a_u;
-            const float hv = o_v + tS * dv.x - a_v;
-            const float u = hv * b_nu + hu * b_nv;
-            const float v = hu * c_nu + hv * c_nv;
-            if (u >= 0 && v >= 0 && u + v <= 1.0f) occ = true;
-        }
-        if (!(tC < minC || tC > bt)) {
-            const float hu = o_u + tC * du.y - a_u;
-            const float hv = o_v + tC * dv.y - a_v;
-            const float u = hv * b_nu + hu * b_nv;
-            const float v = hu * c_nu + hv * c_nv;
-            if (u >= 0 && v >= 0 && u + v <= 1.0f) {
-                if (!found || tC < bt || prim > bestPrim) {
-                    found = true; bestPrim = prim; bt = tC; bu = u; bv = v;
-                }
-            }
-        }
-#endif
-    }
-}
-#else
 // FAST (axis-aligned groups only): the two quotients through div_by_rcp with
 // the rays' reciprocals yS = RN(1/s_k), yC = RN(1/c_k)
 template <int K, bool AL, bool FAST, bool STATS>
@@ -589,7 +504,6 @@ __device__ __forceinline__ void scan_pair_k(cst_tri *tris, uint32_t n, f3 o, f3 
         }
     }
 }
-#endif
 
 template <bool STATS>
 __device__ __forceinline__ void scan_pair(const MtsgLaunch &L, f3 o, f3 ds, f3 dc, float minS, float maxS, float minC,
