@@ -298,7 +298,14 @@ int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap);
  * 168-173); as in the loader they take precedence over the file's <default>s
  * (scenehandler.cpp:684-687).  A property's flags say whether its value went
  * through a substitution (MTSGPU_XML_PROP_PARAM) and whether a <default>
- * supplied it (MTSGPU_XML_PROP_DEFAULT).  The shim rebuilds a Properties
+ * supplied it (MTSGPU_XML_PROP_DEFAULT).  A property element this reader
+ * does not turn into a value -- one without a value attribute (<spectrum
+ * filename=...>, <blackbody ...>) or a sampled spectrum ("400:0.1, 500:0.2")
+ * -- is returned with MTSGPU_XML_PROP_UNSUPPORTED and its attributes as
+ * "key=value ..." in value: the shim takes such a value from the plugin's own
+ * Properties, which the loader has parsed.  The parse of a file (with its
+ * includes and parameters) is cached while the files are unchanged, so the
+ * shim's one call per BSDF reads the scene once.  The shim rebuilds a Properties
  * object per node.  Returns MTSGPU_OK, MTSGPU_ENOENT (the id is not in the
  * file), MTSGPU_EINVAL (unreadable file, syntax error, undefined parameter,
  * duplicate id, wrong element kind; message in err), or MTSGPU_ENOMEM when a
@@ -306,7 +313,7 @@ int mtsgpu_check_scene(const mtsgpu_scene_desc *scene, char *msg, size_t cap);
  * mtsgpu_xml_bsdf is the BY_ID lookup without loader parameters. */
 enum { MTSGPU_XML_BSDF = 0, MTSGPU_XML_TEXTURE = 1 };
 enum { MTSGPU_XML_BY_ID = 0, MTSGPU_XML_BY_SHAPE = 1 };
-enum { MTSGPU_XML_PROP_PARAM = 1, MTSGPU_XML_PROP_DEFAULT = 2 };
+enum { MTSGPU_XML_PROP_PARAM = 1, MTSGPU_XML_PROP_DEFAULT = 2, MTSGPU_XML_PROP_UNSUPPORTED = 4 };
 typedef struct {
     int32_t kind;                   /* MTSGPU_XML_BSDF / MTSGPU_XML_TEXTURE        */
     int32_t parent;                 /* parent node index, -1 for node 0            */

@@ -49,6 +49,8 @@
 #include <mitsuba/core/bitmap.h>
 
 #include <cstring>
+#include <set>
+#include <vector>
 #include <fstream>
 #include <sstream>
 
@@ -389,17 +391,22 @@ private:
                                                shape->getName().c_str(), shape->getID().c_str());
         if (!m_sceneFile.empty()) {
             int idx = xmlBsdf(bsdf, bsdf->getID(), MTSGPU_XML_BY_ID, where);
-            if (idx == -2) idx = xmlBsdf(bsdf, shape->getID(), MTSGPU_XML_BY_SHAPE, where);
+            /* the meshes of a compound shape (OBJ, serialized) carry no <shape> id: TriMesh(name, ...)
+               is built on empty Properties (trimesh.cpp:43), so its id is "unnamed" */
+            if (idx == -2 && shape->getID() != "unnamed") idx = xmlBsdf(bsdf, shape->getID(), MTSGPU_XML_BY_SHAPE, where);
             if (idx >= 0) return idx;
         }
         const Properties &p = bsdf->getProperties();
+        const std::string hint = shape->getID() == "unnamed"
+            ? "a mesh of a compound shape (OBJ / serialized file) does not carry its <shape>'s id: give the BSDF "
+              "itself an id (<bsdf id=...>, or a <ref> to one) in " : "give the BSDF (or its shape) an id in ";
         if (p.getPluginName() == "twosided")
             Log(EError, "twosided BSDF \"%s\" %s: its nested BSDFs are read from the scene file, which does not "
-                "hold it; give the BSDF (or its shape) an id in %s", bsdf->getID().c_str(), where.c_str(),
+                "hold it; %s%s", bsdf->getID().c_str(), where.c_str(), hint.c_str(),
                 m_sceneFile.empty() ? "a scene file" : m_sceneFile.string().c_str());
         if (!isConstant(bsdf))
             Log(EError, "BSDF \"%s\" %s has a textured parameter, and textures are read from the scene file, which "
-                "does not hold it; give the BSDF (or its shape) an id in %s", bsdf->getID().c_str(), where.c_str(),
+                "does not hold it; %s%s", bsdf->getID().c_str(), where.c_str(), hint.c_str(),
                 m_sceneFile.empty() ? "a scene file" : m_sceneFile.string().c_str());
         return appendDesc(p, bsdf, NULL);
     }
@@ -407,22 +414,26 @@ private:
     /* The loader's parameters ($name substitutions): the integrator's
        'parameters' property ("name=value;name=value") if set, else the
        `mitsuba -D name=value` arguments of this process (mitsuba.cpp:168-173).
-       They take precedence over the file's <default>s, as in the loader. */
-    void loaderParameters(std::vector<std::string> &names, std::vector<std::string> &values) const {
+       They take precedence over the file's <default>s, as in the loader.
+       Returns false when they cannot be known: no 'parameters' property, and this
+       process is not the mitsuba command-line renderer (mtssrv, mtsgui, Python). */
+    bool loaderParameters(std::vector<std::string> &names, std::vector<std::string> &values) const {
         std::string cmdline, bad;
         if (!m_props.hasProperty("parameters")) {
             std::ifstream is("/proc/self/cmdline", std::ios::binary);
             cmdline.assign(std::istreambuf_iterator<char>(is), std::istreambuf_iterator<char>());
         }
+        bool known = true;
         if (!gpupath_loader_params(m_props.hasProperty("parameters"), m_props.getString("parameters", ""), cmdline,
-                                   names, values, bad))
+                                   names, values, bad, &known))
             Log(EError, "Invalid parameter specification \"%s\"", bad.c_str());
+        return known;
     }
 
     /* The file's tree for `id` -> descriptors; -2 when the file does not hold it */
     int xmlBsdf(const BSDF *bsdf, const std::string &id, int lookup, const std::string &where) {
         std::vector<std::string> pn, pv;
-        loaderParameters(pn, pv);
+        const bool paramsKnown = loaderParameters(pn, pv);
         std::vector<const char *> pnc, pvc;
         for (size_t i = 0; i < pn.size(); ++i) { pnc.push_back(pn[i].c_str()); pvc.push_back(pv[i].c_str()); }
         std::vector<mtsgpu_xml_node> nodes(64);
@@ -442,15 +453,36 @@ private:
         if (rc != MTSGPU_OK)
             Log(EError, "BSDF \"%s\" %s, read from %s: %s", bsdf->getID().c_str(), where.c_str(), file.c_str(), err);
         nodes.resize((size_t) nn);
-        /* The top BSDF's own properties are visible: a value the file's <default>
-           supplied must be the one the loader used, or the loader had a parameter
-           this shim was not given (nested elements could differ the same way). */
+        props.resize((size_t) np);
         const Properties &have = bsdf->getProperties();
+        /* by id: the element must describe this object.  An OBJ's .mtl materials are BSDFs
+           whose id is the material name (obj.cpp:573) and which the file does not hold; an
+           unrelated file element with that id differs from them in its plugin or in the set of
+           its own properties (the loader sets exactly the file's properties on a BSDF it builds) */
+        if (lookup == MTSGPU_XML_BY_ID) {
+            bool same = std::string(nodes[0].plugin) == have.getPluginName();
+            std::set<std::string> fileNames;
+            for (int i = nodes[0].first_prop; i < nodes[0].first_prop + nodes[0].num_props; ++i)
+                fileNames.insert(props[i].name);
+            const std::vector<std::string> haveNames = have.getPropertyNames();
+            same = same && fileNames.size() == haveNames.size();
+            for (size_t k = 0; same && k < haveNames.size(); ++k) same = fileNames.count(haveNames[k]) != 0;
+            if (!same) return -2;
+        }
         if (std::string(nodes[0].plugin) != have.getPluginName())
             Log(EError, "BSDF \"%s\" %s is a \"%s\" in the scene but a \"%s\" in %s", bsdf->getID().c_str(),
                 where.c_str(), have.getPluginName().c_str(), nodes[0].plugin, file.c_str());
+        for (size_t i = 0; i < props.size(); ++i)
+            if (!paramsKnown && (props[i].flags & MTSGPU_XML_PROP_PARAM))
+                Log(EError, "BSDF \"%s\" %s: %s uses $parameters (\"%s\"), and this process is not the mitsuba "
+                    "renderer, whose -D arguments they would be: set the integrator's 'parameters' property to the "
+                    "loader's name=value list", bsdf->getID().c_str(), where.c_str(), file.c_str(), props[i].name);
+        /* The top BSDF's own properties are visible: a value the file's <default>
+           supplied must be the one the loader used, or the loader had a parameter
+           this shim was not given (nested elements could differ the same way). */
         Properties fromFile(nodes[0].plugin);
         for (int i = nodes[0].first_prop; i < nodes[0].first_prop + nodes[0].num_props; ++i) {
+            if (props[i].flags & MTSGPU_XML_PROP_UNSUPPORTED) continue;   /* taken from `have` (xmlNode) */
             setProperty(fromFile, props[i]);
             const std::string name = props[i].name;
             if ((props[i].flags & MTSGPU_XML_PROP_DEFAULT) && have.hasProperty(name) &&
@@ -467,8 +499,20 @@ private:
     int xmlNode(const std::vector<mtsgpu_xml_node> &nodes, const std::vector<mtsgpu_xml_prop> &props, int k,
                 const BSDF *obj) {
         Properties p(nodes[k].plugin);
-        for (int i = nodes[k].first_prop; i < nodes[k].first_prop + nodes[k].num_props; ++i)
-            setProperty(p, props[i]);
+        for (int i = nodes[k].first_prop; i < nodes[k].first_prop + nodes[k].num_props; ++i) {
+            if (!(props[i].flags & MTSGPU_XML_PROP_UNSUPPORTED)) {
+                setProperty(p, props[i]);
+                continue;
+            }
+            /* <spectrum filename=...>, a sampled spectrum, <blackbody>: the loader's parsed value,
+               which only the top BSDF's own Properties expose */
+            const std::string name = props[i].name;
+            if (k != 0 || !obj || !obj->getProperties().hasProperty(name))
+                Log(EError, "<%s name=\"%s\" %s> in a nested element of BSDF \"%s\": this form is only supported "
+                    "on the top BSDF (or give it as a value)", props[i].tag, props[i].name, props[i].value,
+                    obj ? obj->getID().c_str() : nodes[0].id);
+            p.copyAttribute(obj->getProperties(), name, name);
+        }
         std::vector<std::pair<std::string, mtsgpu_texture_desc> > tex;
         std::vector<int> nested;
         for (int c = k + 1; c < (int) nodes.size(); ++c) {

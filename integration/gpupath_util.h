@@ -7,10 +7,11 @@
  *                           a BSDF the scene file does not hold, to refuse a
  *                           textured one instead of rendering its defaults;
  *   gpupath_loader_params   the loader's $parameters: the integrator's
- *                           'parameters' property, else the process's
+ *                           'parameters' property, else -- in the mitsuba
+ *                           command-line renderer only -- the process's
  *                           `mitsuba -D name=value` arguments
  *                           (src/mitsuba/mitsuba.cpp:168-173, getopt syntax:
- *                           "-D", "a=b" or "-Da=b").
+ *                           "-D", "a=b" or "-Da=b"; tokenize on '=').
  */
 #ifndef GPUPATH_UTIL_H
 #define GPUPATH_UTIL_H
@@ -37,14 +38,33 @@ inline std::vector<std::pair<float, float> > gpupath_probe_uv() {
     return uv;
 }
 
+/* mitsuba.cpp's tokenize(optarg, "="): the pieces between '=' characters, empty
+   ones dropped ("a==b" and "=a=b" give a and b) */
+inline std::vector<std::string> gpupath_tokenize_eq(const std::string &s) {
+    std::vector<std::string> t;
+    size_t b = 0;
+    while (b <= s.size()) {
+        size_t e = s.find('=', b);
+        if (e == std::string::npos) e = s.size();
+        if (e > b) t.push_back(s.substr(b, e - b));
+        b = e + 1;
+    }
+    return t;
+}
+
 /* name=value pairs.  `property`: the 'parameters' property ("a=1;b=2"), used
-   when `has_property`; otherwise `argv` (the NUL-separated /proc/self/cmdline).
-   Returns false (and the offending token in `bad`) for a pair without '=',
-   which the loader rejects as an "Invalid parameter specification". */
+   when `has_property`; otherwise `argv` (the NUL-separated /proc/self/cmdline),
+   but only when argv[0] is the mitsuba command-line renderer: under mtssrv,
+   mtsgui or the Python bindings the -D arguments belong to another program,
+   and *known is set to false (no parameters are returned).  A pair is split as
+   mitsuba.cpp:168-173 splits it (tokenize on '=', exactly two tokens); returns
+   false (and the offending token in `bad`) for one the loader rejects with
+   "Invalid parameter specification". */
 inline bool gpupath_loader_params(bool has_property, const std::string &property, const std::string &cmdline,
                                   std::vector<std::string> &names, std::vector<std::string> &values,
-                                  std::string &bad) {
+                                  std::string &bad, bool *known = 0) {
     std::vector<std::string> pairs;
+    if (known) *known = true;
     if (has_property) {
         size_t b = 0;
         while (b <= property.size()) {
@@ -62,6 +82,11 @@ inline bool gpupath_loader_params(bool has_property, const std::string &property
             argv.push_back(cmdline.substr(b, e - b));
             b = e + 1;
         }
+        const std::string exe = argv.empty() ? std::string() : argv[0].substr(argv[0].find_last_of('/') + 1);
+        if (exe != "mitsuba") {
+            if (known) *known = false;
+            return true;
+        }
         for (size_t i = 1; i < argv.size(); ++i) {
             if (argv[i] == "--") break;
             if (argv[i] == "-D" && i + 1 < argv.size()) pairs.push_back(argv[++i]);
@@ -69,15 +94,13 @@ inline bool gpupath_loader_params(bool has_property, const std::string &property
         }
     }
     for (size_t i = 0; i < pairs.size(); ++i) {
-        /* mitsuba.cpp tokenizes on '=' and wants exactly two tokens */
-        const size_t eq = pairs[i].find('=');
-        if (eq == std::string::npos || eq == 0 || eq + 1 == pairs[i].size() ||
-            pairs[i].find('=', eq + 1) != std::string::npos) {
+        const std::vector<std::string> t = gpupath_tokenize_eq(pairs[i]);
+        if (t.size() != 2) {
             bad = pairs[i];
             return false;
         }
-        names.push_back(pairs[i].substr(0, eq));
-        values.push_back(pairs[i].substr(eq + 1));
+        names.push_back(t[0]);
+        values.push_back(t[1]);
     }
     return true;
 }

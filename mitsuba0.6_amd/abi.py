@@ -126,7 +126,7 @@ def uptr(a):
 
 XML_BSDF, XML_TEXTURE = 0, 1
 XML_BY_ID, XML_BY_SHAPE = 0, 1                # mtsgpu_xml_bsdf_ex lookup
-XML_PROP_PARAM, XML_PROP_DEFAULT = 1, 2      # mtsgpu_xml_prop.flags
+XML_PROP_PARAM, XML_PROP_DEFAULT, XML_PROP_UNSUPPORTED = 1, 2, 4   # mtsgpu_xml_prop.flags
 
 
 class XmlNode(C.Structure):

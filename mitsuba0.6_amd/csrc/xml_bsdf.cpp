@@ -22,9 +22,11 @@
 //   - ids are registered when their element ends; a second element with the
 //     same id is an error (:784-786), and so is an <alias> onto a taken id
 //     (:646-656);
-//   - <include filename> parses the named file with the same parameters and
-//     ids (:658-680), relative to the including file's directory (the
-//     FileResolver has the scene's directory first);
+//   - <include filename> parses the named file with the ids shared and a copy
+//     of the parameters (:658-680, SceneHandler(m_params, ...)), so a <default>
+//     inside the included file does not reach the including one; a relative
+//     name resolves against the main scene file's directory first, as the
+//     FileResolver has it first (mitsuba.cpp), then as given;
 //   - the `type` attribute is lower-cased (:275).
 // Each returned property carries flags saying whether its value went through a
 // substitution and whether a <default> supplied it, so a caller that cannot
@@ -33,12 +35,15 @@
 // The XML subset is the scene format's own: elements, attributes in single or
 // double quotes, self-closing tags, comments, the XML declaration, the five
 // predefined entities.
+#include <sys/stat.h>
+
 #include <cctype>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <sstream>
 #include <string>
@@ -72,10 +77,14 @@ struct XParser {
     std::string err;
     explicit XParser(const std::string &src) : s(src) {}
 
-    int line_at(size_t pos) const {
-        int line = 1;
-        for (size_t k = 0; k < pos && k < s.size(); ++k) line += s[k] == '\n';
-        return line;
+    // line numbers: counted forward from the last position asked for (elements are
+    // parsed in document order), so a parse is linear in the file size
+    size_t line_pos = 0;
+    int line_no = 1;
+    int line_at(size_t pos) {
+        if (pos < line_pos) { line_pos = 0; line_no = 1; }
+        for (; line_pos < pos && line_pos < s.size(); ++line_pos) line_no += s[line_pos] == '\n';
+        return line_no;
     }
     bool fail(const std::string &m) {
         if (err.empty()) err = m + " (line " + std::to_string(line_at(i)) + ")";
@@ -186,6 +195,11 @@ std::string dir_of(const std::string &path) {
 
 // The document-order pass of SceneHandler over a file and its includes:
 // parameter substitution, <default>, ids, <alias>, <include>.
+bool file_exists(const std::string &path) {
+    struct stat st;
+    return ::stat(path.c_str(), &st) == 0;
+}
+
 struct Loader {
     std::map<std::string, std::string> params;   // name -> value (the loader's and then <default>'s)
     std::set<std::string> from_default;          // names a <default> supplied
@@ -255,8 +269,15 @@ struct Loader {
         if (e.tag == "include") {
             const std::string *fn = e.attr("filename");
             if (!fn) return fail(file, e, "<include> without a filename");
-            const std::string p = (!fn->empty() && (*fn)[0] == '/') ? *fn : dir_of(file) + *fn;
-            return load(p, depth + 1);
+            std::string p = *fn;
+            if (!fn->empty() && (*fn)[0] != '/' && file_exists(dir_of(files[0]) + *fn)) p = dir_of(files[0]) + *fn;
+            // SceneHandler(m_params, m_namedObjects, true): ids shared, parameters copied
+            const std::map<std::string, std::string> saved = params;
+            const std::set<std::string> savedDefault = from_default;
+            const bool ok = load(p, depth + 1);
+            params = saved;
+            from_default = savedDefault;
+            return ok;
         }
         const std::string *id = e.attr("id");
         if (id && !id->empty() && e.tag != "ref" && e.tag != "scene") {
@@ -308,13 +329,23 @@ struct TreeBuilder {
             if (v) {
                 val = *v;
                 p.flags = k->attr_flags("value");
+                // a sampled spectrum ("wavelength:value, ..."): the plugin's parsed value is used
+                if (t == "spectrum" && val.find(':') != std::string::npos) p.flags |= MTSGPU_XML_PROP_UNSUPPORTED;
             } else if (t == "point" || t == "vector") {   // x/y/z form
                 auto xyz = [&](const char *a) { return k->attr(a) ? *k->attr(a) : std::string("0"); };
                 val = xyz("x") + ", " + xyz("y") + ", " + xyz("z");
                 p.flags = k->attr_flags("x") | k->attr_flags("y") | k->attr_flags("z");
             } else {
-                err = "<" + t + "> in <" + e.tag + " type=\"" + *type + "\"> has no value (not supported here)";
-                return false;
+                // <spectrum filename=...>, <blackbody temperature=...>, ...: the attributes as
+                // text; the caller takes the value from the plugin's own Properties
+                for (size_t a = 0; a < k->attrs.size(); ++a) {
+                    if (k->attrs[a].first == "name") continue;
+                    if (!val.empty()) val += " ";
+                    val += k->attrs[a].first + "=" + k->attrs[a].second;
+                    p.flags |= k->flags[a];
+                }
+                if (val.size() > sizeof p.value - 1) val.resize(sizeof p.value - 1);
+                p.flags |= MTSGPU_XML_PROP_UNSUPPORTED;
             }
             if (!copy(p.tag, sizeof p.tag, t) || !copy(p.name, sizeof p.name, nm ? *nm : std::string()) ||
                 !copy(p.value, sizeof p.value, val)) {
@@ -353,6 +384,53 @@ struct TreeBuilder {
     }
 };
 
+// One parsed scene per (file, parameters), reused while none of its files changed
+// (size and modification time of the main file and of every include): the shim asks
+// once per BSDF, and an exported scene with thousands of shapes must not be re-read
+// for each.
+struct FileStamp {
+    std::string path;
+    long long size, mtime_ns;
+    bool operator==(const FileStamp &o) const { return path == o.path && size == o.size && mtime_ns == o.mtime_ns; }
+};
+FileStamp stamp(const std::string &path) {
+    struct stat st;
+    if (::stat(path.c_str(), &st) != 0) return {path, -1, -1};
+    return {path, (long long)st.st_size, (long long)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec};
+}
+struct CacheEntry {
+    std::map<std::string, std::string> params;
+    std::vector<FileStamp> stamps;
+    std::shared_ptr<const Loader> loader;
+};
+std::mutex g_cache_mu;
+std::vector<CacheEntry> g_cache;   // most recent last, at most 4 scenes
+
+std::shared_ptr<const Loader> cached_load(const std::string &path, const std::map<std::string, std::string> &params,
+                                          std::string &err) {
+    std::lock_guard<std::mutex> lock(g_cache_mu);
+    for (size_t k = 0; k < g_cache.size(); ++k) {
+        const CacheEntry &c = g_cache[k];
+        if (c.params != params || c.stamps.empty() || c.stamps[0].path != path) continue;
+        bool same = true;
+        for (const FileStamp &f : c.stamps) same = same && stamp(f.path) == f;
+        if (same) return c.loader;
+    }
+    std::shared_ptr<Loader> L(new Loader());
+    L->params = params;
+    if (!L->load(path, 0)) {
+        err = L->err;
+        return nullptr;
+    }
+    CacheEntry c;
+    c.params = params;
+    for (const std::string &f : L->files) c.stamps.push_back(stamp(f));
+    c.loader = L;
+    if (g_cache.size() >= 4) g_cache.erase(g_cache.begin());
+    g_cache.push_back(c);
+    return L;
+}
+
 }  // namespace
 
 extern "C" int mtsgpu_xml_bsdf_ex(const char *xml_path, const char *id, int32_t lookup, const char *const *param_names,
@@ -368,12 +446,15 @@ extern "C" int mtsgpu_xml_bsdf_ex(const char *xml_path, const char *id, int32_t 
         (lookup != MTSGPU_XML_BY_ID && lookup != MTSGPU_XML_BY_SHAPE))
         return fail(MTSGPU_EINVAL, "null or invalid argument");
     *num_nodes = *num_props = 0;
-    Loader L;
+    std::map<std::string, std::string> params;
     for (int k = 0; k < num_params; ++k) {
         if (!param_names[k] || !param_values[k]) return fail(MTSGPU_EINVAL, "null parameter name or value");
-        L.params[param_names[k]] = param_values[k];
+        params[param_names[k]] = param_values[k];
     }
-    if (!L.load(xml_path, 0)) return fail(MTSGPU_EINVAL, L.err);
+    std::string lerr;
+    std::shared_ptr<const Loader> Lp = cached_load(xml_path, params, lerr);
+    if (!Lp) return fail(MTSGPU_EINVAL, lerr);
+    const Loader &L = *Lp;
     TreeBuilder E(L);
     auto it = L.ids.find(id);
     const XElem *bsdf = nullptr;

@@ -35,8 +35,10 @@ int main(int argc, char **argv) {
     std::string cmd((std::istreambuf_iterator<char>(std::cin)), std::istreambuf_iterator<char>());
     std::vector<std::string> n, v;
     std::string bad;
-    const bool ok = gpupath_loader_params(argv[2][0] == '1', argv[3], cmd, n, v, bad);
+    bool known = true;
+    const bool ok = gpupath_loader_params(argv[2][0] == '1', argv[3], cmd, n, v, bad, &known);
     if (!ok) { printf("BAD %s\n", bad.c_str()); return 0; }
+    if (!known) { printf("UNKNOWN\n"); return 0; }
     for (size_t k = 0; k < n.size(); ++k) printf("%s|%s\n", n[k].c_str(), v[k].c_str());
     return 0;
 }
@@ -97,6 +99,13 @@ def test_probe_sees_both_colours(harness):
     (None, ['mitsuba', '-Dnoequals'], ['BAD noequals']),
     (None, ['mitsuba', '-Da='], ['BAD a=']),
     ('x=1=2', [], ['BAD x=1=2']),
+    # tokenize(optarg, "=") drops empty tokens (mitsuba.cpp:169-172)
+    (None, ['/opt/mitsuba/bin/mitsuba', '-Da==b', '-D', '=c=d'], ['a|b', 'c|d']),
+    ('x==1;=y=2', [], ['x|1', 'y|2']),
+    # -D arguments of another program are not the loader's (mtssrv, mtsgui, python)
+    (None, ['python3', 'render.py', '-Da=1'], ['UNKNOWN']),
+    (None, ['mtssrv', '-Da=1'], ['UNKNOWN']),
+    ('a=1', ['python3', '-Db=2'], ['a|1']),
 ])
 def test_loader_params(harness, prop, cmd, want):
     out = subprocess.run([harness, 'params', '1' if prop is not None else '0', prop or ''],

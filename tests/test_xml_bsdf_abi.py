@@ -314,3 +314,78 @@ def test_ids_alias_include_and_duplicates(tmp_path):
     noinc.write_text('<scene version="0.6.0"><include filename="missing.xml"/><bsdf type="diffuse" id="a"/></scene>')
     rc, _, _, _, err = _read(str(noinc), 'a')
     assert rc == abi.EINVAL and 'missing.xml' in err
+
+
+# ---- unsupported property forms, <include> parameter scope, one parse per scene -----
+
+def test_unsupported_property_forms_are_flagged(tmp_path):
+    """<spectrum filename=...>, sampled spectra and <blackbody> are not turned into values
+    here: the element comes back flagged MTSGPU_XML_PROP_UNSUPPORTED with its attributes,
+    and the shim takes the loader's parsed value from the plugin's own Properties."""
+    p = tmp_path / 'spd.xml'
+    p.write_text('''<scene version="0.6.0">
+        <bsdf type="roughconductor" id="c">
+            <string name="distribution" value="ggx"/>
+            <spectrum name="eta" filename="data/ior/Cu.eta.spd"/>
+            <spectrum name="k" value="400:0.1, 500:0.2"/>
+            <blackbody name="specularReflectance" temperature="5000K" scale="0.5"/>
+            <float name="alpha" value="0.2"/>
+        </bsdf></scene>''')
+    rc, nodes, props, _, err = _read(str(p), 'c')
+    assert rc == abi.OK, err
+    got = {q.name.decode(): (q.tag.decode(), q.value.decode(), q.flags) for q in props}
+    U = abi.XML_PROP_UNSUPPORTED
+    assert got['eta'] == ('spectrum', 'filename=data/ior/Cu.eta.spd', U)
+    assert got['k'][2] & U and got['k'][1] == '400:0.1, 500:0.2'
+    assert got['specularReflectance'] == ('blackbody', 'temperature=5000K scale=0.5', U)
+    assert got['alpha'] == ('float', '0.2', 0) and got['distribution'][2] == 0
+
+
+def test_include_gets_a_copy_of_the_parameters(tmp_path):
+    """SceneHandler(m_params, ...) for an <include> (scenehandler.cpp:670): the included
+    file sees the including file's parameters, but its own <default> does not reach the
+    including file, whose later <default> of the same name then applies."""
+    sub = tmp_path / 'sub'
+    sub.mkdir()
+    (sub / 'inc.xml').write_text('''<scene version="0.6.0"><default name="a" value="0.9"/>
+        <bsdf type="roughconductor" id="inner"><float name="alpha" value="$a"/>
+        <string name="material" value="$m"/></bsdf><include filename="leaf.xml"/></scene>''')
+    # the FileResolver has the main scene's directory first: leaf.xml resolves there, not in sub/
+    (tmp_path / 'leaf.xml').write_text('<scene version="0.6.0"><bsdf type="diffuse" id="leaf"/></scene>')
+    p = tmp_path / 'main.xml'
+    p.write_text('''<scene version="0.6.0"><default name="m" value="Au"/>
+        <include filename="sub/inc.xml"/>
+        <default name="a" value="0.3"/>
+        <bsdf type="roughconductor" id="outer"><float name="alpha" value="$a"/></bsdf></scene>''')
+    rc, _, props, _, err = _read(str(p), 'inner')
+    assert rc == abi.OK, err
+    assert {q.name: q.value for q in props} == {b'alpha': b'0.9', b'material': b'Au'}
+    rc, _, props, _, err = _read(str(p), 'outer')
+    assert rc == abi.OK and props[0].value == b'0.3', err
+    rc, nodes, _, _, err = _read(str(p), 'leaf')
+    assert rc == abi.OK and nodes[0].plugin == b'diffuse', err
+
+
+def test_large_scene_parsed_once(tmp_path):
+    """An exported scene with thousands of shapes: a parse is linear in the file size and is
+    reused for every BSDF of the scene while the file is unchanged (ADVICE r05)."""
+    import time
+    n = 4000
+    parts = ['<scene version="0.6.0">']
+    for k in range(n):
+        parts.append('<bsdf type="diffuse" id="b%d"><rgb name="reflectance" value="%g, 0.5, 0.5"/></bsdf>' % (k, k / n))
+        parts.append('<shape type="obj" id="s%d"><string name="filename" value="m%d.obj"/><ref id="b%d"/></shape>'
+                     % (k, k, k))
+    parts.append('</scene>')
+    p = tmp_path / 'big.xml'
+    p.write_text('\n'.join(parts))
+    t0 = time.perf_counter()
+    for k in range(0, n, 10):
+        rc, nodes, props, _, err = _read(str(p), 's%d' % k, lookup=abi.XML_BY_SHAPE)
+        assert rc == abi.OK and props[0].value.decode().startswith('%g' % (k / n)), err
+    assert time.perf_counter() - t0 < 10.0
+    # a changed file is read again
+    time.sleep(0.01)
+    p.write_text('\n'.join(parts).replace('id="b0"><rgb name="reflectance" value="0,', 'id="b0"><rgb name="reflectance" value="0.25,'))
+    rc, _, props, _, err = _read(str(p), 'b0')
+    assert rc == abi.OK and props[0].value.startswith(b'0.25'), err

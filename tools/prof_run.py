@@ -16,7 +16,8 @@ cfg = sys.argv[1] if len(sys.argv) > 1 else 'C2'
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 stride = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 engine = sys.argv[4] if len(sys.argv) > 4 else None
-sc, it = scenes.build(cfg, rfilter='box')
+# C2g: C2 with the gaussian filter (bench.py's secondary block)
+sc, it = scenes.build(cfg.rstrip('g'), rfilter='gaussian' if cfg.endswith('g') else 'box')
 ctx = Context(0)
 ctx.upload(sc)
 print('scene', ctx.scene_info())

@@ -14,7 +14,8 @@ from collections import defaultdict
 
 src, rnd = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 1024}
+SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 1024,
+           'C2g': 1280 * 720 * 512}
 sha = None
 if os.path.exists(os.path.join(src, 'lib.sha256')):
     sha = open(os.path.join(src, 'lib.sha256')).read().split()[0]
@@ -37,7 +38,7 @@ def counters(d):
     return acc, n, durs
 
 
-for cfg in ('C2', 'C3', 'C4', 'C5'):
+for cfg in ('C2', 'C3', 'C4', 'C5', 'C2g'):
     a, na, da = counters(os.path.join(src, 'stall_%s_A' % cfg))
     b, nb, db = counters(os.path.join(src, 'stall_%s_B' % cfg))
     c, nc, dc = counters(os.path.join(src, 'stall_%s_C' % cfg))

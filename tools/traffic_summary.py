@@ -36,9 +36,10 @@ def counter(path_glob, name):
 
 
 # samples per profiled launch (one full frame = one launch; C5's 1024 spp fit one splat buffer since r03)
-SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 1024}
+SAMPLES = {'C2': 1280 * 720 * 512, 'C3': 1280 * 720 * 512, 'C4': 1280 * 720 * 256, 'C5': 1280 * 720 * 1024,
+           'C2g': 1280 * 720 * 512}
 
-for cfg in ('C2', 'C3', 'C4', 'C5'):
+for cfg in ('C2', 'C3', 'C4', 'C5', 'C2g'):
     fetch = counter(os.path.join(src, 'pmc_%s_FETCH_SIZE' % cfg, '**', '*counter_collection.csv'), 'FETCH_SIZE')
     write = counter(os.path.join(src, 'pmc_%s_WRITE_SIZE' % cfg, '**', '*counter_collection.csv'), 'WRITE_SIZE')
     if fetch and write:
@@ -65,7 +66,7 @@ for cfg in ('C2', 'C3', 'C4', 'C5'):
         shutil.copy(log, os.path.join(prof, '%s_bench_%s.log' % (rnd, cfg)))
 
 SIMDS, XCDS = 256 * 4, 8
-for cfg in ('C2', 'C3', 'C4', 'C5'):
+for cfg in ('C2', 'C3', 'C4', 'C5', 'C2g'):
     base = os.path.join(src, 'pmc_%s_SQ' % cfg, '**', '*counter_collection.csv')
     names = ['SQ_WAVES', 'SQ_WAVE_CYCLES', 'SQ_ACTIVE_INST_VALU', 'SQ_ACTIVE_INST_ANY', 'SQ_WAIT_ANY',
              'SQ_WAIT_INST_ANY', 'SQ_INSTS_VALU', 'SQ_BUSY_CYCLES', 'GRBM_GUI_ACTIVE']
