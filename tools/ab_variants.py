@@ -39,7 +39,7 @@ def with_env(name, fn):
                 os.environ[k] = v
 
 
-sc, it = scenes.build(cfg, rfilter='box')
+sc, it = scenes.build(cfg.rstrip('g'), rfilter='gaussian' if cfg.endswith('g') else 'box')   # C2g: gaussian
 ctxs = {}
 for name, path in variants:
     c = Context(0, lib_path=path)
