@@ -697,6 +697,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         L.bset = (std::getenv("MTSGPU_NO_BSDF_SETS") || !(extent < 32768.0f) || P->strict_normals) ? 0u
                  : (ggx ? (uint32_t)MTSG_FEAT_GGX : 0u) | (rc ? 0u : (uint32_t)MTSG_FEAT_NORC) |
                        (rd ? 0u : (uint32_t)MTSG_FEAT_NORD);
+        // envmap-only scenes (no area light, no constant emitter): the set kernels without
+        // refN (MTSG_FEAT_NOREFN, dpath.h PathShader::REFN)
+        bool envOnly = H.env.emitter >= 0 && !H.env.constant && !std::getenv("MTSGPU_NO_REFN_SPEC");
+        for (const MtsgEmitter &em : H.emitters) envOnly &= em.type == MTSG_EMITTER_ENVMAP;
+        if (L.bset && envOnly) L.bset |= (uint32_t)MTSG_FEAT_NOREFN;
     }
     // MIDirectIntegrator::configure / configureSampler (direct.cpp:128-143)
     L.integrator = P->integrator;
@@ -754,11 +759,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             budget = std::min<size_t>(freeB / 4 + ctx->contrib.bytes, (size_t)32 << 30);
     }
     if (const char *env = std::getenv("MTSGPU_CONTRIB_BYTES")) budget = std::max<size_t>(std::strtoull(env, nullptr, 10), 1 << 20);
-    const size_t perSample = (size_t)L.num_pixels * (L.gather ? 5 : 4) * 4;   // float4 (+ sy) per sample
+    const size_t perSample = (size_t)L.num_pixels * (L.gather ? 32 : 16);   // one (gather mode: two) float4 per sample
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));
     const size_t filmFloats = (size_t)L.fw * L.fh * 5;
     if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||
-        (e = ctx->counters.ensure(16 * 8)) != hipSuccess || (e = ctx->contrib.ensure(perSample * chunk)) != hipSuccess)
+        (e = ctx->counters.ensure(16 * 8)) != hipSuccess || (e = ctx->contrib.ensure(perSample * (chunk + (chunk & 1)))) != hipSuccess)
         return hip_fail(ctx, e, "film allocation");
     float *own = film_dev ? film_dev : (float *)ctx->film_own.p;
     const size_t nsamp = samples_host ? (size_t)P->width * P->height * P->spp * MTSGPU_SAMPLE_RECORD_FLOATS : 0;
@@ -774,7 +779,6 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     L.film_spill = (float *)ctx->film_spill.p;
     L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
     L.contrib = (float *)ctx->contrib.p;
-    L.contrib_y = L.gather ? L.contrib + (size_t)4 * chunk * L.num_pixels : nullptr;
     unsigned long long *cnt = (unsigned long long *)ctx->counters.p;
     L.counters = cnt;
 
@@ -904,14 +908,16 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     std::memcpy(ctx->last_counters, hc, sizeof hc);
     // counter 15: which kernel ran -- for the megakernel path_kernel<INSTR, SCENE_LDS, FEAT, WAVES>:
     // FEAT's low 8 bits | WAVES << 8 | SCENE_LDS << 12 | INSTR << 13 | (FEAT & NOSTRICT) << 14 (the
-    // set kernels' strictNormals-free build); 1 << 16 for the wavefront engine (tests and A/B logs read it)
+    // set kernels' strictNormals-free build) | (FEAT & NOREFN) << 15; 1 << 16 for the wavefront engine
+    // (tests and A/B logs read it)
     if (wave) {
         ctx->last_counters[15] = 1ull << 16;
     } else {
         const int v = mtsg_path_variant(L);
         ctx->last_counters[15] = (unsigned long long)((v & 0xff) | (int)(L.waves << 8) | (int)(L.scene_lds << 12) |
                                                       ((nsamp != 0 || stats_mode) ? 1 << 13 : 0) |
-                                                      ((v & MTSG_FEAT_NOSTRICT) ? 1 << 14 : 0));
+                                                      ((v & MTSG_FEAT_NOSTRICT) ? 1 << 14 : 0) |
+                                                      ((v & MTSG_FEAT_NOREFN) ? 1 << 15 : 0));
     }
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);

@@ -893,8 +893,22 @@ __device__ __forceinline__ bool film_splat(const MtsgLaunch &L, int px, int py, 
 // the own-pixel weight w (alpha in {0,1} in its sign bit; film_reduce re-forms
 // weight * value[k]) and the rare neighbour splats as atomics.  Gather mode: the
 // sample's value and film position, {L.rgb, sx (alpha in its sign bit: sx >= +0)}
-// and sy (-1: an invalid sample, which ImageBlock::put drops whole); film_gather
-// forms every footprint weight from them with film_splat's arithmetic.
+// and {sy (-1: an invalid sample, which ImageBlock::put drops whole), 0, 0, 0} in one
+// 32 B record: HBM writes whole 32 B sectors (profiles/r06_write_gran), so the
+// record costs what a lone 16 B store costs, where a separate 4 B sy array cost
+// another sector; film_gather forms every footprint weight with film_splat's arithmetic.
+#ifndef MTSG_SPLAT_PAIR
+#define MTSG_SPLAT_PAIR 1
+#endif
+// the record slot of sample jj (= j - j0) of compact pixel pix.  Box filter: the records
+// of samples 2k and 2k+1 of a pixel share one 32 B sector (the lanes that write them
+// run at different times; the sector is written to HBM once if both halves meet in L2).
+// Gather mode: one 32 B record per slot.
+__device__ __forceinline__ size_t film_slot(const MtsgLaunch &L, uint32_t jj, uint32_t pix) {
+    if (MTSG_SPLAT_PAIR && !L.gather) return ((size_t)(jj >> 1) * L.num_pixels + pix) * 2 + (jj & 1);
+    return (size_t)jj * L.num_pixels + pix;
+}
+
 __device__ __forceinline__ void film_record(const MtsgLaunch &L, size_t slot, int px, int py, float sx, float sy,
                                             const float *val, bool alpha) {
     float4 rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -904,11 +918,13 @@ __device__ __forceinline__ void film_record(const MtsgLaunch &L, size_t slot, in
         for (int i = 0; i < 3; ++i)
             if (!isfinite(val[i]) || val[i] < 0) valid = false;   // (alpha and 1 are valid)
         if (valid) rec4 = make_float4(val[0], val[1], val[2], alpha ? sx : -sx);
-        L.contrib_y[slot] = valid ? sy : -1.0f;
-    } else {
-        float ownW = 0.0f;
-        if (film_splat(L, px, py, sx, sy, val, ownW)) rec4 = make_float4(val[0], val[1], val[2], alpha ? ownW : -ownW);
+        float4 *r = reinterpret_cast<float4 *>(L.contrib) + 2 * slot;
+        r[0] = rec4;
+        r[1] = make_float4(valid ? sy : -1.0f, 0.0f, 0.0f, 0.0f);
+        return;
     }
+    float ownW = 0.0f;
+    if (film_splat(L, px, py, sx, sy, val, ownW)) rec4 = make_float4(val[0], val[1], val[2], alpha ? ownW : -ownW);
     reinterpret_cast<float4 *>(L.contrib)[slot] = rec4;
 }
 
@@ -1212,6 +1228,11 @@ struct PathShader {
     // the BSDF-set megakernels are built without strictNormals (the geometric normal
     // is then dead once the hit is formed); scenes with it run the generic kernel
     static constexpr bool NOSTRICT = (FEAT & MTSG_FEAT_NOSTRICT) != 0;
+    // REFN false (MTSG_FEAT_NOREFN, capi.cpp): the scene's only emitter is a non-constant
+    // envmap, whose sampleDirect / pdfDirect do not read refN (envmap.cpp:516-556): the area
+    // light and constant-emitter code is compiled out and refN (three floats live across the
+    // NEE and BSDF calls and the next traversal) is not kept
+    static constexpr bool REFN = (FEAT & MTSG_FEAT_NOREFN) == 0;
     const MtsgLaunch &L;
     const HitSrc<SCENE_LDS> &hs;
     const SobolCtx &SC;
@@ -1322,15 +1343,16 @@ struct PathShader {
                 // missed: the environment emitter, if any (path.cpp:233-247)
                 if (ENV && !(L.hide_emitters && !P.scattered)) {
                     glb_env *E = (glb_env *)S.env;
+                    const bool cst = REFN && E->constant;
                     EnvValPdf vp = {mk(0, 0, 0), 0.0f};
-                    if (!E->constant) vp = env_eval_pdf_at(E, env_uv(E, rd));   // one (u, v) and texel set for both
-                    const f3 value = E->constant ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : vp.value;
+                    if (!cst) vp = env_eval_pdf_at(E, env_uv(E, rd));   // one (u, v) and texel set for both
+                    const f3 value = cst ? mk(E->radiance[0], E->radiance[1], E->radiance[2]) : vp.value;
                     float nT, fT;
                     // EnvironmentMap::fillDirectSamplingRecord (envmap.cpp:358-374)
                     if (env_bsphere(E, ro, rd, nT, fT) && !(nT > 0 || fT < 0)) {
                         float lumPdf = 0;
                         if (!PV_DELTA(P))   // pdfDirect (envmap.cpp:545-556) x pdfEmitterDiscrete
-                            lumPdf = (E->constant ? const_pdf_direct(rd, P.refN) : vp.pdf) *
+                            lumPdf = (cst ? const_pdf_direct(rd, P.refN) : vp.pdf) *
                                      (S.emitters[S.env_emitter].weight * S.em_norm);
                         const float a2 = P.bsdfPdf * P.bsdfPdf, b2 = lumPdf * lumPdf;
                         P.L = add(P.L, mul(mulv(P.thr, value), a2 / (a2 + b2)));
@@ -1341,7 +1363,7 @@ struct PathShader {
                 endPath = true;   // !its.isValid(): break after the environment term
             } else if constexpr (HITK != 2) {
                 auto &sh = hs.shapes[P.its.shape];
-                if (sh.emitter >= 0) {
+                if (REFN && sh.emitter >= 0) {
                     const f3 value = area_Le(S, P.its, neg(rd));
                     float lumPdf = 0;
                     if (!PV_DELTA(P)) {
@@ -1394,7 +1416,7 @@ struct PathShader {
                     rxd = add(rd, mul(sub(rxd, rd), L.diff_scale));   // RayDifferential::scaleDifferential (ray.h:163-168)
                     ryd = add(rd, mul(sub(ryd, rd), L.diff_scale));
                     glb_env *E = (glb_env *)S.env;
-                    if (E->constant) {   // ConstantBackgroundEmitter::evalEnvironment (constant.cpp:241-243)
+                    if (REFN && E->constant) {   // ConstantBackgroundEmitter::evalEnvironment (constant.cpp:241-243)
                         P.L = add(P.L, mulv(P.thr, mk(E->radiance[0], E->radiance[1], E->radiance[2])));
                     } else {
                     P.L = add(P.L, mulv(P.thr, env_eval_diff(E, rd, rxd, ryd)));
@@ -1420,7 +1442,7 @@ struct PathShader {
                     }
                     return rpc;
                 };
-                if (sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
+                if (REFN && sh.emitter >= 0 && P.emitted && (!L.hide_emitters || P.scattered))
                     P.L = add(P.L, mulv(P.thr, area_Le(S, P.its, neg(rd))));
                 // volpath.cpp:214-221 stops only for a strictly negative -dot(geoN, d) * cosTheta(wi)
                 const float snp = dot(rd, P.its.geoN) * P.its.wi.z;
@@ -1428,7 +1450,8 @@ struct PathShader {
                     (!NOSTRICT && L.strict_normals && (L.integrator == MTSG_INTEGRATOR_VOLPATH ? snp > 0 : snp >= 0))) {
                     endPath = true;
                 } else {
-                    P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
+                    if constexpr (REFN)
+                        P.refN = (bsdf.flags & (MTSG_F_TRANSMISSION | MTSG_F_BACK)) == 0 ? P.its.sh.n : mk(0, 0, 0);
                     if (bsdf.flags & MTSG_F_SMOOTH) {
                         // Scene::sampleEmitterDirect (scene.cpp:828-852)
                         float ex, ey;
@@ -1441,13 +1464,14 @@ struct PathShader {
                         float pdf = 0.0f, dist = 0.0f;
                         f3 vlp = mk(0, 0, 0);   // dRec.p where it does not define dRec.d exactly (volpath)
                         bool vrecomp = false;
-                        if (ENV && e.type != MTSG_EMITTER_AREA) {
+                        if (ENV && (!REFN || e.type != MTSG_EMITTER_AREA)) {
                             glb_env *E = (glb_env *)S.env;
-                            const EnvSample es = E->constant ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
-                                                             : env_sample_direct(E, P.its.p, ex, ey);
+                            const EnvSample es = (REFN && E->constant) ? const_sample_direct(E, P.its.p, P.refN, ex, ey)
+                                                                       : env_sample_direct(E, P.its.p, ex, ey);
                             value = es.value; dd = es.d; dist = es.dist; pdf = es.pdf;
                             vlp = add(P.its.p, mul(dd, dist));   // dRec.p = ray(farT) (envmap.cpp:536, constant.cpp:254)
                             vrecomp = true;
+                        } else if constexpr (!REFN) {
                         } else if (ANA && S.shapes[e.shape].analytic >= 0) {
                             const AnaSample as =
                                 ana_sample_direct(((GAna *)S.analytic)[S.shapes[e.shape].analytic], P.its.p, ex, ey);
@@ -1593,7 +1617,7 @@ struct PathShader {
         // film_reduce re-forms weight * value[k] -- the same products
         const float alpha = P.alpha ? 1.0f : 0.0f;
         const float val[5] = {P.L.x, P.L.y, P.L.z, alpha, 1.0f};
-        film_record(L, (size_t)(j - L.j0) * L.num_pixels + pix, px, py, sx, sy, val, P.alpha);
+        film_record(L, film_slot(L, j - L.j0, pix), px, py, sx, sy, val, P.alpha);
         if (INSTR && L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;

@@ -107,7 +107,9 @@ enum { MTSG_FEAT_ENV = 1, MTSG_FEAT_EXT = 2, MTSG_FEAT_ANA = 4,
        // BSDF uses GGX / no roughdielectric / no roughconductor in the scene
        MTSG_FEAT_GGX = 16, MTSG_FEAT_NORD = 32, MTSG_FEAT_NORC = 64,
        MTSG_FEAT_INL = 128,     // microfacet / Fresnel helpers inline (the wavefront per-type kernels)
-       MTSG_FEAT_NOSTRICT = 256 };   // megakernel BSDF-set variants: strictNormals off (capi.cpp picks the generic kernel otherwise)
+       MTSG_FEAT_NOSTRICT = 256,     // megakernel BSDF-set variants: strictNormals off (capi.cpp picks the generic kernel otherwise)
+       MTSG_FEAT_NOREFN = 512 };     // BSDF-set variants of scenes lit by a (non-constant) envmap alone: no area
+                                     // light and no constant emitter, so DirectSamplingRecord::refN is never read
 enum { MTSG_INTEGRATOR_PATH = 0, MTSG_INTEGRATOR_DIRECT = 1, MTSG_INTEGRATOR_VOLPATH = 2 };   // = MTSGPU_INTEGRATOR_*
 enum { MTSG_SAMPLER_SOBOL = 0, MTSG_SAMPLER_INDEPENDENT = 1, MTSG_SAMPLER_SFMT_REPLAY = 2,
        MTSG_SAMPLER_SFMT_BLOCKS = 3 };    // = MTSGPU_SAMPLER_*
@@ -319,9 +321,10 @@ struct MtsgLaunch {
     uint32_t replay, units;
     const uint32_t *order, *unit_start;
     uint32_t *sfmt;
-    float *contrib;                   // [chunk_spp][num_pixels] float4 per sample: box filter {L.rgb, own-pixel
-                                      // weight, alpha in its sign}; gather mode {L.rgb, sx, alpha in its sign}
-    float *contrib_y;                 // gather mode: [chunk_spp][num_pixels] sy (negative: invalid sample)
+    float *contrib;                   // the samples' splat records, slot (j - j0) * num_pixels + pix (film_slot):
+                                      // box filter one float4 {L.rgb, own-pixel weight, alpha in its sign};
+                                      // gather mode two, one 32 B sector: {L.rgb, sx (alpha in its sign)},
+                                      // {sy (negative: an invalid sample), 0, 0, 0}
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction), or the gathered film
     float *film_spill;                // fw*fh*5: splats into other pixels (atomics; box filter only)
     // gather mode (filters whose footprint covers neighbours, e.g. gaussian): the kernels store

@@ -5,7 +5,9 @@
 // Per set: the generic kernel (every BSDF, virtual-dispatch order of
 // path.cpp:171-211), for all-diffuse small scenes (PATH_FEAT 0) the DIFF
 // kernel, and the 7 BSDF-set specialisations of large scenes (dbsdf.h BSet):
-// bits = {every rough BSDF is GGX, no roughdielectric, no roughconductor}.
+// bits = {every rough BSDF is GGX, no roughdielectric, no roughconductor};
+// with an environment emitter also the 7 sets of envmap-only scenes (bit 3,
+// MTSG_FEAT_NOREFN: no area light, no constant emitter).
 // The set kernels are compiled without strictNormals (MTSG_FEAT_NOSTRICT).
 #include "dmega.h"
 
@@ -15,7 +17,8 @@
 namespace {
 constexpr int spec_feat(int bits) {
     return PATH_FEAT | (int)MTSG_FEAT_NOSTRICT | ((bits & 1) ? (int)MTSG_FEAT_GGX : 0) |
-           ((bits & 2) ? (int)MTSG_FEAT_NORD : 0) | ((bits & 4) ? (int)MTSG_FEAT_NORC : 0);
+           ((bits & 2) ? (int)MTSG_FEAT_NORD : 0) | ((bits & 4) ? (int)MTSG_FEAT_NORC : 0) |
+           ((bits & 8) ? (int)MTSG_FEAT_NOREFN : 0);
 }
 
 // variants: small scenes (BVH in LDS) run 3 waves/SIMD with 32 Sobol dims in
@@ -65,6 +68,15 @@ hipError_t PF_NAME(mtsg_launch_path_f, PATH_FEAT)(const MtsgLaunch &L, int grid,
         case 5: launch_v<spec_feat(5)>(L, grid, instr, s); break;
         case 6: launch_v<spec_feat(6)>(L, grid, instr, s); break;
         case 7: launch_v<spec_feat(7)>(L, grid, instr, s); break;
+#if PATH_FEAT & 1   // envmap-only scenes (MTSG_FEAT_NOREFN): feature sets with an environment emitter
+        case 9: launch_v<spec_feat(9)>(L, grid, instr, s); break;
+        case 10: launch_v<spec_feat(10)>(L, grid, instr, s); break;
+        case 11: launch_v<spec_feat(11)>(L, grid, instr, s); break;
+        case 12: launch_v<spec_feat(12)>(L, grid, instr, s); break;
+        case 13: launch_v<spec_feat(13)>(L, grid, instr, s); break;
+        case 14: launch_v<spec_feat(14)>(L, grid, instr, s); break;
+        case 15: launch_v<spec_feat(15)>(L, grid, instr, s); break;
+#endif
         default:
 #if PATH_FEAT == 0
             if (L.all_diffuse) { launch_v<MTSG_FEAT_DIFF>(L, grid, instr, s); break; }
@@ -84,6 +96,15 @@ int PF_NAME(mtsg_path_occupancy_f, PATH_FEAT)(const MtsgLaunch &L, int bits, int
         case 5: return occupancy_v<spec_feat(5)>(L, bpc);
         case 6: return occupancy_v<spec_feat(6)>(L, bpc);
         case 7: return occupancy_v<spec_feat(7)>(L, bpc);
+#if PATH_FEAT & 1
+        case 9: return occupancy_v<spec_feat(9)>(L, bpc);
+        case 10: return occupancy_v<spec_feat(10)>(L, bpc);
+        case 11: return occupancy_v<spec_feat(11)>(L, bpc);
+        case 12: return occupancy_v<spec_feat(12)>(L, bpc);
+        case 13: return occupancy_v<spec_feat(13)>(L, bpc);
+        case 14: return occupancy_v<spec_feat(14)>(L, bpc);
+        case 15: return occupancy_v<spec_feat(15)>(L, bpc);
+#endif
         default:
 #if PATH_FEAT == 0
             if (L.all_diffuse) return occupancy_v<MTSG_FEAT_DIFF>(L, bpc);

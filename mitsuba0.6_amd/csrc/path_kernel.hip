@@ -405,7 +405,7 @@ __global__ __launch_bounds__(BLOCK, MTSG_WAVES_PER_EU) void direct_kernel(MtsgLa
         }
         // block->put(samplePos, spec, alpha) (integrator.cpp:184), as path_kernel
         const float val[5] = {Li.x, Li.y, Li.z, alpha, 1.0f};
-        film_record(L, (size_t)(j - L.j0) * L.num_pixels + pix, px, py, sx, sy, val, alpha != 0.0f);
+        film_record(L, film_slot(L, j - L.j0, pix), px, py, sx, sy, val, alpha != 0.0f);
         if (L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
@@ -487,9 +487,9 @@ __global__ void film_reduce(MtsgLaunch L) {
     float acc[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) acc[k] = dst[k];
-    const float4 *c = reinterpret_cast<const float4 *>(L.contrib) + p;
+    const float4 *c = reinterpret_cast<const float4 *>(L.contrib);
     for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
-        const float4 r = c[(size_t)jj * L.num_pixels];
+        const float4 r = c[film_slot(L, jj, p)];
         const float w = fabsf(r.w);
         const float alpha = signbit(r.w) ? 0.0f : 1.0f;
         acc[0] += w * r.x;
@@ -543,6 +543,10 @@ __device__ __forceinline__ long long pix_index(const MtsgLaunch &L, int qx, int 
     return (long long)tile * 64 + in;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+#ifndef MTSG_GATHER_PK
+#define MTSG_GATHER_PK 1
+#endif
 #define GATHER_T 16
 __host__ __device__ constexpr size_t gather_lds_floats(int H) {
     return (size_t)(GATHER_T + 2 * H) * (GATHER_T + 2 * H) * (4 + 2 * (2 * H + 1)) + 32;
@@ -566,17 +570,24 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
     const int sx0 = ox - b - H, sy0 = oy - b - H;
     for (int i = threadIdx.x; i <= MTSG_FILTER_RES; i += 256) fv[i] = F.values[i];
     long long pi[SLOTS];
+    int rendered = 0;
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k) {
         const int s = threadIdx.x + 256 * k;
         pi[k] = s < S ? pix_index(L, sx0 + s % SW, sy0 + s / SW) : -1;
+        rendered |= pi[k] >= 0;
     }
+    // a tile none of whose sources this launch renders (another shard's part of the
+    // window: with N-way tile sharding a rank renders every N-th tile column) keeps
+    // its film values: the whole block leaves before the first barrier
+    if (!__syncthreads_or(rendered)) return;
     float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     float *dst = L.film_own + ((size_t)gy * L.fw + gx) * 5;
     if (live) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) acc[k] = dst[k];   // the previous chunks' running sums
     }
+    f2v a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
     const float4 *rec = reinterpret_cast<const float4 *>(L.contrib);
     for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
         __syncthreads();   // the previous sample's neighbours are summed
@@ -590,8 +601,8 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
             for (int o = 0; o < NW; ++o) wx[o] = wy[o] = 0.0f;
             if (pi[k] >= 0) {
                 const size_t slot = (size_t)jj * L.num_pixels + (size_t)pi[k];
-                const float4 r = rec[slot];
-                const float sy = L.contrib_y[slot];
+                const float4 r = rec[2 * slot];
+                const float sy = rec[2 * slot + 1].x;
                 if (!signbit(sy)) {
                     const int qx = sx0 + s % SW, qy = sy0 + s / SW;
                     const float sx = fabsf(r.w);
@@ -624,7 +635,9 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
         }
         __syncthreads();
         if (live) {
-            // neighbour d = (dx, dy): source q at film position g + d; g sits at offset -d from it
+            // neighbour d = (dx, dy): source q at film position g + d; g sits at offset -d from it.
+            // The four value channels as two packed pairs (v_pk_mul_f32 + v_pk_add_f32: each half
+            // the IEEE product and sum of its own channel, one instruction for two)
 #pragma unroll
             for (int dy = -H; dy <= H; ++dy) {
 #pragma unroll
@@ -632,16 +645,23 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
                     const int s = (ty + H + dy) * SW + (tx + H + dx);
                     const float w = wxs[(H - dx) * S + s] * wys[(H - dy) * S + s];
                     const float4 v = val[s];
-                    acc[0] += w * v.x;
-                    acc[1] += w * v.y;
-                    acc[2] += w * v.z;
-                    acc[3] += w * v.w;
+#if MTSG_GATHER_PK
+                    const f2v ww = {w, w};
+                    a01 += ww * f2v{v.x, v.y};
+                    a23 += ww * f2v{v.z, v.w};
+#else
+                    a01.x += w * v.x;
+                    a01.y += w * v.y;
+                    a23.x += w * v.z;
+                    a23.y += w * v.w;
+#endif
                     acc[4] += w * 1.0f;
                 }
             }
         }
     }
     if (live) {
+        acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
 #pragma unroll
         for (int k = 0; k < 5; ++k) dst[k] = acc[k];
     }
@@ -708,7 +728,8 @@ int mtsg_path_features(const MtsgLaunch &L) {
 // small scenes staged in LDS and the direct integrator take the generic kernel.
 static int spec_bits(const MtsgLaunch &L) {
     if (L.scene_lds || L.integrator == MTSG_INTEGRATOR_DIRECT) return 0;
-    return ((L.bset & MTSG_FEAT_GGX) ? 1 : 0) | ((L.bset & MTSG_FEAT_NORD) ? 2 : 0) | ((L.bset & MTSG_FEAT_NORC) ? 4 : 0);
+    const int b = ((L.bset & MTSG_FEAT_GGX) ? 1 : 0) | ((L.bset & MTSG_FEAT_NORD) ? 2 : 0) | ((L.bset & MTSG_FEAT_NORC) ? 4 : 0);
+    return b | ((b && (L.bset & MTSG_FEAT_NOREFN) && (mtsg_path_features(L) & MTSG_FEAT_ENV)) ? 8 : 0);
 }
 
 template <int FEAT>
@@ -816,7 +837,7 @@ hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, i
 int mtsg_path_variant(const MtsgLaunch &L) {
     const int bits = spec_bits(L), f = mtsg_path_features(L);
     if (bits) return f | MTSG_FEAT_NOSTRICT | ((bits & 1) ? MTSG_FEAT_GGX : 0) | ((bits & 2) ? MTSG_FEAT_NORD : 0) |
-                     ((bits & 4) ? MTSG_FEAT_NORC : 0);
+                     ((bits & 4) ? MTSG_FEAT_NORC : 0) | ((bits & 8) ? MTSG_FEAT_NOREFN : 0);
     return (f == 0 && L.all_diffuse) ? (int)MTSG_FEAT_DIFF : f;
 }
 

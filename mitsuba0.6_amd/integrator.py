@@ -194,7 +194,7 @@ class Context:
         c = self.debug_counters()[15]
         if c & (1 << 16):
             return None
-        feat = (c & 0xff) | (256 if c & (1 << 14) else 0)
+        feat = (c & 0xff) | (256 if c & (1 << 14) else 0) | (512 if c & (1 << 15) else 0)
         instr, lds, waves = bool(c & (1 << 13)), bool(c & (1 << 12)), (c >> 8) & 0xf
         b = lambda v: 'true' if v else 'false'
         return {'instr': instr, 'scene_lds': lds, 'feat': feat, 'waves': waves,

@@ -41,8 +41,8 @@ THREADS = min(16, os.cpu_count() or 1)
 BANDS = {'C2': (352, 16), 'C3': (356, 8), 'C4': (300, 4), 'C5': (360, 4), 'C2g': (360, 16)}
 KERNELS = {'C1': 'path_kernel<false, true, 8, 4>', 'C2': 'path_kernel<false, true, 8, 4>',
            'C2g': 'path_kernel<false, true, 8, 4>',
-           'C3': 'path_kernel<false, false, 305, 4>', 'C4': 'path_kernel<false, false, 336, 4>',
-           'C5': 'path_kernel<false, false, 371, 4>'}
+           'C3': 'path_kernel<false, false, 817, 4>', 'C4': 'path_kernel<false, false, 336, 4>',
+           'C5': 'path_kernel<false, false, 883, 4>'}
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 

@@ -7,3 +7,5 @@ template __global__ void path_kernel<false, true, 8, 4>(MtsgLaunch);
 template __global__ void path_kernel<false, false, 49 | 256, 4>(MtsgLaunch);
 template __global__ void path_kernel<false, false, 80 | 256, 4>(MtsgLaunch);
 template __global__ void path_kernel<false, false, 115 | 256, 4>(MtsgLaunch);
+template __global__ void path_kernel<false, false, 115 | 256 | 512, 4>(MtsgLaunch);
+template __global__ void path_kernel<false, false, 49 | 256 | 512, 4>(MtsgLaunch);

@@ -18,7 +18,7 @@ stride = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 engine = sys.argv[4] if len(sys.argv) > 4 else None
 # C2g: C2 with the gaussian filter (bench.py's secondary block)
 sc, it = scenes.build(cfg.rstrip('g'), rfilter='gaussian' if cfg.endswith('g') else 'box')
-ctx = Context(0)
+ctx = Context(0, lib_path=os.environ.get('PROF_LIB'))   # PROF_LIB: a variant build (A/B traffic passes)
 ctx.upload(sc)
 print('scene', ctx.scene_info())
 for f in range(frames):
