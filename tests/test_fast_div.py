@@ -12,7 +12,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_fast_division_matches_ieee(tmp_path):
     exe = tmp_path / 'fdc'
     subprocess.run(['gcc', '-O2', '-ffp-contract=off', '-mfma', '-o', str(exe),
-                    os.path.join(REPO, 'tools', 'r05', 'fast_div_check.c'), '-lm'], check=True)
+                    os.path.join(REPO, 'tools', 'gpu_runs', 'r05', 'fast_div_check.c'), '-lm'], check=True)
     out = subprocess.run([str(exe), '4000000'], check=True, capture_output=True, text=True).stdout
     last = out.strip().splitlines()[-1].split()
     assert last[0] == 'checked' and int(last[1]) > 3_000_000
