@@ -25,7 +25,7 @@
 hipError_t mtsg_launch_path(const MtsgLaunch &L, int grid, bool samples, bool stats, hipStream_t stream);
 hipError_t mtsg_launch_gather(const MtsgLaunch &L, hipStream_t stream);
 hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream);
-hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream);
+hipError_t mtsg_launch_finalize(float *own, const double *spill, size_t n, hipStream_t stream);
 hipError_t mtsg_launch_arith_probe(const float *a, const float *b, float *out, int n, hipStream_t stream);
 hipError_t mtsg_launch_libm_probe(int fn, const float *a, const float *b, float *out, size_t n, uint32_t first,
                                   hipStream_t s);
@@ -734,6 +734,10 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         const int w = std::atoi(env);
         L.waves = w == 4 ? 4u : 3u;
     }
+    // megakernel sample runs (dmega.h): 2^round_shift samples of a pixel per lane in a row
+    // (1: pairs, whose box records share a 32 B sector; profiles/r06_ab_rounds_*.log)
+    L.round_shift = MTSG_ROUND_SHIFT;
+    if (const char *env = std::getenv("MTSGPU_ROUND_SHIFT")) L.round_shift = (uint32_t)std::min(6, std::max(0, std::atoi(env)));
     // gather mode (film_gather, path_kernel.hip): filters whose footprint covers the
     // neighbours (gaussian) -- every film pixel sums its neighbourhood's sample records in
     // a fixed order instead of taking atomic splats.  H = the largest footprint offset from a
@@ -762,7 +766,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
     const size_t perSample = (size_t)L.num_pixels * (L.gather ? 32 : 16);   // one (gather mode: two) float4 per sample
     const uint32_t chunk = (uint32_t)std::max<size_t>(1, std::min<size_t>(P->spp, budget / perSample));
     const size_t filmFloats = (size_t)L.fw * L.fh * 5;
-    if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 4)) != hipSuccess ||
+    if ((e = ctx->film_own.ensure(filmFloats * 4)) != hipSuccess || (e = ctx->film_spill.ensure(filmFloats * 8)) != hipSuccess ||
         (e = ctx->counters.ensure(16 * 8)) != hipSuccess || (e = ctx->contrib.ensure(perSample * (chunk + (chunk & 1)))) != hipSuccess)
         return hip_fail(ctx, e, "film allocation");
     float *own = film_dev ? film_dev : (float *)ctx->film_own.p;
@@ -772,11 +776,11 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         if ((e = hipMemsetAsync(ctx->samples.p, 0, nsamp * 4, stream)) != hipSuccess) return hip_fail(ctx, e, "memset");
     }
     if ((e = hipMemsetAsync(own, 0, filmFloats * 4, stream)) != hipSuccess ||
-        (e = hipMemsetAsync(ctx->film_spill.p, 0, filmFloats * 4, stream)) != hipSuccess ||
+        (e = hipMemsetAsync(ctx->film_spill.p, 0, filmFloats * 8, stream)) != hipSuccess ||
         (e = hipMemsetAsync(ctx->counters.p, 0, 16 * 8, stream)) != hipSuccess)
         return hip_fail(ctx, e, "memset");
     L.film_own = own;
-    L.film_spill = (float *)ctx->film_spill.p;
+    L.film_spill = (double *)ctx->film_spill.p;
     L.samples = nsamp ? (float *)ctx->samples.p : nullptr;
     L.contrib = (float *)ctx->contrib.p;
     unsigned long long *cnt = (unsigned long long *)ctx->counters.p;

@@ -3,8 +3,9 @@
 // SamplingIntegrator::renderBlock, src/librender/integrator.cpp:140-188),
 // instantiated per scene feature set in path_f.hip:
 //
-//  * lane g of the persistent grid takes items g, g + lanes, g + 2 lanes, ...
-//    (static striding: no queue, no tail of long per-pixel tasks);
+//  * lane g of the persistent grid takes sample runs g, g + lanes, g + 2 lanes, ...
+//    (static striding: no queue, no tail of long per-pixel tasks), a run being
+//    2^round_shift consecutive samples of one pixel, one after the other;
 //  * a lane whose path ends starts its next item immediately (regeneration);
 //  * each loop iteration traces the lane's pending shadow ray and its
 //    closest-hit ray, then shades (PathShader, dpath.h);
@@ -47,9 +48,9 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     PathCounters c = {};   // INSTR statistics only: the always-on counts are wave-uniform (wc)
     WaveCounters wc = {};
 
-    // static striding: lane g takes items g + k * lanes, k = 0, 1, ... (`round` is
-    // k, or the SFMT replay's position in its unit: 32 bits, not a 64-bit item
-    // index, live across the bounce loop)
+    // static striding: lane g takes sample runs g + k * lanes, k = 0, 1, ... (`round`
+    // counts the lane's samples, or the SFMT replay's position in its unit: 32 bits,
+    // not a 64-bit item index, live across the bounce loop)
     const uint64_t lanes = (uint64_t)gridDim.x * BLOCK;
     const uint32_t g = xcd_block(L.xcds) * BLOCK + threadIdx.x;
     uint32_t round = 0;
@@ -91,10 +92,17 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
                 sh.start_xy(st, L.order[k], jj);
                 break;
             }
-            const uint64_t it = g + (uint64_t)round * lanes;
-            if (it >= L.num_items) { done = true; break; }
+            // sample runs: the lane's rounds r * 2^s .. r * 2^s + 2^s - 1 render samples
+            // k * 2^s .. of one pixel back to back (run q = g + r * lanes; s = L.round_shift):
+            // a box-filter record sector (film_slot: samples 2k, 2k + 1) has both halves
+            // stored one path apart, while the line is still in this XCD's L2, and the
+            // wave's primary rays revisit the same pixels
+            const uint32_t rs = L.round_shift;
+            const uint64_t q = g + (uint64_t)(round >> rs) * lanes;
+            const uint32_t jq = (uint32_t)(q / L.num_pixels), jr = jq << rs, jj = jr + (round & ((1u << rs) - 1u));
+            if (jr >= L.chunk_spp) { done = true; break; }
             ++round;
-            sh.start(st, it);
+            if (jj < L.chunk_spp) sh.start_jp(st, jj, (uint32_t)(q - (uint64_t)jq * L.num_pixels));
         }
         if (__all(done)) break;
         MK_STAMP(mkT[0], mkT0);

@@ -846,7 +846,7 @@ __device__ __forceinline__ uint32_t dd_sample_reuse(const float *__restrict__ cd
 // ---------------------------------------------------------------------------
 // film splat: ImageBlock::put (render/imageblock.h:124-204) into the 32x32
 // block that owns pixel (px, py); own-pixel weight goes to the lane's
-// registers, other touched pixels to the spill film (atomics)
+// registers, other touched pixels to the spill film (double atomics)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float filter_disc(const MtsgFilter &F, float x) {
     int i = (int)fabsf(x * F.scale);
@@ -879,9 +879,12 @@ __device__ __forceinline__ bool film_splat(const MtsgLaunch &L, int px, int py, 
             if (gx == px + b && gy == py + b) {
                 ownW = weight;
             } else {
-                float *dst = L.film_spill + ((size_t)gy * L.fw + gx) * 5;
+                // weight * value[k] in float as the reference forms it, summed in double:
+                // exact for contributions within 2^29 of each other, so the spill film
+                // does not depend on the order the atomics land (film_finalize rounds once)
+                double *dst = L.film_spill + ((size_t)gy * L.fw + gx) * 5;
 #pragma unroll
-                for (int k = 0; k < 5; ++k) atomicAdd(dst + k, weight * val[k]);
+                for (int k = 0; k < 5; ++k) atomicAdd(dst + k, (double)(weight * val[k]));
             }
         }
     }
@@ -1243,7 +1246,11 @@ struct PathShader {
     // (integrator.cpp:165-186, path.cpp:119-133); false for a padding pixel
     __device__ __forceinline__ bool start(PathState &st, uint64_t it) const {
         const uint32_t jj = (uint32_t)(it / L.num_pixels);
-        st.pix = (uint32_t)(it - (uint64_t)jj * L.num_pixels);
+        return start_jp(st, jj, (uint32_t)(it - (uint64_t)jj * L.num_pixels));
+    }
+    // sample jj of the chunk at compact pixel pix
+    __device__ __forceinline__ bool start_jp(PathState &st, uint32_t jj, uint32_t pix) const {
+        st.pix = pix;
         int px, py;
         if (!pixel_of(L, st.pix, px, py)) return false;
         begin(st, jj, px, py);

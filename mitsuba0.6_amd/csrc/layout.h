@@ -284,6 +284,7 @@ struct MtsgLaunch {
     uint32_t tiles_x;                 // 8x8 pixel tiles across the window
     uint32_t num_pixels;              // compact pixels incl. padding of partial tiles
     uint32_t j0, chunk_spp;
+    uint32_t round_shift;             // megakernel: a lane renders 2^round_shift samples of a pixel in a row (dmega.h)
     uint64_t num_items;
     // Sobol direction numbers as 4-bit lookup tables: nib[dim][c][v] = XOR of the
     // columns 4c..4c+3 selected by v (same product as sobolseq.h:43-57)
@@ -326,7 +327,8 @@ struct MtsgLaunch {
                                       // gather mode two, one 32 B sector: {L.rgb, sx (alpha in its sign)},
                                       // {sy (negative: an invalid sample), 0, 0, 0}
     float *film_own;                  // fw*fh*5: own-pixel sums (ordered reduction), or the gathered film
-    float *film_spill;                // fw*fh*5: splats into other pixels (atomics; box filter only)
+    double *film_spill;               // fw*fh*5: splats into other pixels (box filter only), double atomics:
+                                      // a pixel's few neighbour splats sum exactly, in any order (dpath.h film_splat)
     // gather mode (filters whose footprint covers neighbours, e.g. gaussian): the kernels store
     // each sample's value and position; film_gather<H> forms every pixel's sum in a fixed order
     uint32_t gather;                  // 1: gather mode
@@ -335,5 +337,9 @@ struct MtsgLaunch {
     unsigned long long *counters;     // [0] samples [1] rays [2] shadow [3] pathlen [4] nodes [5] tests
                                       // [6] dim errors [7] hits [9] nee [10] sobol words
 };
+
+#ifndef MTSG_ROUND_SHIFT
+#define MTSG_ROUND_SHIFT 1
+#endif
 
 #define MTSG_NIBBLES 13

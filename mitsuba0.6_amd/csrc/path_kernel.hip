@@ -667,9 +667,9 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
     }
 }
 
-__global__ void film_finalize(float *__restrict__ own, const float *__restrict__ spill, size_t n) {
+__global__ void film_finalize(float *__restrict__ own, const double *__restrict__ spill, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) own[i] += spill[i];
+    if (i < n) own[i] += (float)spill[i];
 }
 
 // the device's SFMT19937 stream: n nextULong draws from the stream at w (one lane)
@@ -789,7 +789,7 @@ hipError_t mtsg_launch_gather(const MtsgLaunch &L, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t mtsg_launch_finalize(float *own, const float *spill, size_t n, hipStream_t stream) {
+hipError_t mtsg_launch_finalize(float *own, const double *spill, size_t n, hipStream_t stream) {
     const int threads = 256;
     const int blocks = (int)((n + threads - 1) / threads);
     if (blocks > 0) hipLaunchKernelGGL(film_finalize, dim3(blocks), dim3(threads), 0, stream, own, spill, n);

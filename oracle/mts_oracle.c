@@ -3565,7 +3565,7 @@ static inline float filter_eval_disc(const Filter *f, float x) {
 /* splat into the 32x32 block that renders pixel (px,py); own-pixel weight goes
  * to `own`, every other touched pixel to `spill` (film layout, border b) */
 static int film_put(const Filter *f, int W, int H, int px, int py, float sx, float sy,
-                    const float *val5, float *own, float *spill, int fw, int fh) {
+                    const float *val5, float *own, double *spill, int fw, int fh) {
     for (int i = 0; i < 5; ++i)
         if (!isfinite(val5[i]) || val5[i] < 0) return 0;
     const int b = f->border;
@@ -3590,13 +3590,15 @@ static int film_put(const Filter *f, int W, int H, int px, int py, float sx, flo
             int gx = x + bx, gy = y + by; /* film coordinates (border included) */
             if (gx >= fw || gy >= fh) continue; /* Bitmap::accumulate clips to the film */
             const int isOwn = gx == px + b && gy == py + b;
-            float *dst = (isOwn ? own : spill) + ((size_t)gy * fw + gx) * 5;
             if (isOwn) {
+                float *dst = own + ((size_t)gy * fw + gx) * 5;
                 for (int k = 0; k < 5; ++k) dst[k] += weight * val5[k];
             } else {
-                /* pixels of other tasks: shared between OpenMP threads */
+                /* pixels of other tasks: shared between OpenMP threads.  Summed in double
+                   (the GPU's film_splat): exact, so independent of the order threads land */
+                double *dst = spill + ((size_t)gy * fw + gx) * 5;
                 for (int k = 0; k < 5; ++k) {
-                    const float add = weight * val5[k];
+                    const double add = (double)(weight * val5[k]);
 #ifdef _OPENMP
 #pragma omp atomic
 #endif
@@ -3691,7 +3693,9 @@ typedef struct {
     float diffScale;
     const Filter *F;
     int W, H, fw, fh;
-    float *film, *spill, *samples;
+    float *film;
+    double *spill;   /* neighbour splats, summed in double (film_put) */
+    float *samples;
     GatherRec *recs; /* gather mode: each sample's value and position instead of a splat */
 } RenderCtx;
 
@@ -3791,7 +3795,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
     if (P->x0 + P->width > (uint32_t)W || P->y0 + P->height > (uint32_t)H) { scene_free(&S); return MTSGPU_EINVAL; }
     const int b = F.border, fw = W + 2 * b, fh = H + 2 * b;
     const size_t filmFloats = (size_t)fw * fh * 5;
-    float *spill = (float *)calloc(filmFloats, sizeof(float));
+    double *spill = (double *)calloc(filmFloats, sizeof(double));
     memset(film, 0, filmFloats * sizeof(float));
     PathParams PP = {P->max_depth, P->rr_depth, P->strict_normals, P->hide_emitters, P->has_alpha,
                      P->integrator == MTSGPU_INTEGRATOR_VOLPATH};
@@ -3855,7 +3859,7 @@ int oracle_render(const mtsgpu_scene_desc *scene, const mtsgpu_render_params *P,
         film_gather(&F, P, fw, fh, gh, recs, film);
         free(recs);
     }
-    for (size_t i = 0; i < filmFloats; ++i) film[i] += spill[i];
+    for (size_t i = 0; i < filmFloats; ++i) film[i] += (float)spill[i];
     free(spill);
     if (stats) {
         memset(stats, 0, sizeof *stats);
