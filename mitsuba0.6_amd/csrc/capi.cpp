@@ -565,6 +565,19 @@ static void mtsg_render_order(uint32_t width, uint32_t height, uint32_t bs, std:
     blockStart.push_back((uint32_t)order.size());
 }
 
+// megakernel sample runs (dmega.h): a lane renders 2^s consecutive samples of one pixel, so
+// its wave keeps the same 64 pixels for 2^s paths.  Large scenes: the longest runs that leave
+// every lane MTSG_MIN_RUNS of them (full frame: C3 s = 4 +13%, C5 s = 5 +14% over s = 0; longer
+// runs leave a tail, profiles/r06_rounds/).  Tiny LDS scenes gain nothing: pairs, whose box
+// records share a 32 B sector (film_slot).  MTSGPU_ROUND_SHIFT=s overrides (A/B)
+static uint32_t run_shift(const MtsgLaunch &L, uint64_t lanes) {
+    if (const char *env = std::getenv("MTSGPU_ROUND_SHIFT")) return (uint32_t)std::min(6, std::max(0, std::atoi(env)));
+    uint32_t s = L.scene_lds ? 1u : 6u;
+    const uint64_t perLane = L.num_items / std::max<uint64_t>(1, lanes);
+    while (s > 0 && ((1u << s) > L.chunk_spp || (perLane >> s) < MTSG_MIN_RUNS)) --s;
+    return s;
+}
+
 static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *film_host, float *film_dev,
                        float *samples_host, hipStream_t stream, mtsgpu_stats *stats) {
     if (!ctx || !P) return MTSGPU_EINVAL;
@@ -734,10 +747,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
         const int w = std::atoi(env);
         L.waves = w == 4 ? 4u : 3u;
     }
-    // megakernel sample runs (dmega.h): 2^round_shift samples of a pixel per lane in a row
-    // (1: pairs, whose box records share a 32 B sector; profiles/r06_ab_rounds_*.log)
-    L.round_shift = MTSG_ROUND_SHIFT;
-    if (const char *env = std::getenv("MTSGPU_ROUND_SHIFT")) L.round_shift = (uint32_t)std::min(6, std::max(0, std::atoi(env)));
+    L.round_shift = 0;   // set per chunk (run_shift)
     // gather mode (film_gather, path_kernel.hip): filters whose footprint covers the
     // neighbours (gaussian) -- every film pixel sums its neighbourhood's sample records in
     // a fixed order instead of taking atomic splats.  H = the largest footprint offset from a
@@ -895,6 +905,7 @@ static int render_impl(mtsgpu_ctx *ctx, const mtsgpu_render_params *P, float *fi
             // the replay renders one unit per lane (its own SFMT stream): every unit needs a resident lane
             if (replay && (uint64_t)grid * 256 < L.units)
                 return fail(ctx, MTSGPU_EINVAL, "SFMT replay: more 32x32 blocks than resident lanes (crop too large)");
+            L.round_shift = run_shift(L, (uint64_t)grid * BLOCK_THREADS);
             if ((e = mtsg_launch_path(L, grid, nsamp != 0, stats_mode, stream)) != hipSuccess) return hip_fail(ctx, e, "path kernel launch");
         }
         if ((e = L.gather ? mtsg_launch_gather(L, stream) : mtsg_launch_reduce(L, stream)) != hipSuccess)

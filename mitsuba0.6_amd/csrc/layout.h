@@ -284,7 +284,7 @@ struct MtsgLaunch {
     uint32_t tiles_x;                 // 8x8 pixel tiles across the window
     uint32_t num_pixels;              // compact pixels incl. padding of partial tiles
     uint32_t j0, chunk_spp;
-    uint32_t round_shift;             // megakernel: a lane renders 2^round_shift samples of a pixel in a row (dmega.h)
+    uint32_t round_shift;             // megakernel: a lane renders 2^round_shift samples of a pixel in a row (dmega.h, capi.cpp run_shift)
     uint64_t num_items;
     // Sobol direction numbers as 4-bit lookup tables: nib[dim][c][v] = XOR of the
     // columns 4c..4c+3 selected by v (same product as sobolseq.h:43-57)
@@ -338,8 +338,8 @@ struct MtsgLaunch {
                                       // [6] dim errors [7] hits [9] nee [10] sobol words
 };
 
-#ifndef MTSG_ROUND_SHIFT
-#define MTSG_ROUND_SHIFT 1
+#ifndef MTSG_MIN_RUNS
+#define MTSG_MIN_RUNS 100   // sample runs per lane the megakernel's run length leaves (capi.cpp run_shift)
 #endif
 
 #define MTSG_NIBBLES 13
