@@ -16,6 +16,11 @@
 
 size_t mtsg_path_lds_bytes(const MtsgLaunch &L);   // path_kernel.hip
 
+// tiny-scene kernels keep a pair's first splat record in registers (PathShader::finish)
+#ifndef MTSG_HOLD_PAIR
+#define MTSG_HOLD_PAIR 1
+#endif
+
 // diagnostic build (-DMTSG_MK_STAMPS): wave cycles per megakernel section,
 // summed into counters 11-14 (start, shadow trace, closest trace, shade) by
 // lane 0 of each wave.  s_memtime without draining the memory counters: a
@@ -55,6 +60,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
     const uint32_t g = xcd_block(L.xcds) * BLOCK + threadIdx.x;
     uint32_t round = 0;
     bool done = false;
+    float4 held = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // PathShader::finish's held splat record
     PathState st;
     st.active = false;
     st.pix = 0;
@@ -195,7 +201,7 @@ __global__ __launch_bounds__(BLOCK, WAVES) void path_kernel(MtsgLaunch L) {   //
         bool ended = false;
         if (st.active && sh.shade(st, occluded, hit, slot, prim, hu, hv, ht)) {
             ended = true;
-            sh.template finish<false>(st);
+            sh.template finish<false>(st, MTSG_HOLD_PAIR && SCENE_LDS ? &held : nullptr);
         }
         wc.len += wave_count(was && st.P.depth != d0);
         wc.samples += wave_count(ended);

@@ -1611,8 +1611,11 @@ struct PathShader {
     // block->put(samplePos, spec, alpha) (integrator.cpp:184) and the sample's records
     // LANE_COUNTS: count the sample into c (the wavefront engine); the megakernel
     // counts finished samples per wave instead (WaveCounters)
+    // hold (megakernel, box filter, sample runs of 2 or more): the record of sample 2k is
+    // kept in *hold and stored with sample 2k + 1's, which the same lane renders next, as
+    // one whole 32 B sector (film_slot)
     template <bool LANE_COUNTS = true>
-    __device__ __forceinline__ void finish(PathState &st) const {
+    __device__ __forceinline__ void finish(PathState &st, float4 *hold = nullptr) const {
         PathVars &P = st.P;
         SamplerState &smp = st.smp;
         const uint32_t j = smp.sampleIndex, pix = st.pix;
@@ -1624,7 +1627,24 @@ struct PathShader {
         // film_reduce re-forms weight * value[k] -- the same products
         const float alpha = P.alpha ? 1.0f : 0.0f;
         const float val[5] = {P.L.x, P.L.y, P.L.z, alpha, 1.0f};
-        film_record(L, film_slot(L, j - L.j0, pix), px, py, sx, sy, val, P.alpha);
+        const uint32_t jj = j - L.j0;
+        if (hold && !L.gather && L.round_shift != 0 && MTSG_SPLAT_PAIR) {
+            float ownW = 0.0f;
+            float4 rec4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (film_splat(L, px, py, sx, sy, val, ownW)) rec4 = make_float4(val[0], val[1], val[2], P.alpha ? ownW : -ownW);
+            float4 *c4 = reinterpret_cast<float4 *>(L.contrib);
+            const size_t slot = film_slot(L, jj, pix);
+            if ((jj & 1u) == 0 && jj + 1 < L.chunk_spp) {
+                *hold = rec4;
+            } else if (jj & 1u) {
+                c4[slot - 1] = *hold;
+                c4[slot] = rec4;
+            } else {
+                c4[slot] = rec4;
+            }
+        } else {
+            film_record(L, film_slot(L, jj, pix), px, py, sx, sy, val, P.alpha);
+        }
         if (INSTR && L.samples) {
             const uint32_t pixIdx = (uint32_t)(py - (int)L.y0) * L.width + (uint32_t)(px - (int)L.x0);
             float *rec = L.samples + ((size_t)pixIdx * L.spp + j) * 8;
