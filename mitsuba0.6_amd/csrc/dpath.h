@@ -7,11 +7,13 @@
 // (PathShader), the Sobol / independent samplers, the BVH2 and kd-tree
 // traversals, the hit record and the film splat.
 //
-// Work items are (sample j, pixel p) pairs, j-major, pixels in 8x8 tiles.
-// The own-pixel splat of every sample is stored to HBM ([spp][pixels]) and a
-// second kernel sums each pixel in sample order -- the reference's ImageBlock
-// accumulation order, bit for bit; splats into other pixels (box filter edges,
-// gaussian) go to a spill film with float atomics.  LDS holds the Sobol
+// Work items are (sample j, pixel p) pairs, pixels in 8x8 tiles; the megakernel
+// hands them out as runs of consecutive samples of one pixel (dmega.h).
+// The own-pixel splat of every sample is stored to HBM ([spp][pixels], film_slot)
+// and a second kernel sums each pixel in sample order -- the reference's
+// ImageBlock accumulation order, bit for bit; splats into other pixels (box
+// filter edges) go to a spill film with double atomics, gaussian footprints are
+// gathered per pixel in a fixed order (film_gather).  LDS holds the Sobol
 // direction numbers of the first dimensions as 4-bit lookup tables (8
 // independent reads per 32-bit sample instead of up to 32 dependent ones).
 #pragma once
