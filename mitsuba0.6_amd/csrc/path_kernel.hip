@@ -516,10 +516,11 @@ __global__ void film_reduce(MtsgLaunch L) {
 // renderproc.cpp:142-149); this one replaces the atomic neighbour splats, which
 // had no order at all.
 //
-// One workgroup: a 16x16 tile of film pixels.  Per sample index the tile's
-// (16+2H)^2 source records are staged in LDS together with their per-axis
-// weights towards every offset -H..H (formed once per record, not once per
-// neighbour), then each thread adds its (2H+1)^2 neighbours from LDS.
+// One workgroup: a 16 x 16R tile of film pixels, R = gather_rows(H) vertically
+// adjacent pixels per thread.  Per sample index the tile's (16+2H) x (16R+2H)
+// source records are staged in LDS together with their per-axis weights towards
+// every offset -H..H (formed once per record, not once per neighbour), then each
+// thread adds the (2H+1)^2 neighbours of each of its pixels from LDS.
 // ---------------------------------------------------------------------------
 // the compact pixel index p (work items' pixel, pixel_of's inverse) of image
 // pixel (qx, qy), or -1 when this launch does not render it (outside the
@@ -548,13 +549,22 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 #define MTSG_GATHER_PK 1
 #endif
 #define GATHER_T 16
+// output rows per thread: a thread sums GATHER_ROWS vertically adjacent film pixels, so each
+// staged source record and x weight read from LDS serves up to GATHER_ROWS of its sums
+#ifndef MTSG_GATHER_ROWS
+#define MTSG_GATHER_ROWS 2
+#endif
+// (H = 4 keeps one row: two would need 85 KB of LDS per block)
+__host__ __device__ constexpr int gather_rows(int H) { return H <= 3 ? MTSG_GATHER_ROWS : 1; }
 __host__ __device__ constexpr size_t gather_lds_floats(int H) {
-    return (size_t)(GATHER_T + 2 * H) * (GATHER_T + 2 * H) * (4 + 2 * (2 * H + 1)) + 32;
+    return (size_t)(GATHER_T + 2 * H) * (GATHER_T * gather_rows(H) + 2 * H) * (4 + 2 * (2 * H + 1)) + 32;
 }
 
 template <int H>
 __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy0, int gx1, int gy1) {
-    constexpr int SW = GATHER_T + 2 * H, S = SW * SW, NW = 2 * H + 1, SLOTS = (S + 255) / 256;
+    constexpr int R = gather_rows(H), TY = GATHER_T * R;
+    constexpr int SWX = GATHER_T + 2 * H, SWY = TY + 2 * H, S = SWX * SWY, NW = 2 * H + 1;
+    constexpr int SLOTS = (S + 255) / 256;
     extern __shared__ float glds[];
     float4 *val = reinterpret_cast<float4 *>(glds);   // [S] {L.rgb, alpha}
     float *wxs = glds + 4 * S;                          // [NW][S] weight towards film x = q's + (o - H)
@@ -562,11 +572,10 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
     float *fv = wys + NW * S;                           // the discretised filter (32 values)
     const MtsgFilter &F = L.filter;
     const int b = F.border, bw = MTSG_BLOCK_SIZE + 2 * b;
-    const int tx = threadIdx.x & (GATHER_T - 1), ty = threadIdx.x / GATHER_T;
-    const int ox = gx0 + blockIdx.x * GATHER_T, oy = gy0 + blockIdx.y * GATHER_T;
-    const int gx = ox + tx, gy = oy + ty;
-    const bool live = gx < gx1 && gy < gy1;
-    // source s = image pixel (sx0 + s % SW, sy0 + s / SW): film position q + b = g + d, d in [-H, H]
+    const int tx = threadIdx.x & (GATHER_T - 1), tr = threadIdx.x / GATHER_T;   // output rows tr * R + i
+    const int ox = gx0 + blockIdx.x * GATHER_T, oy = gy0 + blockIdx.y * TY;
+    const int gx = ox + tx;
+    // source s = image pixel (sx0 + s % SWX, sy0 + s / SWX): film position q + b = g + d, d in [-H, H]
     const int sx0 = ox - b - H, sy0 = oy - b - H;
     for (int i = threadIdx.x; i <= MTSG_FILTER_RES; i += 256) fv[i] = F.values[i];
     long long pi[SLOTS];
@@ -574,20 +583,34 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
 #pragma unroll
     for (int k = 0; k < SLOTS; ++k) {
         const int s = threadIdx.x + 256 * k;
-        pi[k] = s < S ? pix_index(L, sx0 + s % SW, sy0 + s / SW) : -1;
+        pi[k] = s < S ? pix_index(L, sx0 + s % SWX, sy0 + s / SWX) : -1;
         rendered |= pi[k] >= 0;
     }
     // a tile none of whose sources this launch renders (another shard's part of the
     // window: with N-way tile sharding a rank renders every N-th tile column) keeps
     // its film values: the whole block leaves before the first barrier
     if (!__syncthreads_or(rendered)) return;
-    float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    float *dst = L.film_own + ((size_t)gy * L.fw + gx) * 5;
-    if (live) {
+    bool live[R];
+    float *dst[R];
+    f2v a01[R], a23[R];
+    float aw[R];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) acc[k] = dst[k];   // the previous chunks' running sums
+    for (int i = 0; i < R; ++i) {
+        const int gy = oy + tr * R + i;
+        live[i] = gx < gx1 && gy < gy1;
+        dst[i] = L.film_own + ((size_t)gy * L.fw + gx) * 5;
+        float acc[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        if (live[i]) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k) acc[k] = dst[i][k];   // the previous chunks' running sums
+        }
+        a01[i] = f2v{acc[0], acc[1]};
+        a23[i] = f2v{acc[2], acc[3]};
+        aw[i] = acc[4];
     }
-    f2v a01 = {acc[0], acc[1]}, a23 = {acc[2], acc[3]};
+    bool anyLive = false;
+#pragma unroll
+    for (int i = 0; i < R; ++i) anyLive |= live[i];
     const float4 *rec = reinterpret_cast<const float4 *>(L.contrib);
     for (uint32_t jj = 0; jj < L.chunk_spp; ++jj) {
         __syncthreads();   // the previous sample's neighbours are summed
@@ -604,7 +627,7 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
                 const float4 r = rec[2 * slot];
                 const float sy = rec[2 * slot + 1].x;
                 if (!signbit(sy)) {
-                    const int qx = sx0 + s % SW, qy = sy0 + s / SW;
+                    const int qx = sx0 + s % SWX, qy = sy0 + s / SWX;
                     const float sx = fabsf(r.w);
                     v = make_float4(r.x, r.y, r.z, signbit(r.w) ? 0.0f : 1.0f);
                     // film_splat's footprint in the block bitmap of q's 32x32 block
@@ -634,36 +657,44 @@ __global__ __launch_bounds__(256) void film_gather(MtsgLaunch L, int gx0, int gy
             }
         }
         __syncthreads();
-        if (live) {
-            // neighbour d = (dx, dy): source q at film position g + d; g sits at offset -d from it.
-            // The four value channels as two packed pairs (v_pk_mul_f32 + v_pk_add_f32: each half
-            // the IEEE product and sum of its own channel, one instruction for two)
+        if (anyLive) {
+            // source row rr of the thread's window (film rows tr * R - H .. tr * R + R - 1 + H):
+            // output i takes it as neighbour row dy = rr - i - H, so each output still adds its
+            // neighbours in row-major order.  neighbour d = (dx, dy): source q at film position
+            // g + d; g sits at offset -d from it.  The four value channels as two packed pairs
+            // (v_pk_mul_f32 + v_pk_add_f32: each half the IEEE product and sum of its own channel)
 #pragma unroll
-            for (int dy = -H; dy <= H; ++dy) {
+            for (int rr = 0; rr < 2 * H + R; ++rr) {
 #pragma unroll
                 for (int dx = -H; dx <= H; ++dx) {
-                    const int s = (ty + H + dy) * SW + (tx + H + dx);
-                    const float w = wxs[(H - dx) * S + s] * wys[(H - dy) * S + s];
+                    const int s = (tr * R + rr) * SWX + (tx + H + dx);
+                    const float wxv = wxs[(H - dx) * S + s];
                     const float4 v = val[s];
+#pragma unroll
+                    for (int i = 0; i < R; ++i) {
+                        const int dy = rr - i - H;
+                        if (dy < -H || dy > H) continue;
+                        const float w = wxv * wys[(H - dy) * S + s];
 #if MTSG_GATHER_PK
-                    const f2v ww = {w, w};
-                    a01 += ww * f2v{v.x, v.y};
-                    a23 += ww * f2v{v.z, v.w};
+                        const f2v ww = {w, w};
+                        a01[i] += ww * f2v{v.x, v.y};
+                        a23[i] += ww * f2v{v.z, v.w};
 #else
-                    a01.x += w * v.x;
-                    a01.y += w * v.y;
-                    a23.x += w * v.z;
-                    a23.y += w * v.w;
+                        a01[i].x += w * v.x;
+                        a01[i].y += w * v.y;
+                        a23[i].x += w * v.z;
+                        a23[i].y += w * v.w;
 #endif
-                    acc[4] += w * 1.0f;
+                        aw[i] += w * 1.0f;
+                    }
                 }
             }
         }
     }
-    if (live) {
-        acc[0] = a01.x; acc[1] = a01.y; acc[2] = a23.x; acc[3] = a23.y;
 #pragma unroll
-        for (int k = 0; k < 5; ++k) dst[k] = acc[k];
+    for (int i = 0; i < R; ++i) {
+        if (!live[i]) continue;
+        dst[i][0] = a01[i].x; dst[i][1] = a01[i].y; dst[i][2] = a23[i].x; dst[i][3] = a23[i].y; dst[i][4] = aw[i];
     }
 }
 
@@ -771,13 +802,14 @@ hipError_t mtsg_launch_reduce(const MtsgLaunch &L, hipStream_t stream) {
 }
 
 // gather mode: the film pixels the launch's samples can reach, [x0 + b - H, x0 + w + b + H)
-// x [y0 + b - H, y0 + h + b + H) clipped to the film, in 16x16 tiles
+// x [y0 + b - H, y0 + h + b + H) clipped to the film, in tiles of 16 x (16 * gather_rows(H))
 hipError_t mtsg_launch_gather(const MtsgLaunch &L, hipStream_t stream) {
     const int H = (int)L.gather_h, b = L.filter.border;
     const int gx0 = std::max(0, (int)L.x0 + b - H), gy0 = std::max(0, (int)L.y0 + b - H);
     const int gx1 = std::min(L.fw, (int)(L.x0 + L.width) + b + H), gy1 = std::min(L.fh, (int)(L.y0 + L.height) + b + H);
     if (gx1 <= gx0 || gy1 <= gy0) return hipSuccess;
-    const dim3 grid((gx1 - gx0 + GATHER_T - 1) / GATHER_T, (gy1 - gy0 + GATHER_T - 1) / GATHER_T);
+    const int ty = GATHER_T * gather_rows(H);
+    const dim3 grid((gx1 - gx0 + GATHER_T - 1) / GATHER_T, (gy1 - gy0 + ty - 1) / ty);
     const size_t lds = gather_lds_floats(H) * 4;
     switch (H) {
         case 1: hipLaunchKernelGGL(film_gather<1>, grid, dim3(256), lds, stream, L, gx0, gy0, gx1, gy1); break;
