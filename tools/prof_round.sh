@@ -11,6 +11,8 @@ OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
 mkdir -p $OUT
 export TMPDIR=/tmp
+# the 1/4-row SQ and stall passes run the full frame's sample-run length (tools/prof_run.py)
+export PROF_FULL_RUNS=1
 # the build these profiles describe (bench.py only trusts profiles of the library it times)
 sha256sum mitsuba0.6_amd/_build/libmtsgpu.so | cut -d' ' -f1 > $OUT/lib.sha256
 for cfg in ${CONFIGS:-C2 C3 C4 C5 C2g}; do
